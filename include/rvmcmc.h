@@ -1,0 +1,126 @@
+/*
+ * rvmcmc.h -- C ABI of librvmcmc.so, the MI355X (gfx950) radial-velocity MCMC hot path.
+ *
+ * The reference (MrSwordFish/rvel-mcmc, Python 2 + REBOUND) has no native interface of its own;
+ * its hot path is reached through three Python call sites, which this ABI replaces in batch:
+ *
+ *   reference call site                                   replaced by
+ *   ----------------------------------------------------  ----------------------------------------
+ *   state.py:103-110  State.get_logp(obs) -> float         rvm_logl_batch (W walkers per call)
+ *     (state.py:36-47 setup_sim, :61-73 get_rv,
+ *      :89-98 get_chi2, :299-315 priorHard, and
+ *      REBOUND sim.add/move_to_com/integrate/Encounter)
+ *   mcmc.py:28-35     lnprob(x, e) (emcee callback)         rvm_logl_batch
+ *   observations.py:6-69 Observation.{tf,tb,rvf,rvb,       rvm_plan_create (epoch schedule, obs data)
+ *     errorf,errorb,Npoints}
+ *   mcmc.py:57-65 Ensemble.step -> emcee 2.2.1 stretch     rvm_stretch_propose / rvm_stretch_accept
+ *     move (EnsembleSampler._propose_stretch)
+ *   mcmc.py:89-121 Mh.generate_proposal / Mh.step          rvm_mh_propose / rvm_mh_accept
+ *   mcmc.py:144-187 Smala.generate_proposal/step           rvm_fd_params (finite-difference stencil)
+ *                                                          + host-side metric
+ *
+ * Conventions
+ *   - All array pointers passed to launch functions are DEVICE pointers (hipMalloc / torch CUDA
+ *     tensors), caller-owned.  Launch functions never allocate, never synchronise, and are
+ *     stream-ordered on `stream` (a hipStream_t; NULL = the null stream), so they are capturable
+ *     into a hipGraph.  rvm_plan_create is the only call that allocates (device buffers owned by
+ *     the plan) and it synchronises once.
+ *   - Walker parameters are SoA, [n_params][n_walkers] float64, n_params = 5*n_planets, with the
+ *     canonical per-planet key order  m, a, h, k, l  (the Python layer maps a
+ *     State's dict order onto it).  Coplanar (ix = iy = 0) systems only in this ABI version.
+ *   - Return code: 0 = success, < 0 = argument / launch error (rvm_last_error() explains).
+ *     Per-walker physics outcomes are never errors: they are status codes plus logl = -INFINITY
+ *     (the reference raises rebound.Encounter / returns -inf from priorHard; mcmc.py:28-35 maps
+ *     every exception to -inf).
+ */
+#ifndef RVMCMC_H
+#define RVMCMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RVM_ABI_VERSION 1
+
+/* per-walker status codes (status_out) */
+#define RVM_STATUS_OK 0
+#define RVM_STATUS_PRIOR 1     /* State.priorHard() true (state.py:299-315) -> logl = -inf        */
+#define RVM_STATUS_ENCOUNTER 2 /* pair distance < exit_min_distance (REBOUND Encounter) -> -inf   */
+#define RVM_STATUS_NONFINITE 3 /* non-finite chi2 -> -inf                                          */
+
+#define RVM_MAX_PLANETS 4
+#define RVM_MAX_LEVELS 6
+
+/* Integrator configuration of a plan. */
+typedef struct {
+    int32_t n_planets;     /* 1..RVM_MAX_PLANETS                                                  */
+    double dt;             /* base (level-1) step in code units (yr/2pi); segments between epochs
+                              are cut into ceil(len/dt) equal steps                                */
+    int32_t n_levels;      /* Richardson levels, 1..RVM_MAX_LEVELS; level k runs (k+1)x the steps   */
+    double npoints_norm;   /* obs.Npoints: chi2 is divided by this (state.py:98), NOT the epoch count */
+} rvm_config;
+
+typedef struct rvm_plan rvm_plan;
+
+/* Build the epoch schedule for one observation set (host arrays, n_obs epochs in any order and
+ * sign; t = 0 is the initial condition).  Allocates device memory and workspace for up to
+ * max_walkers walkers per launch.  observations.py:6-69 (tf/tb/rvf/rvb/errorf/errorb). */
+int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, const double* sigma, int32_t n_obs,
+                    int32_t max_walkers, rvm_plan** out);
+void rvm_plan_destroy(rvm_plan* plan);
+/* schedule introspection: total level-1 steps per direction (fwd, bwd), epochs per direction */
+int rvm_plan_info(const rvm_plan* plan, int32_t* steps_fwd, int32_t* steps_bwd, int32_t* epochs_fwd,
+                  int32_t* epochs_bwd);
+
+/* logl_out[w] = -chi2/npoints_norm or -INF; status_out[w]; rv_out (nullable) = model RV
+ * [n_obs][n_walkers] in the plan's input epoch order.  hill_factor = State.hillRadiusFactor
+ * as the caller sees it (1.0 inside the reference samplers after deepcopy, state.py:212-213). */
+int rvm_logl_batch(const rvm_plan* plan, int32_t n_walkers, const double* params, double hill_factor,
+                   double* logl_out, int32_t* status_out, double* rv_out, void* stream);
+
+/* ---- samplers (device-side proposal / accept; counter-based Philox4x32-10 RNG) ------------------
+ * Draws are keyed by (seed, iteration, stream_id, global walker index), so results do not depend
+ * on how walkers are sharded across ranks.  Every launch takes optional `draws` (device, nullable):
+ * when non-NULL the documented uniforms/normals are read from it instead of Philox (tests inject
+ * the same draws into the oracle). */
+
+/* emcee 2.2.1 stretch move, half-step (S0 = walkers [s0_begin, s0_begin+n_s0) of the GLOBAL
+ * ensemble, complement S1 given as a device array [n_params][n_s1] of positions).
+ * propose: z = ((a-1)u1+1)^2/a, j = floor(u2*n_s1), q = c_j - z (c_j - x)
+ *   writes q_out [n_params][n_s0] and z_out [n_s0].  draws layout: [2][n_s0] (u1, u2).
+ * accept: lnpdiff = (n_params-1) ln z + lnp_new - lnp_old > ln(u3) -> x <- q, lnp <- lnp_new.
+ *   x, lnp: [n_params][n_s0], [n_s0] (in place).  accepted: int32 counters [n_s0] (+= 1).
+ *   draws layout: [n_s0] (u3). */
+int rvm_stretch_propose(int32_t n_params, int32_t n_s0, int64_t s0_begin, const double* x, int32_t n_s1,
+                        const double* c, double a, uint64_t seed, uint64_t iteration, uint32_t half,
+                        const double* draws, double* q_out, double* z_out, void* stream);
+int rvm_stretch_accept(int32_t n_params, int32_t n_s0, int64_t s0_begin, double* x, double* lnp, const double* q,
+                       const double* lnp_new, const double* z, uint64_t seed, uint64_t iteration, uint32_t half,
+                       const double* draws, int32_t* accepted, void* stream);
+
+/* Gaussian random-walk Metropolis-Hastings (mcmc.py:89-121), n_chains independent chains:
+ * propose: q = x + step_size * scales[p] * N(0,1)        draws layout: [n_params][n_chains]
+ * accept : exp(lnp_new - lnp_old) > u -> x <- q, lnp <- lnp_new   draws layout: [n_chains] */
+int rvm_mh_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, const double* x, const double* scales,
+                   double step_size, uint64_t seed, uint64_t iteration, const double* draws, double* q_out,
+                   void* stream);
+int rvm_mh_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, double* lnp, const double* q,
+                  const double* lnp_new, uint64_t seed, uint64_t iteration, const double* draws, int32_t* accepted,
+                  void* stream);
+
+/* Central finite-difference stencil for SMALA's gradient/metric: for each chain c and parameter p,
+ * out[(1 + 2p + s)*n_chains + c] (s = 0: +eps_p, 1: -eps_p) and out[0*n_chains + c] = x;
+ * eps_p = rel_step * max(|x_p|, floor[p]).  out layout: [(2P+1)] blocks of [n_params][n_chains]. */
+int rvm_fd_params(int32_t n_params, int32_t n_chains, const double* x, double rel_step, const double* floor_,
+                  double* out, void* stream);
+
+const char* rvm_last_error(void);
+int rvm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RVMCMC_H */

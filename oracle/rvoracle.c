@@ -1,0 +1,909 @@
+/*
+ * oracle/rvoracle.c -- CPU restatement of the reference's log-likelihood path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (rvel-mcmc_amd/) links, loads or calls
+ * this file; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg do, and
+ * only as the checker / the timed CPU baseline.
+ *
+ * What it restates (reference = /root/reference, Python 2 + REBOUND):
+ *   - state.py:36-47   State.setup_sim   star m=1, planets added with primary=star through
+ *                                         REBOUND's Pal (2009) elements, Hill radii, move_to_com,
+ *                                         exit_min_distance = hillRadiusFactor * max r_Hill
+ *   - state.py:61-73   State.get_rv      fresh simulation, integrate(t) for t in ARRAY ORDER,
+ *                                         record particles[0].vx
+ *   - state.py:89-98   State.get_chi2    sum (rv-obs)^2/sigma^2 over tf then tb, / obs.Npoints
+ *   - state.py:103-110 State.get_logp    priorHard -> -inf, else -chi2
+ *   - state.py:299-315 State.priorHard   a<=0.02, m<=5e-6, h^2+k^2>=1, ix^2+iy^2>=4
+ *   - REBOUND (third-party C, not vendored; ~v3.x, early 2017):
+ *       reb_tools_pal_to_particle (Pal 2009 -> Cartesian), reb_move_to_com,
+ *       the IAS15 integrator (Rein & Spiegel 2015, MNRAS 446, 1424) with REBOUND defaults
+ *       epsilon=1e-9, safety_factor=0.25, min_dt=0, epsilon_global=1, initial dt=0.001,
+ *       reb_integrate(tmax) with exact_finish_time=1, and the exit_min_distance encounter
+ *       check run after every step (raises rebound.Encounter).
+ *     The IAS15 constants are DERIVED (oracle/gen_ias15_consts.py), not transcribed.
+ *   Parity of this restatement is pinned by the reference's stored outputs:
+ *   G1 (Pal + COM vectors), G2 (logp of HD155358 `sol`), G3 (1000-point RV curve), G4.
+ *
+ * It also holds `rvo_wh_*`: a plain-C restatement of the SAME Wisdom-Holman algorithm the HIP
+ * kernel runs (Jacobi coordinates, DKD, epoch-aligned segments), used for the T1 parity tier
+ * (GPU vs CPU, same algorithm) and as the "port" CPU baseline.  It is written independently of
+ * the kernel source (no shared headers).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ias15_consts.h"
+
+#define RVO_MAXP 7
+#define RVO_MAXB (RVO_MAXP + 1)
+#define RVO_N3 (3 * RVO_MAXB)
+
+enum { RVO_OK = 0, RVO_PRIOR = 1, RVO_ENCOUNTER = 2, RVO_NONFINITE = 3 };
+
+/* ------------------------------------------------------------------------------------------ */
+/* Pal (2009) elements -> Cartesian, REBOUND `sim.add(primary=..., m, a, h, k, l[, ix, iy])`.  */
+/* k = e cos(varpi), h = e sin(varpi), l = mean longitude, (ix,iy) = 2 sin(i/2)(cos O, sin O) */
+/* SURVEY.md App. A.2 (pinned bit-level by G1).                                                */
+/* ------------------------------------------------------------------------------------------ */
+static void pal_to_cart(double mu, double a, double lam, double k, double h, double ix, double iy,
+                        double* pos, double* vel) {
+    /* Kepler's equation in eccentric longitude: lam = F - k sin F + h cos F (Newton from F=lam) */
+    double F = lam;
+    for (int it = 0; it < 100; it++) {
+        const double sF = sin(F), cF = cos(F);
+        const double fF = F - k * sF + h * cF - lam;
+        const double dF = 1.0 - k * cF - h * sF;
+        const double step = fF / dF;
+        F -= step;
+        if (fabs(step) <= 1e-16 * (fabs(F) > 1.0 ? fabs(F) : 1.0)) break;
+    }
+    const double sF = sin(F), cF = cos(F);
+    const double beta = 1.0 / (1.0 + sqrt(1.0 - h * h - k * k));
+    const double n = sqrt(mu / (a * a * a));
+    const double r = a * (1.0 - k * cF - h * sF);
+    const double X = a * ((1.0 - h * h * beta) * cF + h * k * beta * sF - k);
+    const double Y = a * ((1.0 - k * k * beta) * sF + h * k * beta * cF - h);
+    const double fac = n * a * a / r;
+    const double VX = fac * (h * k * beta * cF - (1.0 - h * h * beta) * sF);
+    const double VY = fac * ((1.0 - k * k * beta) * cF - h * k * beta * sF);
+    if (ix == 0.0 && iy == 0.0) {
+        pos[0] = X; pos[1] = Y; pos[2] = 0.0;
+        vel[0] = VX; vel[1] = VY; vel[2] = 0.0;
+        return;
+    }
+    /* rotate the orbital plane about the node line by i (Rodrigues), expressed in (ix, iy) */
+    const double W = sqrt(fabs(4.0 - ix * ix - iy * iy));
+    const double axx = 1.0 - 0.5 * iy * iy, axy = 0.5 * ix * iy;
+    const double ayy = 1.0 - 0.5 * ix * ix;
+    pos[0] = axx * X + axy * Y;
+    pos[1] = axy * X + ayy * Y;
+    pos[2] = 0.5 * W * (ix * Y - iy * X);
+    vel[0] = axx * VX + axy * VY;
+    vel[1] = axy * VX + ayy * VY;
+    vel[2] = 0.5 * W * (ix * VY - iy * VX);
+}
+
+/* planet parameter record used across the oracle ABI: m, a, h, k, l, ix, iy */
+#define RVO_PSTRIDE 7
+
+/* state.py:299-315 -- first failing condition wins, planets in order. */
+int rvo_prior_hard(int np, const double* pl, int has_hk, int has_inc) {
+    for (int i = 0; i < np; i++) {
+        const double* p = pl + RVO_PSTRIDE * i;
+        if (p[1] <= 0.02) return 1;
+        if (p[0] <= 5e-6) return 1;
+        if (has_hk && (p[2] * p[2] + p[3] * p[3] >= 1.0)) return 1;
+        if (has_inc && (p[5] * p[5] + p[6] * p[6] >= 4.0)) return 1;
+    }
+    return 0;
+}
+
+/* state.py:36-47: bodies (star first), barycentric after move_to_com; returns max Hill radius */
+static double setup_bodies(int np, const double* pl, double* m, double* x, double* v) {
+    double hill = 0.0;
+    m[0] = 1.0;
+    x[0] = x[1] = x[2] = 0.0;
+    v[0] = v[1] = v[2] = 0.0;
+    for (int i = 0; i < np; i++) {
+        const double* p = pl + RVO_PSTRIDE * i;
+        const int b = i + 1;
+        m[b] = p[0];
+        /* G = 1; primary = the star particle (m = 1, at rest at the origin) */
+        pal_to_cart(1.0 * (m[0] + p[0]), p[1], p[4], p[3], p[2], p[5], p[6], x + 3 * b, v + 3 * b);
+        const double rh = p[1] * pow(p[0] / (3.0 * m[0]), 1.0 / 3.0);
+        if (rh > hill) hill = rh;
+    }
+    /* reb_move_to_com */
+    const int nb = np + 1;
+    double M = 0, cx[3] = {0, 0, 0}, cv[3] = {0, 0, 0};
+    for (int b = 0; b < nb; b++) {
+        M += m[b];
+        for (int c = 0; c < 3; c++) {
+            cx[c] += m[b] * x[3 * b + c];
+            cv[c] += m[b] * v[3 * b + c];
+        }
+    }
+    for (int c = 0; c < 3; c++) { cx[c] /= M; cv[c] /= M; }
+    for (int b = 0; b < nb; b++)
+        for (int c = 0; c < 3; c++) {
+            x[3 * b + c] -= cx[c];
+            v[3 * b + c] -= cv[c];
+        }
+    return hill;
+}
+
+/* Expose setup for the G1 fixture: heliocentric (before COM) and barycentric (after) vectors. */
+void rvo_setup_vectors(int np, const double* pl, double* helio_xv, double* bary_xv) {
+    double m[RVO_MAXB], x[RVO_N3], v[RVO_N3];
+    for (int i = 0; i < np; i++) {
+        const double* p = pl + RVO_PSTRIDE * i;
+        double px[3], pv[3];
+        pal_to_cart(1.0 + p[0], p[1], p[4], p[3], p[2], p[5], p[6], px, pv);
+        for (int c = 0; c < 3; c++) {
+            helio_xv[6 * (i + 1) + c] = px[c];
+            helio_xv[6 * (i + 1) + 3 + c] = pv[c];
+        }
+    }
+    for (int c = 0; c < 6; c++) helio_xv[c] = 0.0;
+    setup_bodies(np, pl, m, x, v);
+    for (int b = 0; b <= np; b++)
+        for (int c = 0; c < 3; c++) {
+            bary_xv[6 * b + c] = x[3 * b + c];
+            bary_xv[6 * b + 3 + c] = v[3 * b + c];
+        }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* IAS15 (REBOUND default integrator), restated.                                               */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    int N;                  /* bodies */
+    double t, dt, dt_last_done, dt_last_success;
+    double m[RVO_MAXB];
+    double x[RVO_N3], v[RVO_N3], a[RVO_N3];
+    double x0[RVO_N3], v0[RVO_N3], a0[RVO_N3], at[RVO_N3];
+    double csx[RVO_N3], csv[RVO_N3];
+    double g[7][RVO_N3], b[7][RVO_N3], e[7][RVO_N3], br[7][RVO_N3], er[7][RVO_N3];
+    double exit_min_distance;
+    double epsilon, safety_factor, min_dt;
+    long nsteps, nrejected;
+} ias_sim;
+
+static void gravity(const ias_sim* s, const double* x, double* acc) {
+    const int N = s->N;
+    for (int k = 0; k < 3 * N; k++) acc[k] = 0.0;
+    for (int i = 0; i < N; i++) {
+        for (int j = i + 1; j < N; j++) {
+            const double dx = x[3 * i] - x[3 * j];
+            const double dy = x[3 * i + 1] - x[3 * j + 1];
+            const double dz = x[3 * i + 2] - x[3 * j + 2];
+            const double r2 = dx * dx + dy * dy + dz * dz;
+            const double r = sqrt(r2);
+            const double pf = 1.0 / (r2 * r); /* G = 1 */
+            const double pfj = -pf * s->m[j];
+            const double pfi = pf * s->m[i];
+            acc[3 * i] += pfj * dx;
+            acc[3 * i + 1] += pfj * dy;
+            acc[3 * i + 2] += pfj * dz;
+            acc[3 * j] += pfi * dx;
+            acc[3 * j + 1] += pfi * dy;
+            acc[3 * j + 2] += pfi * dz;
+        }
+    }
+}
+
+static inline void add_cs(double* p, double* csp, double inp) {
+    const double y = inp - *csp;
+    const double t = *p + y;
+    *csp = (t - *p) - y;
+    *p = t;
+}
+
+static void ias_predict_next_step(double ratio, int N3, double (*e_in)[RVO_N3], double (*b_in)[RVO_N3],
+                                  double (*e)[RVO_N3], double (*b)[RVO_N3]) {
+    if (ratio > 20.0) {
+        for (int j = 0; j < 7; j++)
+            for (int k = 0; k < N3; k++) { e[j][k] = 0.0; b[j][k] = 0.0; }
+        return;
+    }
+    const double q1 = ratio, q2 = q1 * q1, q3 = q1 * q2, q4 = q2 * q2, q5 = q2 * q3, q6 = q3 * q3,
+                 q7 = q3 * q4;
+    for (int k = 0; k < N3; k++) {
+        double be[7];
+        for (int j = 0; j < 7; j++) be[j] = b_in[j][k] - e_in[j][k];
+        const double B0 = b_in[0][k], B1 = b_in[1][k], B2 = b_in[2][k], B3 = b_in[3][k], B4 = b_in[4][k],
+                     B5 = b_in[5][k], B6 = b_in[6][k];
+        e[0][k] = q1 * (B6 * 7.0 + B5 * 6.0 + B4 * 5.0 + B3 * 4.0 + B2 * 3.0 + B1 * 2.0 + B0);
+        e[1][k] = q2 * (B6 * 21.0 + B5 * 15.0 + B4 * 10.0 + B3 * 6.0 + B2 * 3.0 + B1);
+        e[2][k] = q3 * (B6 * 35.0 + B5 * 20.0 + B4 * 10.0 + B3 * 4.0 + B2);
+        e[3][k] = q4 * (B6 * 35.0 + B5 * 15.0 + B4 * 5.0 + B3);
+        e[4][k] = q5 * (B6 * 21.0 + B5 * 6.0 + B4);
+        e[5][k] = q6 * (B6 * 7.0 + B5);
+        e[6][k] = q7 * B6;
+        for (int j = 0; j < 7; j++) b[j][k] = e[j][k] + be[j];
+    }
+}
+
+/* one IAS15 step attempt; returns 1 if accepted, 0 if rejected (dt shrunk, state restored) */
+static int ias_step_try(ias_sim* s) {
+    const int N3 = 3 * s->N;
+    const double* h = IAS15_H;
+    const double* rr = IAS15_RR;
+    const double* c = IAS15_C;
+    const double* d = IAS15_D;
+    double (*g)[RVO_N3] = s->g;
+    double (*b)[RVO_N3] = s->b;
+
+    for (int k = 0; k < N3; k++) {
+        s->x0[k] = s->x[k];
+        s->v0[k] = s->v[k];
+        s->a0[k] = s->a[k];
+    }
+    for (int k = 0; k < N3; k++) {
+        g[0][k] = b[6][k] * d[15] + b[5][k] * d[10] + b[4][k] * d[6] + b[3][k] * d[3] + b[2][k] * d[1] +
+                  b[1][k] * d[0] + b[0][k];
+        g[1][k] = b[6][k] * d[16] + b[5][k] * d[11] + b[4][k] * d[7] + b[3][k] * d[4] + b[2][k] * d[2] + b[1][k];
+        g[2][k] = b[6][k] * d[17] + b[5][k] * d[12] + b[4][k] * d[8] + b[3][k] * d[5] + b[2][k];
+        g[3][k] = b[6][k] * d[18] + b[5][k] * d[13] + b[4][k] * d[9] + b[3][k];
+        g[4][k] = b[6][k] * d[19] + b[5][k] * d[14] + b[4][k];
+        g[5][k] = b[6][k] * d[20] + b[5][k];
+        g[6][k] = b[6][k];
+    }
+    const double dt = s->dt;
+    double pc_err = 1e300, pc_err_last = 2.0;
+    int iterations = 0;
+    double xp[RVO_N3];
+    while (1) {
+        if (pc_err < 1e-16) break;
+        if (iterations > 2 && pc_err_last <= pc_err) break;
+        if (iterations >= 12) break; /* REBOUND warns: predictor-corrector did not converge */
+        pc_err_last = pc_err;
+        pc_err = 0.0;
+        iterations++;
+        for (int n = 1; n < 8; n++) {
+            double sx[9];
+            sx[0] = dt * h[n];
+            sx[1] = sx[0] * sx[0] / 2.0;
+            sx[2] = sx[1] * h[n] / 3.0;
+            sx[3] = sx[2] * h[n] / 2.0;
+            sx[4] = 3.0 * sx[3] * h[n] / 5.0;
+            sx[5] = 2.0 * sx[4] * h[n] / 3.0;
+            sx[6] = 5.0 * sx[5] * h[n] / 7.0;
+            sx[7] = 3.0 * sx[6] * h[n] / 4.0;
+            sx[8] = 7.0 * sx[7] * h[n] / 9.0;
+            for (int k = 0; k < N3; k++) {
+                xp[k] = -s->csx[k] + ((sx[8] * b[6][k] + sx[7] * b[5][k] + sx[6] * b[4][k] + sx[5] * b[3][k] +
+                                       sx[4] * b[2][k] + sx[3] * b[1][k] + sx[2] * b[0][k] + sx[1] * s->a0[k] +
+                                       sx[0] * s->v0[k]) +
+                                      s->x0[k]);
+            }
+            gravity(s, xp, s->at);
+            double maxak = 0.0, maxb6ktmp = 0.0;
+            for (int k = 0; k < N3; k++) {
+                const double gk = s->at[k] - s->a0[k];
+                double tmp;
+                switch (n) {
+                    case 1:
+                        tmp = g[0][k];
+                        g[0][k] = gk / rr[0];
+                        b[0][k] += g[0][k] - tmp;
+                        break;
+                    case 2:
+                        tmp = g[1][k];
+                        g[1][k] = (gk / rr[1] - g[0][k]) / rr[2];
+                        tmp = g[1][k] - tmp;
+                        b[0][k] += tmp * c[0];
+                        b[1][k] += tmp;
+                        break;
+                    case 3:
+                        tmp = g[2][k];
+                        g[2][k] = ((gk / rr[3] - g[0][k]) / rr[4] - g[1][k]) / rr[5];
+                        tmp = g[2][k] - tmp;
+                        b[0][k] += tmp * c[1];
+                        b[1][k] += tmp * c[2];
+                        b[2][k] += tmp;
+                        break;
+                    case 4:
+                        tmp = g[3][k];
+                        g[3][k] = (((gk / rr[6] - g[0][k]) / rr[7] - g[1][k]) / rr[8] - g[2][k]) / rr[9];
+                        tmp = g[3][k] - tmp;
+                        b[0][k] += tmp * c[3];
+                        b[1][k] += tmp * c[4];
+                        b[2][k] += tmp * c[5];
+                        b[3][k] += tmp;
+                        break;
+                    case 5:
+                        tmp = g[4][k];
+                        g[4][k] = ((((gk / rr[10] - g[0][k]) / rr[11] - g[1][k]) / rr[12] - g[2][k]) / rr[13] -
+                                   g[3][k]) /
+                                  rr[14];
+                        tmp = g[4][k] - tmp;
+                        b[0][k] += tmp * c[6];
+                        b[1][k] += tmp * c[7];
+                        b[2][k] += tmp * c[8];
+                        b[3][k] += tmp * c[9];
+                        b[4][k] += tmp;
+                        break;
+                    case 6:
+                        tmp = g[5][k];
+                        g[5][k] = (((((gk / rr[15] - g[0][k]) / rr[16] - g[1][k]) / rr[17] - g[2][k]) / rr[18] -
+                                    g[3][k]) /
+                                       rr[19] -
+                                   g[4][k]) /
+                                  rr[20];
+                        tmp = g[5][k] - tmp;
+                        b[0][k] += tmp * c[10];
+                        b[1][k] += tmp * c[11];
+                        b[2][k] += tmp * c[12];
+                        b[3][k] += tmp * c[13];
+                        b[4][k] += tmp * c[14];
+                        b[5][k] += tmp;
+                        break;
+                    case 7: {
+                        tmp = g[6][k];
+                        g[6][k] = ((((((gk / rr[21] - g[0][k]) / rr[22] - g[1][k]) / rr[23] - g[2][k]) / rr[24] -
+                                     g[3][k]) /
+                                        rr[25] -
+                                    g[4][k]) /
+                                       rr[26] -
+                                   g[5][k]) /
+                                  rr[27];
+                        tmp = g[6][k] - tmp;
+                        b[0][k] += tmp * c[15];
+                        b[1][k] += tmp * c[16];
+                        b[2][k] += tmp * c[17];
+                        b[3][k] += tmp * c[18];
+                        b[4][k] += tmp * c[19];
+                        b[5][k] += tmp * c[20];
+                        b[6][k] += tmp;
+                        const double ak = fabs(s->at[k]);
+                        if (isnormal(ak) && ak > maxak) maxak = ak;
+                        const double b6ktmp = fabs(tmp);
+                        if (isnormal(b6ktmp) && b6ktmp > maxb6ktmp) maxb6ktmp = b6ktmp;
+                    } break;
+                }
+            }
+            if (n == 7) pc_err = maxb6ktmp / maxak;
+        }
+    }
+
+    /* new timestep (epsilon_global = 1) */
+    const double dt_done = dt;
+    if (s->epsilon > 0.0) {
+        double maxak = 0.0, maxb6k = 0.0;
+        for (int k = 0; k < N3; k++) {
+            const double ak = fabs(s->at[k]);
+            if (isnormal(ak) && ak > maxak) maxak = ak;
+            const double b6k = fabs(b[6][k]);
+            if (isnormal(b6k) && b6k > maxb6k) maxb6k = b6k;
+        }
+        const double integrator_error = maxb6k / maxak;
+        double dt_new;
+        if (isnormal(integrator_error)) {
+            dt_new = pow(s->epsilon / integrator_error, 1.0 / 7.0) * dt_done;
+        } else {
+            dt_new = dt_done / s->safety_factor;
+        }
+        if (fabs(dt_new) < s->min_dt) dt_new = copysign(s->min_dt, dt_new);
+        if (fabs(dt_new / dt_done) < s->safety_factor) {
+            for (int k = 0; k < N3; k++) {
+                s->x[k] = s->x0[k];
+                s->v[k] = s->v0[k];
+            }
+            s->dt = dt_new;
+            if (s->dt_last_success != 0.0) {
+                const double ratio = s->dt / s->dt_last_success;
+                ias_predict_next_step(ratio, N3, s->er, s->br, s->e, s->b);
+            }
+            s->nrejected++;
+            return 0;
+        }
+        if (fabs(dt_new / dt_done) > 1.0 / s->safety_factor) dt_new = dt_done / s->safety_factor;
+        s->dt = dt_new;
+    }
+
+    /* advance to the end of the step (compensated summation) */
+    for (int k = 0; k < N3; k++) {
+        const double dx = ((((((((b[6][k] * 7.0 / 9.0 + b[5][k]) * 3.0 / 4.0 + b[4][k]) * 5.0 / 7.0 + b[3][k]) *
+                                   2.0 / 3.0 +
+                               b[2][k]) *
+                                  3.0 / 5.0 +
+                              b[1][k]) /
+                                 2.0 +
+                             b[0][k]) /
+                                3.0 +
+                            s->a0[k]) *
+                               dt_done / 2.0 +
+                           s->v0[k]) *
+                          dt_done;
+        add_cs(&s->x0[k], &s->csx[k], dx);
+        const double dv = (((((((b[6][k] * 7.0 / 8.0 + b[5][k]) * 6.0 / 7.0 + b[4][k]) * 5.0 / 6.0 + b[3][k]) *
+                                  4.0 / 5.0 +
+                              b[2][k]) *
+                                 3.0 / 4.0 +
+                             b[1][k]) *
+                                2.0 / 3.0 +
+                            b[0][k]) /
+                               2.0 +
+                           s->a0[k]) *
+                          dt_done;
+        add_cs(&s->v0[k], &s->csv[k], dv);
+        s->x[k] = s->x0[k];
+        s->v[k] = s->v0[k];
+    }
+    s->t += dt_done;
+    s->dt_last_done = dt_done;
+    s->dt_last_success = dt_done;
+    for (int j = 0; j < 7; j++)
+        for (int k = 0; k < N3; k++) {
+            s->er[j][k] = s->e[j][k];
+            s->br[j][k] = s->b[j][k];
+        }
+    const double ratio = s->dt / dt_done;
+    ias_predict_next_step(ratio, N3, s->e, s->b, s->e, s->b);
+    s->nsteps++;
+    return 1;
+}
+
+static void ias_step(ias_sim* s) {
+    gravity(s, s->x, s->a); /* reb_update_acceleration before integrator part2 */
+    while (!ias_step_try(s)) {
+    }
+}
+
+static int encounter(const ias_sim* s) {
+    if (!(s->exit_min_distance > 0.0)) return 0;
+    const double min2 = s->exit_min_distance * s->exit_min_distance;
+    for (int i = 0; i < s->N; i++)
+        for (int j = 0; j < i; j++) {
+            const double dx = s->x[3 * i] - s->x[3 * j];
+            const double dy = s->x[3 * i + 1] - s->x[3 * j + 1];
+            const double dz = s->x[3 * i + 2] - s->x[3 * j + 2];
+            if (dx * dx + dy * dy + dz * dz < min2) return 1;
+        }
+    return 0;
+}
+
+/* reb_integrate(tmax) with exact_finish_time = 1. Returns 0 or RVO_ENCOUNTER. */
+static int ias_integrate(ias_sim* s, double tmax) {
+    if (encounter(s)) return RVO_ENCOUNTER;
+    if (s->t == tmax) return 0;
+    if (s->dt * (tmax - s->t) < 0.0) s->dt = -s->dt;
+    const double dtsign = s->dt >= 0.0 ? 1.0 : -1.0;
+    double last_full_dt = s->dt;
+    s->dt_last_done = 0.0;
+    while (1) {
+        int last = 0;
+        if ((s->t + s->dt) * dtsign >= tmax * dtsign) {
+            if (s->t == tmax) break;
+            last = 1;
+            if (s->dt_last_done != 0.0) last_full_dt = s->dt_last_done;
+            s->dt = tmax - s->t;
+        }
+        const double want = s->dt;
+        ias_step(s);
+        if (encounter(s)) {
+            s->dt = last_full_dt;
+            return RVO_ENCOUNTER;
+        }
+        if (last && s->dt_last_done == want) {
+            s->t = tmax;
+            break;
+        }
+        if (!isfinite(s->t)) return RVO_NONFINITE;
+    }
+    s->dt = last_full_dt;
+    return 0;
+}
+
+static void ias_init(ias_sim* s, int np, const double* pl, double hill_factor) {
+    memset(s, 0, sizeof(*s));
+    s->N = np + 1;
+    const double hill = setup_bodies(np, pl, s->m, s->x, s->v);
+    s->exit_min_distance = hill_factor * hill;
+    s->dt = 0.001;
+    s->epsilon = 1e-9;
+    s->safety_factor = 0.25;
+    s->min_dt = 0.0;
+}
+
+/* state.py:61-73 -- one fresh simulation, integrate to each time IN ARRAY ORDER, star vx. */
+int rvo_get_rv_ias15(int np, const double* pl, double hill_factor, const double* times, int n, double* rv,
+                     long* nsteps) {
+    ias_sim* s = (ias_sim*)malloc(sizeof(ias_sim));
+    ias_init(s, np, pl, hill_factor);
+    int st = 0;
+    for (int i = 0; i < n; i++) {
+        st = ias_integrate(s, times[i]);
+        if (st) break;
+        rv[i] = s->v[0];
+    }
+    if (nsteps) *nsteps = s->nsteps;
+    free(s);
+    return st;
+}
+
+/* state.py:89-110 + priorHard.  Returns status; *logl = -chi2/npoints or -inf. */
+int rvo_logl_ias15(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* tf,
+                   const double* rvf, const double* ef, int nf, const double* tb, const double* rvb,
+                   const double* eb, int nb, double npoints, double* logl) {
+    if (rvo_prior_hard(np, pl, has_hk, has_inc)) {
+        *logl = -INFINITY;
+        return RVO_PRIOR;
+    }
+    double* rv = (double*)malloc(sizeof(double) * (size_t)(nf > nb ? nf : nb) + 8);
+    double chi2f = 0.0, chi2b = 0.0;
+    int st = rvo_get_rv_ias15(np, pl, hill_factor, tf, nf, rv, NULL);
+    if (!st) {
+        for (int i = 0; i < nf; i++) chi2f += ((rv[i] - rvf[i]) * (rv[i] - rvf[i])) / (ef[i] * ef[i]);
+        st = rvo_get_rv_ias15(np, pl, hill_factor, tb, nb, rv, NULL);
+    }
+    if (!st) {
+        for (int i = 0; i < nb; i++) chi2b += ((rv[i] - rvb[i]) * (rv[i] - rvb[i])) / (eb[i] * eb[i]);
+    }
+    free(rv);
+    if (st) {
+        *logl = -INFINITY;
+        return st;
+    }
+    const double lp = -((chi2b + chi2f) / npoints);
+    if (!isfinite(lp)) {
+        *logl = -INFINITY;
+        return RVO_NONFINITE;
+    }
+    *logl = lp;
+    return RVO_OK;
+}
+
+/* batch helper: W walkers, params [W][np][7] */
+void rvo_logl_ias15_batch(int W, int np, const double* pl, int has_hk, int has_inc, double hill_factor,
+                          const double* tf, const double* rvf, const double* ef, int nf, const double* tb,
+                          const double* rvb, const double* eb, int nb, double npoints, double* logl, int32_t* status) {
+    for (int w = 0; w < W; w++) {
+        status[w] = rvo_logl_ias15(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, tf, rvf, ef,
+                                   nf, tb, rvb, eb, nb, npoints, logl + w);
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Wisdom-Holman (WHFast-style) restatement of the HIP kernel's algorithm (T1 tier).           */
+/*   Jacobi coordinates, Kepler drift (universal variables, Danby Stumpff functions),          */
+/*   interaction kick, DKD, epoch-aligned segments: the segment between consecutive epochs     */
+/*   (outward from t=0) of length D is cut into n = max(1, ceil(D/h - 1e-9)) equal steps,     */
+/*   each step D(h/2) K(h) D(h/2) with interior half-drifts merged.                            */
+/*   Epochs with t>=0 are visited ascending from 0, t<0 descending from 0.                     */
+/* ------------------------------------------------------------------------------------------ */
+static void stumpff(double z, double* c0, double* c1, double* c2, double* c3) {
+    int n = 0;
+    while (fabs(z) > 0.1) {
+        z *= 0.25;
+        n++;
+    }
+    /* c2 = 1/2! - z/4! + z^2/6! ..., c3 = 1/3! - z/5! + ... */
+    double s2 = 0.0, s3 = 0.0;
+    {
+        /* Horner from high order */
+        const double f2[9] = {1.0 / 2, 1.0 / 24, 1.0 / 720, 1.0 / 40320, 1.0 / 3628800, 1.0 / 479001600,
+                              1.0 / 87178291200.0, 1.0 / 20922789888000.0, 1.0 / 6402373705728000.0};
+        const double f3[9] = {1.0 / 6, 1.0 / 120, 1.0 / 5040, 1.0 / 362880, 1.0 / 39916800, 1.0 / 6227020800.0,
+                              1.0 / 1307674368000.0, 1.0 / 355687428096000.0, 1.0 / 121645100408832000.0};
+        for (int j = 8; j >= 0; j--) {
+            s2 = f2[j] - z * s2;
+            s3 = f3[j] - z * s3;
+        }
+    }
+    double C2 = s2, C3 = s3;
+    double C1 = 1.0 - z * C3;
+    double C0 = 1.0 - z * C2;
+    for (; n > 0; n--) {
+        z *= 4.0;
+        C3 = (C2 + C0 * C3) * 0.25;
+        C2 = C1 * C1 * 0.5;
+        C1 = C0 * C1;
+        C0 = 2.0 * C0 * C0 - 1.0;
+    }
+    *c0 = C0;
+    *c1 = C1;
+    *c2 = C2;
+    *c3 = C3;
+}
+
+/* universal-variable Kepler drift of (r, v) about mass GM by dt; returns 0 ok, 1 no convergence */
+static int kepler_drift(double GM, double* r, double* v, double dt) {
+    const double r0 = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    const double v2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+    const double eta0 = r[0] * v[0] + r[1] * v[1] + r[2] * v[2];
+    const double beta = 2.0 * GM / r0 - v2;
+    const double zeta0 = GM - beta * r0;
+    double X = dt / r0 - dt * dt * eta0 / (2.0 * r0 * r0 * r0);
+    double c0, c1, c2, c3, G1 = 0, G2 = 0, G3 = 0, rr = r0;
+    int ok = 0;
+    for (int it = 0; it < 50; it++) {
+        stumpff(beta * X * X, &c0, &c1, &c2, &c3);
+        G1 = X * c1;
+        G2 = X * X * c2;
+        G3 = X * X * X * c3;
+        const double G0 = c0;
+        const double f = r0 * G1 + eta0 * G2 + GM * G3 - dt;
+        rr = r0 * G0 + eta0 * G1 + GM * G2;
+        const double fpp = eta0 * G0 + zeta0 * G1;
+        /* Halley */
+        const double dX = f * rr / (rr * rr - 0.5 * f * fpp);
+        X -= dX;
+        if (fabs(dX) <= 2e-16 * fabs(X) || dX == 0.0) {
+            ok = 1;
+            break;
+        }
+    }
+    stumpff(beta * X * X, &c0, &c1, &c2, &c3);
+    G1 = X * c1;
+    G2 = X * X * c2;
+    G3 = X * X * X * c3;
+    rr = r0 * c0 + eta0 * G1 + GM * G2;
+    const double f = 1.0 - GM * G2 / r0;
+    const double g = dt - GM * G3;
+    const double fd = -GM * G1 / (rr * r0);
+    const double gd = 1.0 - GM * G2 / rr;
+    for (int c = 0; c < 3; c++) {
+        const double rn = f * r[c] + g * v[c];
+        const double vn = fd * r[c] + gd * v[c];
+        r[c] = rn;
+        v[c] = vn;
+    }
+    return ok ? 0 : 1;
+}
+
+typedef struct {
+    int np;
+    double m[RVO_MAXB];  /* m[0] = star */
+    double Mi[RVO_MAXB]; /* interior masses M_i = sum_{j<=i} m_j */
+    double r[RVO_MAXB][3], v[RVO_MAXB][3]; /* Jacobi coordinates, index 1..np */
+    double dmin2;
+    int enc;
+} wh_state;
+
+static void wh_init(wh_state* s, int np, const double* pl, double hill_factor) {
+    memset(s, 0, sizeof(*s));
+    s->np = np;
+    s->m[0] = 1.0;
+    s->Mi[0] = 1.0;
+    double helio_x[RVO_MAXB][3], helio_v[RVO_MAXB][3];
+    double hill = 0.0;
+    for (int i = 1; i <= np; i++) {
+        const double* p = pl + RVO_PSTRIDE * (i - 1);
+        s->m[i] = p[0];
+        s->Mi[i] = s->Mi[i - 1] + p[0];
+        pal_to_cart(1.0 + p[0], p[1], p[4], p[3], p[2], p[5], p[6], helio_x[i], helio_v[i]);
+        const double rh = p[1] * pow(p[0] / 3.0, 1.0 / 3.0);
+        if (rh > hill) hill = rh;
+    }
+    s->dmin2 = (hill_factor * hill) * (hill_factor * hill);
+    /* heliocentric -> Jacobi: r'_i = x_i - (sum_{1<=j<i} m_j x_j)/M_{i-1}  (star at origin) */
+    double sx[3] = {0, 0, 0}, sv[3] = {0, 0, 0};
+    for (int i = 1; i <= np; i++) {
+        for (int c = 0; c < 3; c++) {
+            s->r[i][c] = helio_x[i][c] - sx[c] / s->Mi[i - 1];
+            s->v[i][c] = helio_v[i][c] - sv[c] / s->Mi[i - 1];
+        }
+        for (int c = 0; c < 3; c++) {
+            sx[c] += s->m[i] * helio_x[i][c];
+            sv[c] += s->m[i] * helio_v[i][c];
+        }
+    }
+}
+
+static double wh_star_vx(const wh_state* s) {
+    double vx = 0.0;
+    for (int i = 1; i <= s->np; i++) vx -= (s->m[i] / s->Mi[i]) * s->v[i][0];
+    return vx;
+}
+
+static int wh_drift(wh_state* s, double h) {
+    int bad = 0;
+    for (int i = 1; i <= s->np; i++) bad |= kepler_drift(s->Mi[i], s->r[i], s->v[i], h);
+    return bad;
+}
+
+static void wh_kick(wh_state* s, double h) {
+    const int np = s->np;
+    double x[RVO_MAXB][3]; /* heliocentric positions, star at origin */
+    double acc[RVO_MAXB][3];
+    double cm[3] = {0, 0, 0};
+    x[0][0] = x[0][1] = x[0][2] = 0.0;
+    for (int i = 1; i <= np; i++) {
+        for (int c = 0; c < 3; c++) x[i][c] = s->r[i][c] + cm[c] / s->Mi[i - 1];
+        for (int c = 0; c < 3; c++) cm[c] += s->m[i] * x[i][c];
+    }
+    for (int i = 0; i <= np; i++) acc[i][0] = acc[i][1] = acc[i][2] = 0.0;
+    for (int i = 0; i <= np; i++)
+        for (int j = i + 1; j <= np; j++) {
+            const double dx = x[j][0] - x[i][0], dy = x[j][1] - x[i][1], dz = x[j][2] - x[i][2];
+            const double r2 = dx * dx + dy * dy + dz * dz;
+            if (r2 < s->dmin2) s->enc = 1;
+            const double ir3 = 1.0 / (r2 * sqrt(r2));
+            acc[i][0] += s->m[j] * ir3 * dx;
+            acc[i][1] += s->m[j] * ir3 * dy;
+            acc[i][2] += s->m[j] * ir3 * dz;
+            acc[j][0] -= s->m[i] * ir3 * dx;
+            acc[j][1] -= s->m[i] * ir3 * dy;
+            acc[j][2] -= s->m[i] * ir3 * dz;
+        }
+    double ma[3] = {s->m[0] * acc[0][0], s->m[0] * acc[0][1], s->m[0] * acc[0][2]};
+    for (int i = 1; i <= np; i++) {
+        const double* r = s->r[i];
+        const double rj2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+        const double kep = s->Mi[i] / (rj2 * sqrt(rj2));
+        for (int c = 0; c < 3; c++) {
+            const double aj = acc[i][c] - ma[c] / s->Mi[i - 1];
+            s->v[i][c] += h * (aj + kep * r[c]);
+        }
+        for (int c = 0; c < 3; c++) ma[c] += s->m[i] * acc[i][c];
+    }
+}
+
+/* Integrate one direction.  eps_abs[]: |t| of the epochs, ascending; sign = +1 or -1.
+ * h_target > 0: nominal step.  Writes rv[i].  Returns status. */
+static int wh_direction(int np, const double* pl, double hill_factor, const double* abs_t, int n, double sign,
+                        double h_target, int sub, double* rv) {
+    wh_state s;
+    wh_init(&s, np, pl, hill_factor);
+    {
+        /* initial encounter check (REBOUND heartbeat before the first step) */
+        wh_state tmp = s;
+        wh_kick(&tmp, 0.0);
+        if (tmp.enc) return RVO_ENCOUNTER;
+    }
+    double tprev = 0.0;
+    for (int i = 0; i < n; i++) {
+        const double D = abs_t[i] - tprev;
+        tprev = abs_t[i];
+        int ns = (D > 0.0) ? (int)ceil(D / h_target - 1e-9) : 0;
+        if (D > 0.0 && ns < 1) ns = 1;
+        ns *= sub;
+        if (ns > 0) {
+            const double h = sign * D / ns;
+            wh_drift(&s, 0.5 * h);
+            for (int j = 0; j < ns; j++) {
+                wh_kick(&s, h);
+                wh_drift(&s, (j == ns - 1) ? 0.5 * h : h);
+            }
+        }
+        if (s.enc) return RVO_ENCOUNTER;
+        rv[i] = wh_star_vx(&s);
+        if (!isfinite(rv[i])) return RVO_NONFINITE;
+    }
+    return RVO_OK;
+}
+
+/* RV at arbitrary epochs (any order/sign) with the WH algorithm; `sub` multiplies step counts.
+ * order: scratch int[n].  Returns status. */
+int rvo_wh_rv(int np, const double* pl, double hill_factor, const double* t, int n, double h_target, int sub,
+              double* rv) {
+    /* split by sign, sort by |t| */
+    int* idx = (int*)malloc(sizeof(int) * (size_t)(n + 1));
+    double* at = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+    double* out = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+    int st = RVO_OK;
+    for (int dir = 0; dir < 2 && st == RVO_OK; dir++) {
+        int cnt = 0;
+        for (int i = 0; i < n; i++) {
+            const int fwd = t[i] >= 0.0;
+            if ((dir == 0) == fwd) idx[cnt++] = i;
+        }
+        /* insertion sort by |t| (stable) */
+        for (int a = 1; a < cnt; a++) {
+            const int key = idx[a];
+            int b = a - 1;
+            while (b >= 0 && fabs(t[idx[b]]) > fabs(t[key])) {
+                idx[b + 1] = idx[b];
+                b--;
+            }
+            idx[b + 1] = key;
+        }
+        for (int a = 0; a < cnt; a++) at[a] = fabs(t[idx[a]]);
+        if (cnt) st = wh_direction(np, pl, hill_factor, at, cnt, dir == 0 ? 1.0 : -1.0, h_target, sub, out);
+        for (int a = 0; a < cnt && st == RVO_OK; a++) rv[idx[a]] = out[a];
+    }
+    free(idx);
+    free(at);
+    free(out);
+    return st;
+}
+
+int rvo_logl_wh(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
+                const double* rvobs, const double* err, int n, double npoints, double h_target, int sub,
+                double* logl) {
+    if (rvo_prior_hard(np, pl, has_hk, has_inc)) {
+        *logl = -INFINITY;
+        return RVO_PRIOR;
+    }
+    double* rv = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+    int st = rvo_wh_rv(np, pl, hill_factor, t, n, h_target, sub, rv);
+    double chi2 = 0.0;
+    if (st == RVO_OK)
+        for (int i = 0; i < n; i++) chi2 += (rv[i] - rvobs[i]) * (rv[i] - rvobs[i]) / (err[i] * err[i]);
+    free(rv);
+    if (st != RVO_OK) {
+        *logl = -INFINITY;
+        return st;
+    }
+    *logl = -(chi2 / npoints);
+    if (!isfinite(*logl)) {
+        *logl = -INFINITY;
+        return RVO_NONFINITE;
+    }
+    return RVO_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Richardson-extrapolated WH, the kernel's full algorithm ("port" of rvm_logl_batch):          */
+/*   level L (0-based) integrates with (L+1)x the level-1 steps; the model RV at each epoch is  */
+/*   sum_L w_L rv_L with w the Lagrange-at-zero weights in x = 1/(L+1)^2; an encounter seen by   */
+/*   any level marks the walker.                                                                */
+/* ------------------------------------------------------------------------------------------ */
+void rvo_richardson_weights(int nl, double* w) {
+    for (int k = 0; k < nl; k++) {
+        const double xk = 1.0 / ((double)(k + 1) * (k + 1));
+        double wk = 1.0;
+        for (int j = 0; j < nl; j++) {
+            if (j == k) continue;
+            const double xj = 1.0 / ((double)(j + 1) * (j + 1));
+            wk *= xj / (xj - xk);
+        }
+        w[k] = wk;
+    }
+}
+
+int rvo_whx_rv(int np, const double* pl, double hill_factor, const double* t, int n, double dt, int nl,
+               double* rv) {
+    double w[8];
+    rvo_richardson_weights(nl, w);
+    double* tmp = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+    for (int i = 0; i < n; i++) rv[i] = 0.0;
+    int st = RVO_OK;
+    for (int k = 0; k < nl; k++) {
+        const int s = rvo_wh_rv(np, pl, hill_factor, t, n, dt, k + 1, tmp);
+        if (s != RVO_OK) {
+            if (st == RVO_OK || s == RVO_ENCOUNTER) st = s;
+            continue;
+        }
+        for (int i = 0; i < n; i++) rv[i] += w[k] * tmp[i];
+    }
+    free(tmp);
+    return st;
+}
+
+int rvo_logl_whx(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
+                 const double* rvobs, const double* err, int n, double npoints, double dt, int nl, double* logl) {
+    if (rvo_prior_hard(np, pl, has_hk, has_inc)) {
+        *logl = -INFINITY;
+        return RVO_PRIOR;
+    }
+    double* rv = (double*)malloc(sizeof(double) * (size_t)(n + 1));
+    int st = rvo_whx_rv(np, pl, hill_factor, t, n, dt, nl, rv);
+    double chi2 = 0.0;
+    if (st == RVO_OK)
+        for (int i = 0; i < n; i++) chi2 += ((rv[i] - rvobs[i]) * (rv[i] - rvobs[i])) / (err[i] * err[i]);
+    free(rv);
+    if (st != RVO_OK) {
+        *logl = -INFINITY;
+        return st;
+    }
+    *logl = -(chi2 / npoints);
+    if (!isfinite(*logl)) {
+        *logl = -INFINITY;
+        return RVO_NONFINITE;
+    }
+    return RVO_OK;
+}
+
+/* batch over walkers: params [W][np][7]; threads: OpenMP-free (callers parallelise if they wish) */
+void rvo_logl_whx_batch(int W, int np, const double* pl, int has_hk, int has_inc, double hill_factor,
+                        const double* t, const double* rvobs, const double* err, int n, double npoints, double dt,
+                        int nl, double* logl, int32_t* status) {
+    for (int w = 0; w < W; w++)
+        status[w] = rvo_logl_whx(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs, err,
+                                 n, npoints, dt, nl, logl + w);
+}

@@ -1,0 +1,254 @@
+// rvm_abi.hip -- the extern "C" surface of librvmcmc.so (declared in include/rvmcmc.h).
+//
+// Host-side work here is limited to building the epoch schedule once per observation set
+// (rvm_plan_create) and to argument checking; every per-step entry point only enqueues kernels on
+// the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rvm_internal.h"
+
+namespace rvm {
+hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, double* chi2_part,
+                       int32_t* status_part, double* logl, int32_t* status, double* rv_out, hipStream_t stream);
+hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
+                                  uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
+                                  double* z, hipStream_t st);
+hipError_t launch_stretch_accept(int P, int n0, int64_t s0b, double* x, double* lnp, const double* q,
+                                 const double* lnp_new, const double* z, uint64_t seed, uint64_t it, uint32_t half,
+                                 const double* draws, int32_t* acc, hipStream_t st);
+hipError_t launch_mh_propose(int P, int n, int64_t b, const double* x, const double* scales, double step,
+                             uint64_t seed, uint64_t it, const double* draws, double* q, hipStream_t st);
+hipError_t launch_mh_accept(int P, int n, int64_t b, double* x, double* lnp, const double* q, const double* lnp_new,
+                            uint64_t seed, uint64_t it, const double* draws, int32_t* acc, hipStream_t st);
+hipError_t launch_fd_params(int P, int n, const double* x, double rel, const double* fl, double* out, hipStream_t st);
+}  // namespace rvm
+
+struct rvm_plan {
+    rvm::DevPlan dev;
+    void* dmem = nullptr;        // one device allocation: schedule + workspace
+    double* chi2_part = nullptr; // [2][max_walkers]
+    int32_t* status_part = nullptr;
+    int32_t max_walkers = 0;
+    int32_t steps[2] = {0, 0};
+};
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+static int hip_fail(hipError_t e, const char* where) {
+    return fail(-3, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+extern "C" {
+
+const char* rvm_last_error(void) { return g_err.c_str(); }
+int rvm_abi_version(void) { return RVM_ABI_VERSION; }
+
+int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, const double* sigma, int32_t n_obs,
+                    int32_t max_walkers, rvm_plan** out) {
+    if (!cfg || !t || !rv || !sigma || !out) return fail(-1, "rvm_plan_create: null argument");
+    if (cfg->n_planets < 1 || cfg->n_planets > RVM_MAX_PLANETS) return fail(-1, "rvm_plan_create: n_planets out of range");
+    if (cfg->n_levels < 1 || cfg->n_levels > RVM_MAX_LEVELS) return fail(-1, "rvm_plan_create: n_levels out of range");
+    if (!(cfg->dt > 0.0) || !std::isfinite(cfg->dt)) return fail(-1, "rvm_plan_create: dt must be > 0");
+    if (n_obs < 0 || max_walkers < 1) return fail(-1, "rvm_plan_create: bad sizes");
+    if (!(cfg->npoints_norm != 0.0)) return fail(-1, "rvm_plan_create: npoints_norm must be nonzero");
+    for (int i = 0; i < n_obs; i++) {
+        if (!std::isfinite(t[i]) || !std::isfinite(rv[i]) || !std::isfinite(sigma[i]))
+            return fail(-1, "rvm_plan_create: non-finite observation");
+    }
+
+    // split epochs by direction, sort by |t| (stable), cut segments into ceil(len/dt) steps
+    struct Dir {
+        std::vector<int32_t> idx, seg_n;
+        std::vector<double> seg_len, orv, os2;
+    } dir[2];
+    long long total_steps[2] = {0, 0};
+    for (int dd = 0; dd < 2; dd++) {
+        Dir& D = dir[dd];
+        for (int i = 0; i < n_obs; i++)
+            if ((dd == 0) == (t[i] >= 0.0)) D.idx.push_back(i);
+        std::stable_sort(D.idx.begin(), D.idx.end(), [&](int a, int b) { return std::fabs(t[a]) < std::fabs(t[b]); });
+        const double sign = dd == 0 ? 1.0 : -1.0;
+        double tprev = 0.0;
+        for (int i : D.idx) {
+            const double at = std::fabs(t[i]);
+            const double len = at - tprev;
+            tprev = at;
+            int n = len > 0.0 ? (int)std::ceil(len / cfg->dt - 1e-9) : 0;
+            if (len > 0.0 && n < 1) n = 1;
+            D.seg_n.push_back(n);
+            D.seg_len.push_back(sign * len);
+            D.orv.push_back(rv[i]);
+            D.os2.push_back(sigma[i] * sigma[i]);
+            total_steps[dd] += n;
+        }
+        if (total_steps[dd] * (long long)cfg->n_levels > (1LL << 30))
+            return fail(-1, "rvm_plan_create: dt too small for the epoch span");
+    }
+
+    // device layout: per direction [seg_n | obs_idx] int32 and [seg_len | obs_rv | obs_s2] f64, + workspace
+    const size_t nf = dir[0].idx.size(), nb = dir[1].idx.size();
+    const size_t n_dbl = 3 * (nf + nb) + 2 * (size_t)max_walkers;
+    const size_t n_int = 2 * (nf + nb) + 2 * (size_t)max_walkers;
+    const size_t bytes = n_dbl * sizeof(double) + n_int * sizeof(int32_t) + 64;
+    rvm_plan* plan = new rvm_plan();
+    hipError_t e = hipMalloc(&plan->dmem, bytes);
+    if (e != hipSuccess) {
+        delete plan;
+        return hip_fail(e, "rvm_plan_create: hipMalloc");
+    }
+    std::vector<unsigned char> host(bytes, 0);
+    double* hd = reinterpret_cast<double*>(host.data());
+    int32_t* hi = reinterpret_cast<int32_t*>(host.data() + n_dbl * sizeof(double));
+    double* dd_base = reinterpret_cast<double*>(plan->dmem);
+    int32_t* di_base = reinterpret_cast<int32_t*>(reinterpret_cast<unsigned char*>(plan->dmem) + n_dbl * sizeof(double));
+    size_t od = 0, oi = 0;
+    rvm::DirSched* S[2] = {&plan->dev.fwd, &plan->dev.bwd};
+    for (int dd = 0; dd < 2; dd++) {
+        const Dir& D = dir[dd];
+        const size_t n = D.idx.size();
+        S[dd]->n_epochs = (int32_t)n;
+        std::memcpy(hd + od, D.seg_len.data(), n * sizeof(double));
+        S[dd]->seg_len = dd_base + od;
+        od += n;
+        std::memcpy(hd + od, D.orv.data(), n * sizeof(double));
+        S[dd]->obs_rv = dd_base + od;
+        od += n;
+        std::memcpy(hd + od, D.os2.data(), n * sizeof(double));
+        S[dd]->obs_s2 = dd_base + od;
+        od += n;
+        std::memcpy(hi + oi, D.seg_n.data(), n * sizeof(int32_t));
+        S[dd]->seg_n = di_base + oi;
+        oi += n;
+        std::memcpy(hi + oi, D.idx.data(), n * sizeof(int32_t));
+        S[dd]->obs_idx = di_base + oi;
+        oi += n;
+        plan->steps[dd] = (int32_t)total_steps[dd];
+    }
+    plan->chi2_part = dd_base + od;
+    plan->status_part = di_base + oi;
+    plan->max_walkers = max_walkers;
+    e = hipMemcpy(plan->dmem, host.data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(plan->dmem);
+        delete plan;
+        return hip_fail(e, "rvm_plan_create: hipMemcpy");
+    }
+
+    rvm::DevPlan& P = plan->dev;
+    P.n_planets = cfg->n_planets;
+    P.n_levels = cfg->n_levels;
+    P.npoints = cfg->npoints_norm;
+    P.n_obs = n_obs;
+    // Richardson weights for the h^2 expansion: level k uses step h/(k+1); Lagrange at 0 in x = 1/n^2
+    for (int k = 0; k < RVM_MAX_LEVELS; k++) {
+        P.mult[k] = k + 1;
+        P.lw[k] = 0.0;
+    }
+    for (int k = 0; k < cfg->n_levels; k++) {
+        const double xk = 1.0 / ((double)(k + 1) * (k + 1));
+        double wk = 1.0;
+        for (int j = 0; j < cfg->n_levels; j++) {
+            if (j == k) continue;
+            const double xj = 1.0 / ((double)(j + 1) * (j + 1));
+            wk *= xj / (xj - xk);
+        }
+        P.lw[k] = wk;
+    }
+    *out = plan;
+    return 0;
+}
+
+void rvm_plan_destroy(rvm_plan* plan) {
+    if (!plan) return;
+    if (plan->dmem) (void)hipFree(plan->dmem);
+    delete plan;
+}
+
+int rvm_plan_info(const rvm_plan* plan, int32_t* sf, int32_t* sb, int32_t* ef, int32_t* eb) {
+    if (!plan) return fail(-1, "rvm_plan_info: null plan");
+    if (sf) *sf = plan->steps[0];
+    if (sb) *sb = plan->steps[1];
+    if (ef) *ef = plan->dev.fwd.n_epochs;
+    if (eb) *eb = plan->dev.bwd.n_epochs;
+    return 0;
+}
+
+int rvm_logl_batch(const rvm_plan* plan, int32_t n_walkers, const double* params, double hill_factor,
+                   double* logl_out, int32_t* status_out, double* rv_out, void* stream) {
+    if (!plan) return fail(-1, "rvm_logl_batch: null plan");
+    if (n_walkers == 0) return 0;
+    if (n_walkers < 0 || n_walkers > plan->max_walkers)
+        return fail(-1, "rvm_logl_batch: n_walkers exceeds the plan's max_walkers");
+    if (!params || !logl_out || !status_out) return fail(-1, "rvm_logl_batch: null buffer");
+    if (!(hill_factor >= 0.0)) return fail(-1, "rvm_logl_batch: hill_factor must be >= 0");
+    hipError_t e = rvm::launch_logl(plan->dev, n_walkers, params, hill_factor, plan->chi2_part, plan->status_part,
+                                    logl_out, status_out, rv_out, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "rvm_logl_batch");
+    return 0;
+}
+
+int rvm_stretch_propose(int32_t n_params, int32_t n_s0, int64_t s0_begin, const double* x, int32_t n_s1,
+                        const double* c, double a, uint64_t seed, uint64_t iteration, uint32_t half,
+                        const double* draws, double* q_out, double* z_out, void* stream) {
+    if (n_s0 == 0) return 0;
+    if (n_params < 1 || n_s0 < 0 || n_s1 < 1 || !x || !c || !q_out || !z_out)
+        return fail(-1, "rvm_stretch_propose: bad arguments");
+    if (!(a > 1.0)) return fail(-1, "rvm_stretch_propose: stretch scale a must be > 1");
+    hipError_t e = rvm::launch_stretch_propose(n_params, n_s0, s0_begin, x, n_s1, c, a, seed, iteration, half, draws,
+                                               q_out, z_out, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_propose");
+}
+
+int rvm_stretch_accept(int32_t n_params, int32_t n_s0, int64_t s0_begin, double* x, double* lnp, const double* q,
+                       const double* lnp_new, const double* z, uint64_t seed, uint64_t iteration, uint32_t half,
+                       const double* draws, int32_t* accepted, void* stream) {
+    if (n_s0 == 0) return 0;
+    if (n_params < 1 || n_s0 < 0 || !x || !lnp || !q || !lnp_new || !z)
+        return fail(-1, "rvm_stretch_accept: bad arguments");
+    hipError_t e = rvm::launch_stretch_accept(n_params, n_s0, s0_begin, x, lnp, q, lnp_new, z, seed, iteration, half,
+                                              draws, accepted, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_accept");
+}
+
+int rvm_mh_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, const double* x, const double* scales,
+                   double step_size, uint64_t seed, uint64_t iteration, const double* draws, double* q_out,
+                   void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_chains < 0 || !x || !scales || !q_out) return fail(-1, "rvm_mh_propose: bad arguments");
+    hipError_t e = rvm::launch_mh_propose(n_params, n_chains, chain_begin, x, scales, step_size, seed, iteration, draws,
+                                          q_out, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_mh_propose");
+}
+
+int rvm_mh_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, double* lnp, const double* q,
+                  const double* lnp_new, uint64_t seed, uint64_t iteration, const double* draws, int32_t* accepted,
+                  void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_chains < 0 || !x || !lnp || !q || !lnp_new) return fail(-1, "rvm_mh_accept: bad arguments");
+    hipError_t e = rvm::launch_mh_accept(n_params, n_chains, chain_begin, x, lnp, q, lnp_new, seed, iteration, draws,
+                                         accepted, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_mh_accept");
+}
+
+int rvm_fd_params(int32_t n_params, int32_t n_chains, const double* x, double rel_step, const double* floor_,
+                  double* out, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_chains < 0 || !x || !floor_ || !out || !(rel_step > 0.0))
+        return fail(-1, "rvm_fd_params: bad arguments");
+    hipError_t e = rvm::launch_fd_params(n_params, n_chains, x, rel_step, floor_, out, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_fd_params");
+}
+
+}  // extern "C"

@@ -1,0 +1,30 @@
+// rvm_internal.h -- host/device shared launch descriptors of librvmcmc.so (not part of the ABI).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/rvmcmc.h"
+
+namespace rvm {
+
+// Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
+struct DirSched {
+    int32_t n_epochs;
+    const int32_t* seg_n;     // level-1 steps in the segment ending at this epoch (0: same time)
+    const double* seg_len;    // signed segment length (code time)
+    const double* obs_rv;     // observed RV
+    const double* obs_s2;     // sigma^2
+    const int32_t* obs_idx;   // index of the epoch in the plan's input order (rv_out rows)
+};
+
+// Everything a logl launch needs, passed by value as the kernel argument.
+struct DevPlan {
+    int32_t n_planets;
+    int32_t n_levels;
+    int32_t mult[RVM_MAX_LEVELS];  // level step multipliers (1, 2, 3, ...)
+    double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
+    double npoints;
+    int32_t n_obs;
+    DirSched fwd, bwd;
+};
+
+}  // namespace rvm

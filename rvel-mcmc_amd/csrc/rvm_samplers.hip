@@ -1,0 +1,166 @@
+// rvm_samplers.hip -- device-side proposal / accept steps of the reference samplers.
+//
+//   * emcee 2.2.1 EnsembleSampler stretch move (mcmc.py:40-65 drives it; the algorithm is emcee's
+//     _propose_stretch + the two-half split of sample()).
+//   * Gaussian random-walk Metropolis-Hastings (mcmc.py:89-121).
+//   * The finite-difference stencil that feeds SMALA's gradient/metric (mcmc.py:144-187 with the
+//     north-star's FD replacement of state.py:253-294).
+// All positions are SoA [n_params][n] float64.  Random numbers come from Philox4x32-10 keyed by the
+// GLOBAL walker index, so a sharded ensemble draws exactly what an unsharded one does.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "rvm_device.h"
+#include "rvm_internal.h"
+
+// No FMA contraction in the sampler arithmetic: proposals and accept tests are then bit-identical
+// to a plain IEEE restatement (numpy) fed the same random numbers.
+#pragma clang fp contract(off)
+
+namespace rvm {
+
+enum : uint32_t {
+    RNG_STRETCH_PROPOSE = 1,
+    RNG_STRETCH_ACCEPT = 2,
+    RNG_MH_PROPOSE = 3,
+    RNG_MH_ACCEPT = 4,
+};
+
+__global__ void stretch_propose_kernel(int P, int n0, int64_t s0_begin, const double* __restrict__ x, int n1,
+                                       const double* __restrict__ c, double a, uint64_t seed, uint64_t iteration,
+                                       uint32_t half, const double* __restrict__ draws, double* __restrict__ q,
+                                       double* __restrict__ zout) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n0) return;
+    double u1, u2;
+    if (draws) {
+        u1 = draws[i];
+        u2 = draws[n0 + i];
+    } else {
+        uniform2(seed, (uint64_t)(s0_begin + i), iteration, RNG_STRETCH_PROPOSE | (half << 8), u1, u2);
+    }
+    const double z = ((a - 1.0) * u1 + 1.0) * ((a - 1.0) * u1 + 1.0) / a;
+    int j = (int)floor(u2 * (double)n1);
+    j = j < 0 ? 0 : (j >= n1 ? n1 - 1 : j);
+    for (int p = 0; p < P; p++) {
+        const double cj = c[(size_t)p * n1 + j];
+        q[(size_t)p * n0 + i] = cj - z * (cj - x[(size_t)p * n0 + i]);
+    }
+    zout[i] = z;
+}
+
+__global__ void stretch_accept_kernel(int P, int n0, int64_t s0_begin, double* __restrict__ x,
+                                      double* __restrict__ lnp, const double* __restrict__ q,
+                                      const double* __restrict__ lnp_new, const double* __restrict__ z,
+                                      uint64_t seed, uint64_t iteration, uint32_t half,
+                                      const double* __restrict__ draws, int32_t* __restrict__ accepted) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n0) return;
+    double u3, unused;
+    if (draws) {
+        u3 = draws[i];
+    } else {
+        uniform2(seed, (uint64_t)(s0_begin + i), iteration, RNG_STRETCH_ACCEPT | (half << 8), u3, unused);
+    }
+    // emcee 2.2.1: lnpdiff = (dim - 1) * log(zz) + newlnprob - lnprob0 ; accept = lnpdiff > log(rand)
+    const double lnpdiff = (double)(P - 1) * log(z[i]) + lnp_new[i] - lnp[i];
+    if (lnpdiff > log(u3)) {
+        for (int p = 0; p < P; p++) x[(size_t)p * n0 + i] = q[(size_t)p * n0 + i];
+        lnp[i] = lnp_new[i];
+        if (accepted) accepted[i] += 1;
+    }
+}
+
+__device__ __forceinline__ double box_muller(double u0, double u1) {
+    return sqrt(-2.0 * log(u0)) * cospi(2.0 * u1);
+}
+
+__global__ void mh_propose_kernel(int P, int n, int64_t begin, const double* __restrict__ x,
+                                  const double* __restrict__ scales, double step, uint64_t seed, uint64_t iteration,
+                                  const double* __restrict__ draws, double* __restrict__ q) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int p = 0; p < P; p++) {
+        double g;
+        if (draws) {
+            g = draws[(size_t)p * n + i];
+        } else {
+            double u0, u1;
+            uniform2(seed, (uint64_t)(begin + i), iteration, RNG_MH_PROPOSE | ((uint32_t)p << 8), u0, u1);
+            g = box_muller(u0, u1);
+        }
+        // mcmc.py:91-92: shift = step_size * scales * N(0,1); prop.shift_params(shift)
+        q[(size_t)p * n + i] = x[(size_t)p * n + i] + (step * scales[p]) * g;
+    }
+}
+
+__global__ void mh_accept_kernel(int P, int n, int64_t begin, double* __restrict__ x, double* __restrict__ lnp,
+                                 const double* __restrict__ q, const double* __restrict__ lnp_new, uint64_t seed,
+                                 uint64_t iteration, const double* __restrict__ draws,
+                                 int32_t* __restrict__ accepted) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double u, unused;
+    if (draws) {
+        u = draws[i];
+    } else {
+        uniform2(seed, (uint64_t)(begin + i), iteration, RNG_MH_ACCEPT, u, unused);
+    }
+    // mcmc.py:115: if np.exp(logp_proposal - logp) > np.random.uniform(): accept
+    if (exp(lnp_new[i] - lnp[i]) > u) {
+        for (int p = 0; p < P; p++) x[(size_t)p * n + i] = q[(size_t)p * n + i];
+        lnp[i] = lnp_new[i];
+        if (accepted) accepted[i] += 1;
+    }
+}
+
+// out: SoA [n_params][(2P+1) * n] with walker index s*n + c  (s = 0: x; s = 1+2p: +eps_p; 2+2p: -eps_p)
+__global__ void fd_params_kernel(int P, int n, const double* __restrict__ x, double rel, const double* __restrict__ fl,
+                                 double* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    const int S = 2 * P + 1;
+    const size_t WW = (size_t)S * n;
+    for (int p = 0; p < P; p++) {
+        const double xp = x[(size_t)p * n + c];
+        for (int s = 0; s < S; s++) out[(size_t)p * WW + (size_t)s * n + c] = xp;
+    }
+    for (int p = 0; p < P; p++) {
+        const double xp = x[(size_t)p * n + c];
+        const double ax = fabs(xp) > fl[p] ? fabs(xp) : fl[p];
+        const double eps = rel * ax;
+        out[(size_t)p * WW + (size_t)(1 + 2 * p) * n + c] = xp + eps;
+        out[(size_t)p * WW + (size_t)(2 + 2 * p) * n + c] = xp - eps;
+    }
+}
+
+static inline dim3 grid1(int n) { return dim3((n + 255) / 256); }
+
+hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
+                                  uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
+                                  double* z, hipStream_t st) {
+    stretch_propose_kernel<<<grid1(n0), 256, 0, st>>>(P, n0, s0b, x, n1, c, a, seed, it, half, draws, q, z);
+    return hipGetLastError();
+}
+hipError_t launch_stretch_accept(int P, int n0, int64_t s0b, double* x, double* lnp, const double* q,
+                                 const double* lnp_new, const double* z, uint64_t seed, uint64_t it, uint32_t half,
+                                 const double* draws, int32_t* acc, hipStream_t st) {
+    stretch_accept_kernel<<<grid1(n0), 256, 0, st>>>(P, n0, s0b, x, lnp, q, lnp_new, z, seed, it, half, draws, acc);
+    return hipGetLastError();
+}
+hipError_t launch_mh_propose(int P, int n, int64_t b, const double* x, const double* scales, double step,
+                             uint64_t seed, uint64_t it, const double* draws, double* q, hipStream_t st) {
+    mh_propose_kernel<<<grid1(n), 256, 0, st>>>(P, n, b, x, scales, step, seed, it, draws, q);
+    return hipGetLastError();
+}
+hipError_t launch_mh_accept(int P, int n, int64_t b, double* x, double* lnp, const double* q, const double* lnp_new,
+                            uint64_t seed, uint64_t it, const double* draws, int32_t* acc, hipStream_t st) {
+    mh_accept_kernel<<<grid1(n), 256, 0, st>>>(P, n, b, x, lnp, q, lnp_new, seed, it, draws, acc);
+    return hipGetLastError();
+}
+hipError_t launch_fd_params(int P, int n, const double* x, double rel, const double* fl, double* out, hipStream_t st) {
+    fd_params_kernel<<<grid1(n), 256, 0, st>>>(P, n, x, rel, fl, out);
+    return hipGetLastError();
+}
+
+}  // namespace rvm

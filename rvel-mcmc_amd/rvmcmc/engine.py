@@ -1,0 +1,220 @@
+"""Batched likelihood engine: torch device tensors in, the HIP kernel through the C ABI.
+
+`LoglPlan` owns one `rvm_plan` (epoch schedule + observation data resident in HBM) and launches
+`rvm_logl_batch` on the caller's current torch stream.  `ParamMap` maps a reference-style
+`State` (dict-of-planets, free parameters in dict order, state.py:8-31 / 124-207) onto the
+kernel's canonical SoA layout [5 * n_planets][n_walkers] with per-planet order m, a, h, k, l.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+
+KERNEL_KEYS = ("m", "a", "h", "k", "l")
+SUPPORTED_KEYS = set(KERNEL_KEYS) | {"ix", "iy"}
+
+
+@dataclass(frozen=True)
+class IntegratorConfig:
+    """Wisdom-Holman + Richardson settings.
+
+    steps_per_orbit: level-1 steps per shortest orbital period of the reference state
+                     (dt = P_min / steps_per_orbit) unless `dt` is given explicitly.
+    n_levels:        Richardson levels; level L integrates with dt/(L+1).  n_levels=4 at
+                     steps_per_orbit=20 keeps |logL - logL_IAS15| ~1e-9 on the benchmark
+                     configs (tests/test_parity_gpu.py states the tolerance it enforces).
+    """
+
+    steps_per_orbit: float = 20.0
+    n_levels: int = 4
+    dt: Optional[float] = None
+
+    def step_for(self, planets) -> float:
+        if self.dt is not None:
+            return float(self.dt)
+        return min_period(planets) / float(self.steps_per_orbit)
+
+
+DEFAULT_CONFIG = IntegratorConfig()
+
+
+def min_period(planets) -> float:
+    """Shortest Keplerian period (code units, G = M_star = 1) of a list of planet dicts."""
+    best = math.inf
+    for p in planets:
+        a = float(p["a"])
+        m = float(p.get("m", 0.0))
+        if a > 0:
+            best = min(best, 2.0 * math.pi * math.sqrt(a ** 3 / (1.0 + max(m, 0.0))))
+    if not math.isfinite(best):
+        raise ValueError("cannot derive an integrator step: no planet with a > 0")
+    return best
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def default_device():
+    torch = _torch()
+    if not torch.cuda.is_available():
+        raise _lib.RvmError("no HIP device visible: the likelihood runs only on the GPU (no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class LoglPlan:
+    """rvm_plan for one observation set on one device."""
+
+    def __init__(self, t, rv, sigma, npoints, n_planets, dt, n_levels=4, max_walkers=4096, device=None):
+        torch = _torch()
+        self.lib = _lib.load()
+        self.device = torch.device(device) if device is not None else default_device()
+        t = np.ascontiguousarray(np.asarray(t, dtype=np.float64))
+        rv = np.ascontiguousarray(np.asarray(rv, dtype=np.float64))
+        sigma = np.ascontiguousarray(np.asarray(sigma, dtype=np.float64))
+        if not (len(t) == len(rv) == len(sigma)):
+            raise ValueError("t, rv and sigma must have the same length")
+        self.n_obs = len(t)
+        self.n_planets = int(n_planets)
+        self.dt = float(dt)
+        self.n_levels = int(n_levels)
+        self.npoints = float(npoints)
+        self.max_walkers = int(max_walkers)
+        cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints)
+        handle = C.c_void_p()
+        dp = C.POINTER(C.c_double)
+        with torch.cuda.device(self.device):
+            rc = self.lib.rvm_plan_create(C.byref(cfg), t.ctypes.data_as(dp), rv.ctypes.data_as(dp),
+                                          sigma.ctypes.data_as(dp), self.n_obs, self.max_walkers, C.byref(handle))
+        _lib.check(rc, "rvm_plan_create")
+        self._h = handle
+
+    def info(self):
+        vals = [C.c_int32() for _ in range(4)]
+        _lib.check(self.lib.rvm_plan_info(self._h, *[C.byref(v) for v in vals]), "rvm_plan_info")
+        return dict(steps_fwd=vals[0].value, steps_bwd=vals[1].value, epochs_fwd=vals[2].value,
+                    epochs_bwd=vals[3].value)
+
+    def logl(self, params, hill_factor=1.0, want_rv=False, out=None, status=None, rv_out=None, stream=None):
+        """params: float64 device tensor [5*n_planets][W] (contiguous) -> (logl[W], status[W], rv|None).
+
+        rv (if requested) is [n_obs][W], rows in the plan's input epoch order."""
+        torch = _torch()
+        if params.dtype != torch.float64 or params.device != self.device or params.dim() != 2:
+            raise ValueError("params must be a 2-D float64 tensor on the plan's device")
+        if params.shape[0] != 5 * self.n_planets:
+            raise ValueError(f"params must have {5 * self.n_planets} rows (m,a,h,k,l per planet)")
+        params = params.contiguous()
+        W = params.shape[1]
+        if W > self.max_walkers:
+            raise ValueError(f"{W} walkers exceed the plan's max_walkers={self.max_walkers}")
+        if out is None:
+            out = torch.empty(W, dtype=torch.float64, device=self.device)
+        if status is None:
+            status = torch.empty(W, dtype=torch.int32, device=self.device)
+        rvp = 0
+        if want_rv:
+            if rv_out is None:
+                rv_out = torch.empty((self.n_obs, W), dtype=torch.float64, device=self.device)
+            rvp = rv_out.data_ptr()
+        with torch.cuda.device(self.device):
+            rc = self.lib.rvm_logl_batch(self._h, W, params.data_ptr(), float(hill_factor), out.data_ptr(),
+                                         status.data_ptr(), rvp, _lib.stream_handle(stream))
+        _lib.check(rc, "rvm_logl_batch")
+        return out, status, (rv_out if want_rv else None)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.rvm_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def obs_arrays(obs):
+    """Observation -> (t, rv, sigma) concatenated as tf then tb (rv_out rows follow this order)."""
+    t = np.concatenate([np.asarray(obs.tf, dtype=np.float64), np.asarray(obs.tb, dtype=np.float64)])
+    rv = np.concatenate([np.asarray(obs.rvf, dtype=np.float64), np.asarray(obs.rvb, dtype=np.float64)])
+    er = np.concatenate([np.asarray(obs.errorf, dtype=np.float64), np.asarray(obs.errorb, dtype=np.float64)])
+    return t, rv, er
+
+
+def plan_for(obs, n_planets, dt, n_levels, max_walkers, device=None) -> LoglPlan:
+    """Cached LoglPlan on an Observation object (keyed by device and integrator settings)."""
+    dev = _torch().device(device) if device is not None else default_device()
+    cache = obs.__dict__.setdefault("_rvm_plans", {})
+    key = (str(dev), int(n_planets), float(dt), int(n_levels))
+    plan = cache.get(key)
+    if plan is None or plan.max_walkers < max_walkers:
+        t, rv, er = obs_arrays(obs)
+        cap = max(int(max_walkers), plan.max_walkers * 2 if plan else 0, 64)
+        plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, n_levels, cap, dev)
+        cache[key] = plan
+    return plan
+
+
+class ParamMap:
+    """Free-parameter vectors of a State  <->  kernel SoA parameter blocks.
+
+    The free parameters of a State are its planets' keys in dict order minus ignore_vars /
+    ignore_params (state.py:26-31, 143-155).  The kernel wants every planet's m, a, h, k, l;
+    non-free values are taken from the State's planets (missing h/k/l default to 0 as REBOUND's
+    Pal constructor does)."""
+
+    def __init__(self, state):
+        self.n_planets = len(state.planets)
+        if not 1 <= self.n_planets <= _lib.RVM_MAX_PLANETS:
+            raise ValueError(f"1..{_lib.RVM_MAX_PLANETS} planets supported, got {self.n_planets}")
+        base = np.zeros(5 * self.n_planets)
+        for i, p in enumerate(state.planets):
+            unknown = set(p.keys()) - SUPPORTED_KEYS
+            if unknown:
+                raise ValueError(f"planet {i}: unsupported keys {sorted(unknown)} (Pal elements m,a,h,k,l only)")
+            if float(p.get("ix", 0.0)) != 0.0 or float(p.get("iy", 0.0)) != 0.0:
+                raise NotImplementedError("inclined orbits (ix, iy != 0) are not supported by the kernel")
+            if "a" not in p:
+                raise ValueError(f"planet {i}: 'a' is required")
+            for j, k in enumerate(KERNEL_KEYS):
+                base[5 * i + j] = float(p.get(k, 0.0))
+        self.base = base
+        slots = []
+        for i, planet in enumerate(state.planets):
+            for k in planet.keys():
+                if state._is_free(i, k):
+                    if k in ("ix", "iy"):
+                        raise NotImplementedError("free inclination parameters are not supported by the kernel")
+                    slots.append(5 * i + KERNEL_KEYS.index(k))
+        self.slots = np.asarray(slots, dtype=np.int64)
+        self.n_free = len(slots)
+        self._dev_cache = {}
+
+    def to_kernel(self, X):
+        """X: float64 device tensor [n_free][W] -> kernel params [5*np][W]."""
+        torch = _torch()
+        key = str(X.device)
+        if key not in self._dev_cache:
+            self._dev_cache[key] = (torch.as_tensor(self.base, device=X.device),
+                                    torch.as_tensor(self.slots, device=X.device))
+        base, slots = self._dev_cache[key]
+        W = X.shape[1]
+        K = base[:, None].expand(-1, W).clone()
+        if self.n_free:
+            K.index_copy_(0, slots, X)
+        return K
+
+    def vector_to_kernel_np(self, x):
+        k = self.base.copy()
+        k[self.slots] = np.asarray(x, dtype=np.float64)
+        return k

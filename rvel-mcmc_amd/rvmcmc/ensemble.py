@@ -1,0 +1,191 @@
+"""Device-resident affine-invariant ensemble sampler (emcee 2.2.1 stretch move).
+
+The reference drives emcee 2.2.1's EnsembleSampler (mcmc.py:40-65; version from script.sh:9) with
+threads=1 and a serial map over `lnprob`.  emcee is not vendored; its published algorithm
+(EnsembleSampler.sample + _propose_stretch) is restated here with the ensemble
+kept in HBM as SoA [dim][W] float64 and every walker-logL of a half-step evaluated by one launch of
+the HIP likelihood kernel:
+
+    for (S0, S1) in [(first half, second half), (second half, first half)]:
+        z  = ((a - 1) u1 + 1)^2 / a            (a = 2)
+        j  = floor(u2 |S1|)
+        q  = c_j - z (c_j - x)
+        lnpdiff = (dim - 1) ln z + lnp(q) - lnp(x) ;  accept if lnpdiff > ln u3
+    (S1 of the second half-step is the already-updated first half.)
+
+Random numbers are counter-based (Philox4x32-10, keyed by seed, iteration, half and GLOBAL walker
+index), so a run is reproducible and identical for any number of ranks.
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL/xGMI): each rank owns a contiguous
+slice of each half; before each half-step the complement half's positions are all-gathered
+(dim x W/2 float64 -- the only collective on the data path).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib, engine
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+class EnsembleSampler:
+    def __init__(self, nwalkers, state, obs, a=2.0, seed=0, device=None, hill_factor=None, group=None,
+                 pmap=None):
+        torch = _torch()
+        dim = state.Nvars
+        if nwalkers % 2 != 0:
+            raise ValueError("The number of walkers must be even.")
+        if nwalkers < 2 * dim:
+            raise ValueError("The number of walkers needs to be more than twice the dimension of your parameter space.")
+        self.k = int(nwalkers)
+        self.dim = dim
+        self.a = float(a)
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.state = state
+        self.obs = obs
+        self.pmap = pmap or state.param_map()
+        self.hill_factor = state.hillRadiusFactor if hill_factor is None else float(hill_factor)
+        self.device = torch.device(device) if device is not None else engine.default_device()
+        self.lib = _lib.load()
+        # distributed layout
+        self.group = group
+        if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            self.rank = torch.distributed.get_rank(group)
+            self.world = torch.distributed.get_world_size(group)
+        else:
+            self.rank, self.world = 0, 1
+        self.halfk = self.k // 2
+        if self.halfk % self.world != 0:
+            raise ValueError("nwalkers/2 must be divisible by the world size")
+        self.nloc = self.halfk // self.world  # local walkers per half
+        self.iteration = 0
+        dt = state.integrator.step_for(state.planets)
+        self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, state.integrator.n_levels, self.nloc, self.device)
+        n = self.nloc
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self._q = torch.empty((dim, n), **f64)
+        self._z = torch.empty(n, **f64)
+        self._lnp_new = torch.empty(n, **f64)
+        self._status = torch.empty(n, dtype=torch.int32, device=self.device)
+        self._c_full = torch.empty((dim, self.halfk), **f64)
+        self._gather = torch.empty(self.world * dim * n, **f64) if self.world > 1 else None
+        self.naccepted = torch.zeros(2 * n, dtype=torch.int32, device=self.device)
+        self.nevals = 0
+        self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
+        self.status_counts = torch.zeros(4, dtype=torch.int64, device=self.device)
+
+    # ---- global <-> local indexing ------------------------------------------------------------
+    def global_begin(self, half):
+        return half * self.halfk + self.rank * self.nloc
+
+    def local_slices(self):
+        """Global walker indices owned by this rank (first-half slice, second-half slice)."""
+        return (slice(self.global_begin(0), self.global_begin(0) + self.nloc),
+                slice(self.global_begin(1), self.global_begin(1) + self.nloc))
+
+    # ---- likelihood ---------------------------------------------------------------------------
+    def lnprob(self, X, out=None, status=None):
+        K = self.pmap.to_kernel(X)
+        if self.timing is not None:  # HIP events on the launch stream, around the likelihood launch only
+            torch = _torch()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        lp, st, _ = self.plan.logl(K, hill_factor=self.hill_factor, out=out, status=status)
+        if self.timing is not None:
+            e1.record()
+            self.timing.append((e0, e1, X.shape[1]))
+        self.nevals += X.shape[1]
+        return lp, st
+
+    def _complement(self, Xc):
+        """Full complement half [dim][W/2] in global order (all-gather over ranks)."""
+        torch = _torch()
+        if self.world == 1:
+            return Xc
+        torch.distributed.all_gather_into_tensor(self._gather, Xc.contiguous().view(-1), group=self.group)
+        g = self._gather.view(self.world, self.dim, self.nloc)
+        self._c_full.copy_(g.permute(1, 0, 2).reshape(self.dim, self.halfk))
+        return self._c_full
+
+    def half_step(self, X0, lnp0, Xc, half, draws_propose=None, draws_accept=None):
+        """Update this rank's slice X0 [dim][nloc] (in place) against the complement half."""
+        st = _lib.stream_handle()
+        c = self._complement(Xc)
+        n = self.nloc
+        b = self.global_begin(half)
+        _lib.check(self.lib.rvm_stretch_propose(self.dim, n, b, X0.data_ptr(), self.halfk, c.data_ptr(), self.a,
+                                                self.seed, self.iteration, half,
+                                                draws_propose.data_ptr() if draws_propose is not None else 0,
+                                                self._q.data_ptr(), self._z.data_ptr(), st), "rvm_stretch_propose")
+        self.lnprob(self._q, out=self._lnp_new, status=self._status)
+        acc = self.naccepted[half * n:(half + 1) * n]
+        _lib.check(self.lib.rvm_stretch_accept(self.dim, n, b, X0.data_ptr(), lnp0.data_ptr(), self._q.data_ptr(),
+                                               self._lnp_new.data_ptr(), self._z.data_ptr(), self.seed,
+                                               self.iteration, half,
+                                               draws_accept.data_ptr() if draws_accept is not None else 0,
+                                               acc.data_ptr(), st), "rvm_stretch_accept")
+        self.status_counts.index_add_(0, self._status.long(),
+                                      _torch().ones_like(self._status, dtype=_torch().int64))
+
+    # ---- ensemble state ------------------------------------------------------------------------
+    def set_positions(self, X_global):
+        """X_global: [W][dim] array-like of ALL walkers (every rank passes the same array); this
+        rank keeps its two slices as contiguous device tensors [dim][nloc]."""
+        torch = _torch()
+        Xg = torch.as_tensor(np.asarray(X_global, dtype=np.float64), device=self.device)
+        if Xg.shape != (self.k, self.dim):
+            raise ValueError(f"positions must be [{self.k}][{self.dim}]")
+        s0, s1 = self.local_slices()
+        self.pos = [Xg[s0].t().contiguous(), Xg[s1].t().contiguous()]
+        self.lnp = [None, None]
+
+    def compute_lnprob(self):
+        self.lnp = [self.lnprob(self.pos[h])[0].clone() for h in (0, 1)]
+        for h in (0, 1):
+            self.check_initial(self.lnp[h])
+
+    def step(self):
+        """One emcee iteration (both half-steps) over this rank's walkers."""
+        if self.lnp[0] is None:
+            self.compute_lnprob()
+        A, B = self.pos
+        self.half_step(A, self.lnp[0], B, 0)
+        self.half_step(B, self.lnp[1], A, 1)
+        self.iteration += 1
+
+    def gather_positions(self):
+        """All walkers [W][dim] on every rank (host numpy), global order."""
+        torch = _torch()
+        loc = [p.t().contiguous() for p in self.pos]  # [nloc][dim]
+        if self.world == 1:
+            return torch.cat(loc, 0).cpu().numpy()
+        out = []
+        for h in (0, 1):
+            buf = torch.empty((self.world * self.nloc, self.dim), dtype=torch.float64, device=self.device)
+            torch.distributed.all_gather_into_tensor(buf, loc[h], group=self.group)
+            out.append(buf)
+        return torch.cat(out, 0).cpu().numpy()
+
+    def gather_lnprob(self):
+        torch = _torch()
+        if self.world == 1:
+            return torch.cat(self.lnp, 0).cpu().numpy()
+        out = []
+        for h in (0, 1):
+            buf = torch.empty(self.world * self.nloc, dtype=torch.float64, device=self.device)
+            torch.distributed.all_gather_into_tensor(buf, self.lnp[h].contiguous(), group=self.group)
+            out.append(buf)
+        return torch.cat(out, 0).cpu().numpy()
+
+    def check_initial(self, lnp):
+        torch = _torch()
+        if bool(torch.isnan(lnp).any()):
+            raise ValueError("The initial lnprob was NaN.")
+
+    def acceptance_fraction(self):
+        return self.naccepted.double() / max(self.iteration, 1)

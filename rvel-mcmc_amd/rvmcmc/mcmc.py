@@ -1,0 +1,167 @@
+"""Samplers with the reference's API (mirror of /root/reference/mcmc.py), GPU underneath.
+
+* Mcmc / step_force           mcmc.py:12-25
+* lnprob(x, e)                mcmc.py:28-35   (scalar callback; any exception -> -inf)
+* Ensemble                    mcmc.py:40-75   (emcee 2.2.1 stretch move; here the whole ensemble
+                                               lives on the GPU, see ensemble.EnsembleSampler)
+* Mh                          mcmc.py:80-121  (single chain, host RNG as the reference)
+* Smala                       mcmc.py:126-187 (SoftAbs SMALA; derivatives by finite differences)
+* MhChains                    batched independent MH chains on the device (new; the batched
+                              counterpart of Mh, one logL launch per step for all chains)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib, engine
+from .ensemble import EnsembleSampler
+from .state import Encounter
+
+
+class Mcmc(object):
+    def __init__(self, initial_state, obs):
+        self.state = initial_state.deepcopy()  # NOTE: resets hillRadiusFactor to 1.0 (state.py:212-213)
+        self.obs = obs
+
+    def step(self):
+        return True
+
+    def step_force(self):
+        tries = 1
+        while self.step() == False:  # noqa: E712 (reference semantics)
+            tries += 1
+        return tries
+
+
+def lnprob(x, e):
+    """mcmc.py:28-35: emcee-style callback; every exception maps to -inf."""
+    e.state.set_params(x)
+    try:
+        logp = e.state.get_logp(e.obs)
+    except Exception:
+        return -np.inf
+    return logp
+
+
+def _scales_vector(state, scales):
+    out = np.ones(state.Nvars)
+    for i, k in enumerate(state.get_rawkeys()):
+        if k in scales:
+            out[i] = scales[k]
+    return out
+
+
+class Ensemble(Mcmc):
+    """mcmc.py:40-75 -- same constructor and step() contract; emcee replaced by the device sampler."""
+
+    def __init__(self, initial_state, obs, scales, nwalkers=10, seed=None):
+        super(Ensemble, self).__init__(initial_state, obs)
+        self.set_scales(scales)
+        self.nwalkers = nwalkers
+        self.states = [self.state.get_params() for i in range(nwalkers)]
+        self.previous_states = [self.state.get_params() for i in range(nwalkers)]
+        self.lnprob = None
+        self.totalErrorCount = 0
+        for i, s in enumerate(self.states):
+            shift = 0.1e-2 * self.scales * np.random.normal(size=self.state.Nvars)
+            self.states[i] += shift
+        if seed is None:
+            seed = int(np.random.randint(0, 2 ** 62))
+        self.sampler = EnsembleSampler(nwalkers, self.state, obs, seed=seed)
+        self.sampler.set_positions(np.array(self.states))
+
+    def step(self):
+        self.previous_states = self.states
+        self.sampler.step()
+        self.states = list(self.sampler.gather_positions())
+        self.lnprob = self.sampler.gather_lnprob()
+        for i in range(len(self.states)):
+            for j in range(len(self.states[0])):
+                if self.previous_states[i][j] != self.states[i][j]:
+                    return True
+        return False
+
+    def set_scales(self, scales):
+        self.scales = _scales_vector(self.state, scales)
+
+
+class Mh(Mcmc):
+    """mcmc.py:80-121 -- one chain, numpy global RNG in the reference's draw order."""
+
+    def __init__(self, initial_state, obs):
+        super(Mh, self).__init__(initial_state, obs)
+        self.step_size = 3e-5
+
+    def generate_proposal(self):
+        prop = self.state.deepcopy()
+        shift = self.step_size * self.scales * np.random.normal(size=self.state.Nvars)
+        prop.shift_params(shift)
+        return prop
+
+    def set_scales(self, scales):
+        self.scales = _scales_vector(self.state, scales)
+
+    def step(self):
+        while True:
+            try:
+                logp = self.state.get_logp(self.obs)
+                proposal = self.generate_proposal()
+                if proposal.priorHard():
+                    return False
+                logp_proposal = proposal.get_logp(self.obs)
+                if np.exp(logp_proposal - logp) > np.random.uniform():
+                    self.state = proposal
+                    return True
+                return False
+            except Encounter:
+                return False
+
+
+class MhChains:
+    """n_chains independent Gaussian random-walk MH chains, all resident on the device.
+
+    Per step: one proposal kernel, one likelihood launch for all chains, one accept kernel
+    (mcmc.py:89-121 semantics per chain; priorHard / Encounter proposals are rejected through
+    logp = -inf)."""
+
+    def __init__(self, initial_state, obs, scales, step_size, n_chains, X0=None, seed=0, device=None):
+        import torch
+
+        self.state = initial_state.deepcopy()
+        self.obs = obs
+        self.dim = self.state.Nvars
+        self.n = int(n_chains)
+        self.step_size = float(step_size)
+        self.seed = int(seed)
+        self.iteration = 0
+        self.device = torch.device(device) if device is not None else engine.default_device()
+        self.lib = _lib.load()
+        self.pmap = self.state.param_map()
+        dt = self.state.integrator.step_for(self.state.planets)
+        self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, self.state.integrator.n_levels, self.n, self.device)
+        self.scales = torch.as_tensor(_scales_vector(self.state, scales), device=self.device)
+        if X0 is None:
+            X0 = np.tile(self.state.get_params()[:, None], (1, self.n))
+        self.X = torch.as_tensor(np.asarray(X0, dtype=np.float64), device=self.device).contiguous()
+        self.lnp, _, _ = self.plan.logl(self.pmap.to_kernel(self.X), hill_factor=self.state.hillRadiusFactor)
+        self.lnp = self.lnp.clone()
+        self.Q = torch.empty_like(self.X)
+        self.accepted = torch.zeros(self.n, dtype=torch.int32, device=self.device)
+
+    def step(self, draws_propose=None, draws_accept=None):
+        st = _lib.stream_handle()
+        _lib.check(self.lib.rvm_mh_propose(self.dim, self.n, 0, self.X.data_ptr(), self.scales.data_ptr(),
+                                           self.step_size, self.seed, self.iteration,
+                                           draws_propose.data_ptr() if draws_propose is not None else 0,
+                                           self.Q.data_ptr(), st), "rvm_mh_propose")
+        lnp_new, _, _ = self.plan.logl(self.pmap.to_kernel(self.Q), hill_factor=self.state.hillRadiusFactor)
+        _lib.check(self.lib.rvm_mh_accept(self.dim, self.n, 0, self.X.data_ptr(), self.lnp.data_ptr(),
+                                          self.Q.data_ptr(), lnp_new.data_ptr(), self.seed, self.iteration,
+                                          draws_accept.data_ptr() if draws_accept is not None else 0,
+                                          self.accepted.data_ptr(), st), "rvm_mh_accept")
+        self.iteration += 1
+
+
+from .smala import Smala, SmalaChains  # noqa: E402  (re-export with the reference's module layout)
+
+__all__ = ["Mcmc", "lnprob", "Ensemble", "Mh", "MhChains", "Smala", "SmalaChains", "EnsembleSampler"]

@@ -1,0 +1,216 @@
+"""SMALA (simplified manifold MALA with the SoftAbs metric), mcmc.py:126-187.
+
+The reference takes logp, its gradient and its Hessian from REBOUND's 1st/2nd-order variational
+equations (state.py:229-294).  Here (north-star: "SMALA with finite-difference grad logL") every
+derivative comes from ONE batched likelihood launch over the central-difference stencil
+(2P+1 parameter vectors per chain, `rvm_fd_params`):
+
+  grad_p logp  = (logp(x + e_p) - logp(x - e_p)) / (2 e_p)
+  J[e, p]      = (rv_e(x + e_p) - rv_e(x - e_p)) / (2 e_p)      (per-epoch model RV Jacobian)
+  H            = -(2 / Npoints) J^T diag(1/sigma^2) J          (Gauss-Newton Hessian of logp)
+
+The SoftAbs metric G = Q diag(lambda coth(alpha lambda)) Q^T of eig(-H) (mcmc.py:135-139), the
+drift mu = x + eps^2/2 G^-1 grad, the proposal x* = mu + eps chol(G^-1) z, and the Gaussian
+q-ratio (mcmc.py:144-187) follow the reference.  The Gauss-Newton Hessian drops the
+residual * d2rv term of the exact Hessian, so per-step parity with the reference SMALA is not
+defined; parity is statistical.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _lib, engine
+
+# relative FD step and per-key absolute floors (h, k and l can be ~0)
+FD_REL_STEP = 1e-6
+FD_FLOOR = {"m": 1e-4, "a": 1e-2, "h": 1e-2, "k": 1e-2, "l": 1.0, "ix": 1e-2, "iy": 1e-2}
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def fd_floor_vector(state):
+    return np.array([FD_FLOOR.get(k, 1e-2) for k in state.get_rawkeys()], dtype=np.float64)
+
+
+def fd_logp_grad_metric(state, obs, X, rel_step=FD_REL_STEP, pmap=None, hill_factor=None):
+    """X: [P][C] float64 device tensor -> (logp[C], grad[P][C], H[P][P][C], status[C])."""
+    torch = _torch()
+    lib = _lib.load()
+    P, C_ = X.shape
+    pmap = pmap or state.param_map()
+    fl = torch.as_tensor(fd_floor_vector(state), device=X.device)
+    S = 2 * P + 1
+    stencil = torch.empty((P, S * C_), dtype=torch.float64, device=X.device)
+    _lib.check(lib.rvm_fd_params(P, C_, X.contiguous().data_ptr(), float(rel_step), fl.data_ptr(),
+                                 stencil.data_ptr(), _lib.stream_handle()), "rvm_fd_params")
+    lp, st, rv = state.get_logp_batch(obs, stencil, hill_factor=hill_factor, want_rv=True, pmap=pmap)
+    lp = lp.view(S, C_)
+    st = st.view(S, C_)
+    rv = rv.view(-1, S, C_)
+    ax = torch.maximum(X.abs(), fl[:, None])
+    eps = rel_step * ax                                       # [P][C]
+    # the stencil kernel forms x +/- eps exactly as below; use the realised step for the divisor
+    xp = X + eps
+    xm = X - eps
+    den = (xp - xm)                                           # [P][C]
+    idx_p = torch.arange(P, device=X.device) * 2 + 1
+    grad = (lp[idx_p] - lp[idx_p + 1]) / den                  # [P][C]
+    J = (rv[:, idx_p, :] - rv[:, idx_p + 1, :]) / den[None]   # [E][P][C]
+    t, rvo, er = engine.obs_arrays(obs)
+    w = torch.as_tensor(1.0 / (er * er), device=X.device)     # [E]
+    H = -(2.0 / float(obs.Npoints)) * torch.einsum("epc,e,eqc->pqc", J, w, J)
+    # a chain is usable only if its whole stencil evaluated cleanly
+    bad = (st != 0).any(0)
+    status = torch.where(bad, torch.where(st[0] != 0, st[0], torch.full_like(st[0], 2)), st[0])
+    return lp[0], grad, H, status
+
+
+def softabs_inv(H, alpha):
+    """Batched SoftAbs: H [P][P][C] -> (Ginv [C][P][P], chol(Ginv) [C][P][P], logdet(Ginv) [C], ok [C])."""
+    torch = _torch()
+    A = (-H).permute(2, 0, 1).contiguous()                    # [C][P][P]
+    A = 0.5 * (A + A.transpose(1, 2))
+    lam, Q = torch.linalg.eigh(A)
+    al = alpha * lam
+    small = al.abs() < 1e-8
+    lt = torch.where(small, torch.full_like(lam, 1.0 / alpha), lam / torch.tanh(torch.where(small, torch.ones_like(al), al)))
+    inv = 1.0 / lt
+    Ginv = (Q * inv[:, None, :]) @ Q.transpose(1, 2)
+    Ginv = 0.5 * (Ginv + Ginv.transpose(1, 2))
+    L, info = torch.linalg.cholesky_ex(Ginv)
+    ok = (info == 0) & torch.isfinite(lt).all(1)
+    logdet = torch.log(inv).sum(1)
+    return Ginv, L, logdet, ok
+
+
+def _mvn_logpdf(x, mu, Ginv, logdetGinv, eps):
+    """log N(x; mu, eps^2 Ginv) for batches: x, mu [C][P]."""
+    torch = _torch()
+    P = x.shape[1]
+    d = (x - mu)[:, :, None]
+    cov = (eps * eps) * Ginv
+    sol = torch.linalg.solve(cov, d)
+    maha = (d * sol).sum((1, 2))
+    logdet = P * math.log(eps * eps) + logdetGinv
+    return -0.5 * (maha + logdet + P * math.log(2.0 * math.pi))
+
+
+class SmalaChains:
+    """C independent SMALA chains on the device (config 4: 256 chains)."""
+
+    def __init__(self, initial_state, obs, eps, alpha, n_chains, X0=None, seed=0, device=None, rel_step=FD_REL_STEP):
+        torch = _torch()
+        self.state = initial_state.deepcopy()
+        self.obs = obs
+        self.eps = float(eps)
+        self.alpha = float(alpha)
+        self.P = self.state.Nvars
+        self.n = int(n_chains)
+        self.rel_step = rel_step
+        self.device = torch.device(device) if device is not None else engine.default_device()
+        self.pmap = self.state.param_map()
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(seed))
+        if X0 is None:
+            X0 = np.tile(self.state.get_params()[:, None], (1, self.n))
+        self.X = torch.as_tensor(np.asarray(X0, dtype=np.float64), device=self.device).contiguous()
+        self.cache = self._derive(self.X)
+        self.accepted = torch.zeros(self.n, dtype=torch.int64, device=self.device)
+        self.linalg_failures = 0
+        self.iteration = 0
+
+    def _derive(self, X):
+        lp, g, H, st = fd_logp_grad_metric(self.state, self.obs, X, self.rel_step, self.pmap, hill_factor=1.0)
+        Ginv, L, logdet, ok = softabs_inv(H, self.alpha)
+        mu = X.t() + 0.5 * self.eps ** 2 * (Ginv @ g.t()[:, :, None])[:, :, 0]   # [C][P]
+        return dict(lp=lp, g=g, Ginv=Ginv, L=L, logdet=logdet, ok=ok & (st == 0), mu=mu)
+
+    def step(self, z=None, u=None):
+        torch = _torch()
+        c = self.cache
+        if z is None:
+            z = torch.randn((self.n, self.P), generator=self.gen, device=self.device, dtype=torch.float64)
+        if u is None:
+            u = torch.rand(self.n, generator=self.gen, device=self.device, dtype=torch.float64)
+        Xs = c["mu"] + self.eps * (c["L"] @ z[:, :, None])[:, :, 0]               # [C][P]
+        Xs = torch.where(c["ok"][:, None], Xs, self.X.t())
+        cs = self._derive(Xs.t().contiguous())
+        q_ts_t = _mvn_logpdf(Xs, c["mu"], c["Ginv"], c["logdet"], self.eps)
+        q_t_ts = _mvn_logpdf(self.X.t(), cs["mu"], cs["Ginv"], cs["logdet"], self.eps)
+        ratio = torch.exp(cs["lp"] - c["lp"] + q_t_ts - q_ts_t)
+        acc = (ratio > u) & cs["ok"] & c["ok"] & torch.isfinite(cs["lp"])
+        self.linalg_failures += int((~cs["ok"] & torch.isfinite(cs["lp"])).sum().item())
+        self.X = torch.where(acc[None, :], Xs.t(), self.X).contiguous()
+        for k in c:
+            v, vs = c[k], cs[k]
+            m = acc.view(1, -1) if k == "g" else acc.view((-1,) + (1,) * (v.dim() - 1))
+            c[k] = torch.where(m, vs, v)
+        self.accepted += acc.long()
+        self.iteration += 1
+        return acc
+
+
+class Smala:
+    """mcmc.py:126-187 with the reference's host-side control flow and numpy global RNG."""
+
+    def __init__(self, initial_state, obs, eps, alp):
+        from .mcmc import Mcmc  # noqa: F401 (class hierarchy mirrors the reference)
+
+        self.state = initial_state.deepcopy()
+        self.obs = obs
+        self.epsilon = eps
+        self.alpha = alp
+
+    def step_force(self):
+        tries = 1
+        while self.step() == False:  # noqa: E712
+            tries += 1
+        return tries
+
+    def softabs(self, hessians):  # mcmc.py:135-139
+        lam, Q = np.linalg.eigh(-0.5 * (hessians + hessians.T))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            lam_twig = np.where(np.abs(self.alpha * lam) < 1e-8, 1.0 / self.alpha, lam * 1. / np.tanh(self.alpha * lam))
+        return np.dot(Q, np.dot(np.diag(lam_twig), Q.T))
+
+    def generate_proposal(self):  # mcmc.py:144-153
+        logp, logp_d, logp_dd = self.state.get_logp_d_dd(self.obs)
+        Ginv = np.linalg.inv(self.softabs(logp_dd))
+        Ginvsqrt = np.linalg.cholesky(Ginv)
+        mu = self.state.get_params() + (self.epsilon) ** 2 * np.dot(Ginv, logp_d) / 2.
+        newparams = mu + self.epsilon * np.dot(Ginvsqrt, np.random.normal(0., 1., self.state.Nvars))
+        prop = self.state.deepcopy()
+        prop.set_params(newparams)
+        return prop
+
+    def transitionProbability(self, state_from, state_to):  # mcmc.py:158-162
+        from scipy import stats
+
+        logp, logp_d, logp_dd = state_from.get_logp_d_dd(self.obs)
+        Ginv = np.linalg.inv(self.softabs(logp_dd))
+        mu = state_from.get_params() + (self.epsilon) ** 2 * np.dot(Ginv, logp_d) / 2.
+        return stats.multivariate_normal.logpdf(state_to.get_params(), mean=mu, cov=(self.epsilon) ** 2 * Ginv)
+
+    def step(self):  # mcmc.py:167-187
+        from .state import Encounter
+
+        try:
+            stateStar = self.generate_proposal()
+            if stateStar.priorHard():
+                return False
+            q_ts_t = self.transitionProbability(self.state, stateStar)
+            q_t_ts = self.transitionProbability(stateStar, self.state)
+        except Encounter:
+            return False
+        except np.linalg.LinAlgError:
+            return False  # the reference quit()s the process here (mcmc.py:179-183); we reject
+        if np.exp(stateStar.logp - self.state.logp + q_t_ts - q_ts_t) > np.random.uniform():
+            self.state = stateStar
+            return True
+        return False

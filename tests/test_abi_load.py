@@ -1,0 +1,45 @@
+"""The C-ABI library loads on a CPU-only host and exports every symbol include/rvmcmc.h declares.
+
+No compute calls here (no GPU); the GPU tests exercise the same entry points."""
+import os
+import re
+
+from conftest import ROOT
+
+from rvmcmc import _lib
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "rvmcmc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rvm_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    fns = header_functions()
+    for f in ("rvm_plan_create", "rvm_logl_batch", "rvm_stretch_propose", "rvm_stretch_accept",
+              "rvm_mh_propose", "rvm_mh_accept", "rvm_fd_params", "rvm_last_error", "rvm_abi_version"):
+        assert f in fns
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    for f in header_functions():
+        assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
+    assert lib.rvm_abi_version() == 1
+
+
+def test_python_binding_matches_header():
+    assert set(_lib.SIGNATURES) == set(header_functions())
+
+
+def test_argument_errors_do_not_touch_the_device():
+    import ctypes as C
+
+    lib = _lib.load()
+    cfg = _lib.RvmConfig(0, 0.1, 4, 100.0)  # n_planets = 0 -> rejected before any HIP call
+    h = C.c_void_p()
+    z = (C.c_double * 1)(0.0)
+    rc = lib.rvm_plan_create(C.byref(cfg), z, z, z, 1, 64, C.byref(h))
+    assert rc < 0 and b"n_planets" in lib.rvm_last_error()
+    assert lib.rvm_logl_batch(None, 1, 0, 1.0, 0, 0, 0, 0) < 0

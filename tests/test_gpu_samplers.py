@@ -1,0 +1,166 @@
+"""Device samplers vs numpy restatements of the reference samplers with injected random numbers.
+
+* emcee 2.2.1 stretch move (EnsembleSampler.sample/_propose_stretch):
+  decisions must be identical to a numpy restatement fed the same (u1, u2, u3) draws, except
+  walkers with |lnpdiff - ln u3| < 1e-9 (counted; none expected at these sizes).
+* Metropolis-Hastings (mcmc.py:89-121) with injected N(0,1) and U(0,1).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import S2_PLANETS, S2_SCALES, s2_obs_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _state_and_obs():
+    from rvmcmc import state
+
+    s = state.State(planets=[dict(p) for p in S2_PLANETS])
+    return s, s2_obs_oracle()
+
+
+def _oracle_logl(X, s, obs, dt):
+    """X [W][dim] in the State's free-parameter order -> oracle logL with the kernel algorithm."""
+    pm = s.param_map()
+    P = np.stack([O.kernel_params_to_oracle(pm.vector_to_kernel_np(x)[:, None], 2)[0] for x in X])
+    return O.logl_whx_batch(P, 2, obs, dt, 4)[0]
+
+
+def numpy_stretch_half(p_s0, lnp_s0, c, u1, u2, u3, lnprob_fn, a=2.0):
+    """emcee 2.2.1 _propose_stretch + in-place update, restated (rows = walkers)."""
+    Ns, dim = p_s0.shape
+    Nc = len(c)
+    zz = ((a - 1.) * u1 + 1) ** 2. / a
+    rint = np.floor(u2 * Nc).astype(int)
+    q = c[rint] - zz[:, None] * (c[rint] - p_s0)
+    newlnp = lnprob_fn(q)
+    lnpdiff = (dim - 1.) * np.log(zz) + newlnp - lnp_s0
+    acc = lnpdiff > np.log(u3)
+    p = p_s0.copy()
+    l = lnp_s0.copy()
+    p[acc] = q[acc]
+    l[acc] = newlnp[acc]
+    return p, l, acc, np.abs(lnpdiff - np.log(u3))
+
+
+def test_stretch_decisions_match_numpy_emcee():
+    torch = _torch()
+    from rvmcmc.ensemble import EnsembleSampler
+
+    s, obs = _state_and_obs()
+    W, dim = 128, s.Nvars
+    rng = np.random.default_rng(0)
+    scales = np.array([S2_SCALES[k] for k in s.get_rawkeys()])
+    X0 = s.get_params()[None] + 1e-3 * scales * rng.standard_normal((W, dim))
+    ens = EnsembleSampler(W, s, obs, seed=1)
+    ens.set_positions(X0)
+    ens.compute_lnprob()
+    dt = ens.plan.dt
+    lnp0 = np.concatenate([l.cpu().numpy() for l in ens.lnp])
+    ref_lnp0 = _oracle_logl(X0, s, obs, dt)
+    np.testing.assert_allclose(lnp0, ref_lnp0, rtol=1e-12, atol=0)
+    n = W // 2
+    pos = [X0[:n].copy(), X0[n:].copy()]
+    lnp = [lnp0[:n].copy(), lnp0[n:].copy()]
+    near = 0
+    for it in range(3):
+        for half in (0, 1):
+            u1, u2, u3 = rng.random(n), rng.random(n), rng.random(n)
+            dp = torch.as_tensor(np.concatenate([u1, u2]), device="cuda")
+            da = torch.as_tensor(u3, device="cuda")
+            A, B = ens.pos[half], ens.pos[1 - half]
+            ens.half_step(A, ens.lnp[half], B, half, draws_propose=dp, draws_accept=da)
+            p_new, l_new, acc, margin = numpy_stretch_half(pos[half], lnp[half], pos[1 - half], u1, u2, u3,
+                                                           lambda q: _oracle_logl(q, s, obs, dt))
+            near += int((margin < 1e-9).sum())
+            pos[half], lnp[half] = p_new, l_new
+            got = ens.pos[half].t().cpu().numpy()
+            same = np.all(got == p_new, axis=1) | (margin < 1e-9)
+            assert same.all(), f"iteration {it} half {half}: {np.nonzero(~same)[0]}"
+            # keep both sides bit-identical for the next half-step
+            pos[half] = got
+            lnp[half] = ens.lnp[half].cpu().numpy()
+        ens.iteration += 1
+    assert near == 0
+
+
+def test_mh_chains_match_numpy():
+    torch = _torch()
+    from rvmcmc.mcmc import MhChains
+
+    s, obs = _state_and_obs()
+    C, dim = 64, s.Nvars
+    scales = {"m": 1.e-3, "a": 0.3, "h": 0.5, "k": 0.5, "l": np.pi / 2.}  # mcmc_benchmark_mh.py:52
+    mh = MhChains(s, obs, scales, 1e-3, C, seed=3)
+    dt = mh.plan.dt
+    sc = np.array([scales[k] for k in s.get_rawkeys()])
+    X = np.tile(s.get_params()[:, None], (1, C))
+    lnp = _oracle_logl(X.T, s, obs, dt)
+    rng = np.random.default_rng(5)
+    for it in range(3):
+        g = rng.standard_normal((dim, C))
+        u = rng.random(C)
+        mh.step(draws_propose=torch.as_tensor(g, device="cuda"), draws_accept=torch.as_tensor(u, device="cuda"))
+        Q = X + (1e-3 * sc)[:, None] * g
+        lq = _oracle_logl(Q.T, s, obs, dt)
+        acc = np.exp(lq - lnp) > u
+        X = np.where(acc[None], Q, X)
+        lnp = np.where(acc, lq, lnp)
+        got = mh.X.cpu().numpy()
+        np.testing.assert_array_equal(got, X)
+
+
+def test_ensemble_reproducible_and_moves():
+    from rvmcmc.ensemble import EnsembleSampler
+
+    s, obs = _state_and_obs()
+    W = 256
+    rng = np.random.default_rng(1)
+    scales = np.array([S2_SCALES[k] for k in s.get_rawkeys()])
+    X0 = s.get_params()[None] + 1e-3 * scales * rng.standard_normal((W, s.Nvars))
+    runs = []
+    for _ in range(2):
+        e = EnsembleSampler(W, s, obs, seed=42)
+        e.set_positions(X0)
+        for _ in range(5):
+            e.step()
+        runs.append((e.gather_positions(), e.gather_lnprob(), e.acceptance_fraction().cpu().numpy()))
+    np.testing.assert_array_equal(runs[0][0], runs[1][0])
+    assert 0.05 < runs[0][2].mean() < 0.95
+    assert np.isfinite(runs[0][1]).all()
+
+
+def test_reference_api_ensemble_and_mh_step():
+    from rvmcmc import mcmc
+
+    s, obs = _state_and_obs()
+    np.random.seed(0)
+    ens = mcmc.Ensemble(s, obs, scales=S2_SCALES, nwalkers=32)
+    moved = ens.step()
+    assert isinstance(moved, bool) and len(ens.states) == 32 and len(ens.lnprob) == 32
+    mh = mcmc.Mh(s, obs)
+    mh.set_scales({"m": 1.e-3, "a": 0.3, "h": 0.5, "k": 0.5, "l": np.pi / 2.})
+    mh.step_size = 1e-4
+    tries = mh.step_force()
+    assert tries >= 1 and np.isfinite(mh.state.logp)
+
+
+def test_smala_chains_run():
+    from rvmcmc.smala import SmalaChains
+
+    s, obs = _state_and_obs()
+    sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=16, seed=0)
+    for _ in range(5):
+        sm.step()
+    assert sm.iteration == 5
+    assert np.isfinite(sm.cache["lp"].cpu().numpy()).all()
+    assert int(sm.accepted.sum()) > 0

@@ -1,0 +1,127 @@
+"""Pin the CPU oracle against the reference's stored outputs.
+
+G1  (Ex)HD155358.ipynb:82-97   Pal -> Cartesian + move_to_com vectors          1 ulp
+G2  (Ex)HD155358.ipynb:149     logp of `sol` on HD155358.vels, Npoints=100     printed 12 digits
+G3  plotArchive/Ben's 2-1/log_Ben-2-1:4   1000-point RV curve                  printed 12 digits
+G4  (Ex)HD155358.ipynb:717-720 logp at a 9-significant-digit parameter vector  1e-6 relative
+Plus the T2 tier: the kernel's algorithm (Richardson-extrapolated WH, restated in C) against
+the IAS15 restatement at the default integrator settings.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import GOLDEN, S2_PLANETS, s2_obs_oracle
+
+# T2 tolerance: |logL_kernel_algorithm - logL_IAS15| (absolute) at default settings
+T2_LOGL_ABS = 1e-8
+
+
+def _sol_planets(sol):
+    return [{"m": sol[3], "a": sol[0], "h": sol[1], "k": sol[2], "l": sol[4]},
+            {"m": sol[8], "a": sol[5], "h": sol[6], "k": sol[7], "l": sol[9]}]
+
+
+def test_g1_pal_and_com(golden):
+    g = golden["G1"]
+    helio, bary = O.setup_vectors(g["planets"])
+    # heliocentric (before move_to_com): planets only, star at rest at origin
+    for b in range(3):
+        np.testing.assert_allclose(helio[b, 3:6], g["helio_v"][b], rtol=0, atol=3e-16)
+        np.testing.assert_allclose(helio[b, 0:3], g["helio_x"][b], rtol=0, atol=3e-16)
+        np.testing.assert_allclose(bary[b, 3:6], g["bary_v"][b], rtol=0, atol=3e-16)
+        np.testing.assert_allclose(bary[b, 0:3], g["bary_x"][b], rtol=0, atol=3e-16)
+    assert float("%.12g" % bary[0, 3]) == g["star_vx_print"]
+
+
+def test_g2_logp(golden, hd_obs_oracle):
+    g = golden["G2"]
+    lp, st = O.logl_ias15(_sol_planets(g["sol"]), hd_obs_oracle, hill_factor=g["hillRadiusFactor"])
+    assert st == 0
+    # Python 2 `print float` shows 12 significant digits
+    assert float("%.12g" % lp) == g["logp_print12"]
+
+
+def test_g3_rv_curve(golden):
+    g = golden["G3"]
+    d = np.load(os.path.join(GOLDEN, g["file"]))
+    obs = O.obs_from_file(os.path.join(GOLDEN, g["obs"]), Npoints=g["Npoints"])
+    times = np.linspace(obs.tb[0], obs.tf[len(obs.tf) - 1], 1000)  # state.py:79
+    np.testing.assert_allclose(times, d["t"], rtol=1e-11, atol=1e-10)
+    rv, st, _ = O.get_rv_ias15(g["planets"], times)
+    assert st == 0
+    # 12 printed significant digits of values ~5e-3
+    np.testing.assert_allclose(rv, d["rv"], rtol=0, atol=2e-14)
+
+
+def test_g4_logp(golden, hd_obs_oracle):
+    g = golden["G4"]
+    lp, st = O.logl_ias15(_sol_planets(g["params_9sig"]), hd_obs_oracle, hill_factor=1.0)
+    assert st == 0
+    assert abs(lp - g["logp_print"]) / abs(g["logp_print"]) < 1e-6  # parameters printed to 9 digits
+
+
+def test_obs_from_file_split(hd_obs_oracle):
+    o = hd_obs_oracle
+    assert len(o.tb) == 61 and len(o.tf) == 61
+    assert o.tb[-1] == 0.0 and o.tf[0] > 0
+    raw = np.loadtxt(os.path.join(GOLDEN, "HD155358.vels"))
+    np.testing.assert_array_equal(o.t, raw[:, 0] * 0.01720 - (raw[60, 0] * 0.01720))
+    np.testing.assert_array_equal(o.err, raw[:, 2] * 3.355e-5)
+
+
+def test_fake_obs_rng_order():
+    """observations.py:19-50 draw order: tf uniforms, tb uniforms, then (sigma, noise) per epoch."""
+    np.random.seed(7)
+    o = O.fake_obs(S2_PLANETS, Npoints=10, error=1.5e-4, errorVar=2.5e-5, tmax=12.)
+    np.random.seed(7)
+    tf = np.append([0], np.sort(np.random.uniform(0., 6., 5)))
+    tb = np.sort(np.random.uniform(0., -6., 5))
+    np.testing.assert_array_equal(o.tf, tf)
+    np.testing.assert_array_equal(o.tb, tb)
+    e0 = 1.5e-4 + np.random.normal(0., 2.5e-5)
+    assert o.errorf[0] == e0
+    assert len(o.rvf) == 6 and len(o.rvb) == 5 and o.Npoints == 10
+
+
+def test_prior_hard_thresholds():
+    base = [dict(p) for p in S2_PLANETS]
+    pl = O.pal_params(base)
+    assert O.lib().rvo_prior_hard(2, O._p(np.ascontiguousarray(pl)), 1, 0) == 0
+    for key, val in (("a", 0.02), ("m", 5e-6), ("h", 0.9999), ("k", -1.0)):
+        b = [dict(p) for p in base]
+        b[1][key] = val
+        if key == "h":
+            b[1]["k"] = 0.1
+        q = np.ascontiguousarray(O.pal_params(b))
+        assert O.lib().rvo_prior_hard(2, O._p(q), 1, 0) == 1, key
+
+
+def test_ias15_encounter_status():
+    pl = [{"m": 1e-3, "a": 1.0, "h": 0.0, "k": 0.0, "l": 0.0},
+          {"m": 1e-3, "a": 1.02, "h": 0.0, "k": 0.0, "l": 0.05}]
+    rv, st, _ = O.get_rv_ias15(pl, [5.0], hill_factor=1.0)
+    assert st == O.ORACLE_ENCOUNTER
+
+
+@pytest.mark.parametrize("which", ["HD", "S2"])
+def test_t2_kernel_algorithm_vs_ias15(which, hd_obs_oracle, golden):
+    """T2: Richardson-extrapolated WH (n_levels=4, dt = P_min/20) vs the IAS15 restatement."""
+    if which == "HD":
+        planets, obs = _sol_planets(golden["G2"]["sol"]), hd_obs_oracle
+    else:
+        planets, obs = S2_PLANETS, s2_obs_oracle()
+    pmin = min(2 * np.pi * np.sqrt(p["a"] ** 3 / (1 + p["m"])) for p in planets)
+    rng = np.random.default_rng(1)
+    base = O.pal_params(planets)
+    W = 12
+    params = np.repeat(base[None], W, 0)
+    params[:, :, :5] *= 1 + 1e-3 * rng.standard_normal((W, len(planets), 5))
+    ref, st_ref = O.logl_ias15_batch(params, len(planets), obs, hill_factor=1.0)
+    got, st = O.logl_whx_batch(params, len(planets), obs, pmin / 20.0, 4, hill_factor=1.0)
+    assert (st == st_ref).all()
+    ok = st == 0
+    assert ok.sum() >= W - 1
+    assert np.max(np.abs(got[ok] - ref[ok])) < T2_LOGL_ABS
