@@ -70,15 +70,20 @@ __device__ __forceinline__ void stumpff(double z, double& c0, double& c1, double
 // ---- Pal (2009) -> heliocentric Cartesian (coplanar); REBOUND reb_tools_pal_to_particle -------
 __device__ __forceinline__ void pal_to_cart(double mu, double a, double lam, double k, double h, double& X,
                                             double& Y, double& VX, double& VY) {
+    // Newton from F = lam; a lane stops updating at its own convergence (as a scalar loop would),
+    // so the result never depends on the other lanes of the wave.
     double F = lam;
+    bool done = false;
     for (int it = 0; it < 100; it++) {
         double sF, cF;
         sincos(F, &sF, &cF);
         const double fF = F - k * sF + h * cF - lam;
         const double dF = 1.0 - k * cF - h * sF;
         const double step = fF / dF;
-        F -= step;
-        const bool done = !(fabs(step) > 1e-16 * (fabs(F) > 1.0 ? fabs(F) : 1.0));
+        const double Fn = F - step;
+        const bool conv = !(fabs(step) > 1e-16 * (fabs(Fn) > 1.0 ? fabs(Fn) : 1.0));
+        F = done ? F : Fn;
+        done = done || conv;
         if (__all(done)) break;
     }
     double sF, cF;
@@ -118,8 +123,13 @@ __device__ __forceinline__ void drift(Sys<NP>& s, double dt) {
         zeta[p] = GM[p] - beta[p] * r0[p];
         X[p] = dt / r0[p] - dt * dt * eta[p] / (2.0 * r0[p] * r0[p] * r0[p]);
     }
+    // Halley iterations; each (lane, planet) freezes at its own convergence so that results are
+    // independent of the wave's other lanes (bit-reproducible across batch compositions).
+    bool done[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) done[p] = false;
     for (int it = 0; it < 50; it++) {
-        bool conv = true;
+        bool all = true;
 #pragma unroll
         for (int p = 0; p < NP; p++) {
             double c0, c1, c2, c3;
@@ -130,10 +140,13 @@ __device__ __forceinline__ void drift(Sys<NP>& s, double dt) {
             const double fp = r0[p] * c0 + eta[p] * G1 + GM[p] * G2;
             const double fpp = eta[p] * c0 + zeta[p] * G1;
             const double dX = f * fp / (fp * fp - 0.5 * f * fpp);
-            X[p] = x - dX;
-            conv = conv && !(fabs(dX) > 2e-16 * fabs(X[p]));
+            const double Xn = x - dX;
+            const bool conv = !(fabs(dX) > 2e-16 * fabs(Xn));
+            X[p] = done[p] ? x : Xn;
+            done[p] = done[p] || conv;
+            all = all && done[p];
         }
-        if (__all(conv)) break;
+        if (__all(all)) break;
     }
 #pragma unroll
     for (int p = 0; p < NP; p++) {

@@ -27,11 +27,11 @@ class IntegratorConfig:
     steps_per_orbit: level-1 steps per shortest orbital period of the reference state
                      (dt = P_min / steps_per_orbit) unless `dt` is given explicitly.
     n_levels:        Richardson levels; level L integrates with dt/(L+1).  n_levels=4 at
-                     steps_per_orbit=20 keeps |logL - logL_IAS15| ~1e-9 on the benchmark
-                     configs (tests/test_parity_gpu.py states the tolerance it enforces).
+                     steps_per_orbit=24 keeps |logL - logL_IAS15| <= ~1e-9 on the benchmark
+                     configs (T2 tier; tests/test_gpu_logl.py enforces 5e-9).
     """
 
-    steps_per_orbit: float = 20.0
+    steps_per_orbit: float = 24.0
     n_levels: int = 4
     dt: Optional[float] = None
 

@@ -33,9 +33,53 @@ def _torch():
     return torch
 
 
+class DeviceOps:
+    """The three per-half-step operations on the GPU, through librvmcmc.so: stretch proposal,
+    batched walker log-likelihood (the HIP kernel), stretch accept.  (The distributed tests inject
+    numpy restatements of these three to exercise the sharding logic on CPU with gloo.)"""
+
+    def __init__(self, sampler):
+        torch = _torch()
+        self.s = sampler
+        self.lib = _lib.load()
+        st = sampler.state
+        dt = st.integrator.step_for(st.planets)
+        self.plan = engine.plan_for(sampler.obs, sampler.pmap.n_planets, dt, st.integrator.n_levels, sampler.nloc,
+                                    sampler.device)
+        self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
+        self.status_counts = torch.zeros(4, dtype=torch.int64, device=sampler.device)
+
+    def propose(self, X0, c, half, q, z, draws=None):
+        s = self.s
+        _lib.check(self.lib.rvm_stretch_propose(s.dim, s.nloc, s.global_begin(half), X0.data_ptr(), s.halfk,
+                                                c.data_ptr(), s.a, s.seed, s.iteration, half,
+                                                draws.data_ptr() if draws is not None else 0, q.data_ptr(),
+                                                z.data_ptr(), _lib.stream_handle()), "rvm_stretch_propose")
+
+    def logl(self, X, out=None, status=None):
+        torch = _torch()
+        K = self.s.pmap.to_kernel(X)
+        if self.timing is not None:  # HIP events on the launch stream, around the likelihood launch only
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        lp, st, _ = self.plan.logl(K, hill_factor=self.s.hill_factor, out=out, status=status)
+        if self.timing is not None:
+            e1.record()
+            self.timing.append((e0, e1, X.shape[1]))
+        self.status_counts.index_add_(0, st.long(), torch.ones_like(st, dtype=torch.int64))
+        return lp, st
+
+    def accept(self, X0, lnp0, q, lnp_new, z, half, accepted, draws=None):
+        s = self.s
+        _lib.check(self.lib.rvm_stretch_accept(s.dim, s.nloc, s.global_begin(half), X0.data_ptr(), lnp0.data_ptr(),
+                                               q.data_ptr(), lnp_new.data_ptr(), z.data_ptr(), s.seed, s.iteration,
+                                               half, draws.data_ptr() if draws is not None else 0,
+                                               accepted.data_ptr(), _lib.stream_handle()), "rvm_stretch_accept")
+
+
 class EnsembleSampler:
     def __init__(self, nwalkers, state, obs, a=2.0, seed=0, device=None, hill_factor=None, group=None,
-                 pmap=None):
+                 pmap=None, ops=None):
         torch = _torch()
         dim = state.Nvars
         if nwalkers % 2 != 0:
@@ -51,8 +95,7 @@ class EnsembleSampler:
         self.pmap = pmap or state.param_map()
         self.hill_factor = state.hillRadiusFactor if hill_factor is None else float(hill_factor)
         self.device = torch.device(device) if device is not None else engine.default_device()
-        self.lib = _lib.load()
-        # distributed layout
+        # distributed layout: rank r owns walkers [r*nloc, (r+1)*nloc) of each half
         self.group = group
         if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
             self.rank = torch.distributed.get_rank(group)
@@ -62,10 +105,10 @@ class EnsembleSampler:
         self.halfk = self.k // 2
         if self.halfk % self.world != 0:
             raise ValueError("nwalkers/2 must be divisible by the world size")
-        self.nloc = self.halfk // self.world  # local walkers per half
+        self.nloc = self.halfk // self.world
         self.iteration = 0
-        dt = state.integrator.step_for(state.planets)
-        self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, state.integrator.n_levels, self.nloc, self.device)
+        self.ops = ops(self) if ops is not None else DeviceOps(self)
+        self.plan = getattr(self.ops, "plan", None)
         n = self.nloc
         f64 = dict(dtype=torch.float64, device=self.device)
         self._q = torch.empty((dim, n), **f64)
@@ -76,8 +119,14 @@ class EnsembleSampler:
         self._gather = torch.empty(self.world * dim * n, **f64) if self.world > 1 else None
         self.naccepted = torch.zeros(2 * n, dtype=torch.int32, device=self.device)
         self.nevals = 0
-        self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
-        self.status_counts = torch.zeros(4, dtype=torch.int64, device=self.device)
+
+    @property
+    def timing(self):
+        return getattr(self.ops, "timing", None)
+
+    @timing.setter
+    def timing(self, v):
+        self.ops.timing = v
 
     # ---- global <-> local indexing ------------------------------------------------------------
     def global_begin(self, half):
@@ -88,17 +137,8 @@ class EnsembleSampler:
         return (slice(self.global_begin(0), self.global_begin(0) + self.nloc),
                 slice(self.global_begin(1), self.global_begin(1) + self.nloc))
 
-    # ---- likelihood ---------------------------------------------------------------------------
     def lnprob(self, X, out=None, status=None):
-        K = self.pmap.to_kernel(X)
-        if self.timing is not None:  # HIP events on the launch stream, around the likelihood launch only
-            torch = _torch()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        lp, st, _ = self.plan.logl(K, hill_factor=self.hill_factor, out=out, status=status)
-        if self.timing is not None:
-            e1.record()
-            self.timing.append((e0, e1, X.shape[1]))
+        lp, st = self.ops.logl(X, out=out, status=status)
         self.nevals += X.shape[1]
         return lp, st
 
@@ -114,23 +154,12 @@ class EnsembleSampler:
 
     def half_step(self, X0, lnp0, Xc, half, draws_propose=None, draws_accept=None):
         """Update this rank's slice X0 [dim][nloc] (in place) against the complement half."""
-        st = _lib.stream_handle()
         c = self._complement(Xc)
         n = self.nloc
-        b = self.global_begin(half)
-        _lib.check(self.lib.rvm_stretch_propose(self.dim, n, b, X0.data_ptr(), self.halfk, c.data_ptr(), self.a,
-                                                self.seed, self.iteration, half,
-                                                draws_propose.data_ptr() if draws_propose is not None else 0,
-                                                self._q.data_ptr(), self._z.data_ptr(), st), "rvm_stretch_propose")
+        self.ops.propose(X0, c, half, self._q, self._z, draws_propose)
         self.lnprob(self._q, out=self._lnp_new, status=self._status)
-        acc = self.naccepted[half * n:(half + 1) * n]
-        _lib.check(self.lib.rvm_stretch_accept(self.dim, n, b, X0.data_ptr(), lnp0.data_ptr(), self._q.data_ptr(),
-                                               self._lnp_new.data_ptr(), self._z.data_ptr(), self.seed,
-                                               self.iteration, half,
-                                               draws_accept.data_ptr() if draws_accept is not None else 0,
-                                               acc.data_ptr(), st), "rvm_stretch_accept")
-        self.status_counts.index_add_(0, self._status.long(),
-                                      _torch().ones_like(self._status, dtype=_torch().int64))
+        self.ops.accept(X0, lnp0, self._q, self._lnp_new, self._z, half, self.naccepted[half * n:(half + 1) * n],
+                        draws_accept)
 
     # ---- ensemble state ------------------------------------------------------------------------
     def set_positions(self, X_global):

@@ -67,7 +67,7 @@ def test_stretch_decisions_match_numpy_emcee():
     dt = ens.plan.dt
     lnp0 = np.concatenate([l.cpu().numpy() for l in ens.lnp])
     ref_lnp0 = _oracle_logl(X0, s, obs, dt)
-    np.testing.assert_allclose(lnp0, ref_lnp0, rtol=1e-12, atol=0)
+    np.testing.assert_allclose(lnp0, ref_lnp0, rtol=7e-11, atol=0)  # T1 (4 levels)
     n = W // 2
     pos = [X0[:n].copy(), X0[n:].copy()]
     lnp = [lnp0[:n].copy(), lnp0[n:].copy()]

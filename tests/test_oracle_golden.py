@@ -16,7 +16,7 @@ import oracle as O
 from conftest import GOLDEN, S2_PLANETS, s2_obs_oracle
 
 # T2 tolerance: |logL_kernel_algorithm - logL_IAS15| (absolute) at default settings
-T2_LOGL_ABS = 1e-8
+T2_LOGL_ABS = 5e-9
 
 
 def _sol_planets(sol):
@@ -108,7 +108,7 @@ def test_ias15_encounter_status():
 
 @pytest.mark.parametrize("which", ["HD", "S2"])
 def test_t2_kernel_algorithm_vs_ias15(which, hd_obs_oracle, golden):
-    """T2: Richardson-extrapolated WH (n_levels=4, dt = P_min/20) vs the IAS15 restatement."""
+    """T2: Richardson-extrapolated WH (n_levels=4, dt = P_min/24) vs the IAS15 restatement."""
     if which == "HD":
         planets, obs = _sol_planets(golden["G2"]["sol"]), hd_obs_oracle
     else:
@@ -116,11 +116,11 @@ def test_t2_kernel_algorithm_vs_ias15(which, hd_obs_oracle, golden):
     pmin = min(2 * np.pi * np.sqrt(p["a"] ** 3 / (1 + p["m"])) for p in planets)
     rng = np.random.default_rng(1)
     base = O.pal_params(planets)
-    W = 12
+    W = 24
     params = np.repeat(base[None], W, 0)
     params[:, :, :5] *= 1 + 1e-3 * rng.standard_normal((W, len(planets), 5))
     ref, st_ref = O.logl_ias15_batch(params, len(planets), obs, hill_factor=1.0)
-    got, st = O.logl_whx_batch(params, len(planets), obs, pmin / 20.0, 4, hill_factor=1.0)
+    got, st = O.logl_whx_batch(params, len(planets), obs, pmin / 24.0, 4, hill_factor=1.0)
     assert (st == st_ref).all()
     ok = st == 0
     assert ok.sum() >= W - 1
