@@ -189,6 +189,16 @@ def logl_whx_batch(params, np_, obs, dt, n_levels, hill_factor=1.0, has_hk=1, ha
     return out, st
 
 
+def min_distance_ratio(params, np_, obs, dt, n_levels):
+    """Closest pair approach / exit distance seen by the WH restatement (diagnostic)."""
+    L = lib()
+    L.rvo_debug_min_ratio.restype = C.c_double
+    L.rvo_debug_min_ratio.argtypes = [C.c_int]
+    L.rvo_debug_min_ratio(1)
+    logl_whx_batch(params, np_, obs, dt, n_levels)
+    return float(np.sqrt(L.rvo_debug_min_ratio(1)))
+
+
 def kernel_params_to_oracle(K, n_planets):
     """kernel SoA [5*np][W] (m,a,h,k,l) -> oracle [W][np][7]."""
     K = np.asarray(K, dtype=np.float64)

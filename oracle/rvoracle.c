@@ -610,7 +610,42 @@ static void stumpff(double z, double* c0, double* c1, double* c2, double* c3) {
     *c3 = C3;
 }
 
-/* universal-variable Kepler drift of (r, v) about mass GM by dt; returns 0 ok, 1 no convergence */
+/* Bracketed universal-Kepler solve (the kernel's rare-case path): f(X) = r0 G1 + eta0 G2 + GM G3 - dt
+ * increases with X and f(0) = -dt; double from dt/r0 until the sign changes, then Halley steps,
+ * replaced by bisection when they leave the bracket, to full convergence. */
+static double kepler_safe(double r0, double eta0, double zeta0, double beta, double GM, double dt) {
+    const double sgn = dt >= 0.0 ? 1.0 : -1.0;
+    double lo = 0.0, hi = dt / r0, c0, c1, c2, c3;
+    for (int i = 0; i < 200; i++) {
+        stumpff(beta * hi * hi, &c0, &c1, &c2, &c3);
+        const double f = r0 * hi * c1 + eta0 * hi * hi * c2 + GM * hi * hi * hi * c3 - dt;
+        if (sgn * f > 0.0 || f != f) break;
+        lo = hi;
+        hi *= 2.0;
+    }
+    double X = 0.5 * (lo + hi);
+    for (int i = 0; i < 200; i++) {
+        stumpff(beta * X * X, &c0, &c1, &c2, &c3);
+        const double G1 = X * c1, G2 = X * X * c2, G3 = X * X * X * c3;
+        const double f = r0 * G1 + eta0 * G2 + GM * G3 - dt;
+        const double fp = r0 * c0 + eta0 * G1 + GM * G2;
+        const double fpp = eta0 * c0 + zeta0 * G1;
+        if (sgn * f > 0.0)
+            hi = X;
+        else
+            lo = X;
+        double Xn = X - f * fp / (fp * fp - 0.5 * f * fpp);
+        if (!(sgn * (Xn - lo) > 0.0 && sgn * (hi - Xn) > 0.0)) Xn = 0.5 * (lo + hi);
+        const int conv = !(fabs(Xn - X) > 2e-16 * fabs(Xn)) || lo == hi;
+        X = Xn;
+        if (conv) break;
+    }
+    return X;
+}
+
+/* universal-variable Kepler drift of (r, v) about mass GM by dt; returns 0 ok, 1 no convergence.
+ * Small steps (|beta| (dt/r0)^2 <= 0.5): Halley from a Taylor guess; otherwise (or without
+ * convergence in 8 iterations) the bracketed solve. */
 static int kepler_drift(double GM, double* r, double* v, double dt) {
     const double r0 = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
     const double v2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
@@ -620,23 +655,27 @@ static int kepler_drift(double GM, double* r, double* v, double dt) {
     double X = dt / r0 - dt * dt * eta0 / (2.0 * r0 * r0 * r0);
     double c0, c1, c2, c3, G1 = 0, G2 = 0, G3 = 0, rr = r0;
     int ok = 0;
-    for (int it = 0; it < 50; it++) {
-        stumpff(beta * X * X, &c0, &c1, &c2, &c3);
-        G1 = X * c1;
-        G2 = X * X * c2;
-        G3 = X * X * X * c3;
-        const double G0 = c0;
-        const double f = r0 * G1 + eta0 * G2 + GM * G3 - dt;
-        rr = r0 * G0 + eta0 * G1 + GM * G2;
-        const double fpp = eta0 * G0 + zeta0 * G1;
-        /* Halley */
-        const double dX = f * rr / (rr * rr - 0.5 * f * fpp);
-        X -= dX;
-        if (fabs(dX) <= 2e-16 * fabs(X) || dX == 0.0) {
-            ok = 1;
-            break;
+    const int small = fabs(beta) * (dt / r0) * (dt / r0) <= 0.5;
+    if (small) {
+        for (int it = 0; it < 8; it++) {
+            stumpff(beta * X * X, &c0, &c1, &c2, &c3);
+            G1 = X * c1;
+            G2 = X * X * c2;
+            G3 = X * X * X * c3;
+            const double G0 = c0;
+            const double f = r0 * G1 + eta0 * G2 + GM * G3 - dt;
+            rr = r0 * G0 + eta0 * G1 + GM * G2;
+            const double fpp = eta0 * G0 + zeta0 * G1;
+            /* Halley */
+            const double dX = f * rr / (rr * rr - 0.5 * f * fpp);
+            X -= dX;
+            if (fabs(dX) <= 2e-16 * fabs(X) || dX == 0.0) {
+                ok = 1;
+                break;
+            }
         }
     }
+    if (!ok) X = kepler_safe(r0, eta0, zeta0, beta, GM, dt);
     stumpff(beta * X * X, &c0, &c1, &c2, &c3);
     G1 = X * c1;
     G2 = X * X * c2;
@@ -652,7 +691,7 @@ static int kepler_drift(double GM, double* r, double* v, double dt) {
         r[c] = rn;
         v[c] = vn;
     }
-    return ok ? 0 : 1;
+    return 0;
 }
 
 typedef struct {
@@ -706,6 +745,14 @@ static int wh_drift(wh_state* s, double h) {
     return bad;
 }
 
+/* diagnostics: smallest pair-distance^2 / exit-distance^2 seen by wh_kick since the last reset */
+static double g_min_ratio = 1e300;
+double rvo_debug_min_ratio(int reset) {
+    const double v = g_min_ratio;
+    if (reset) g_min_ratio = 1e300;
+    return v;
+}
+
 static void wh_kick(wh_state* s, double h) {
     const int np = s->np;
     double x[RVO_MAXB][3]; /* heliocentric positions, star at origin */
@@ -722,6 +769,7 @@ static void wh_kick(wh_state* s, double h) {
             const double dx = x[j][0] - x[i][0], dy = x[j][1] - x[i][1], dz = x[j][2] - x[i][2];
             const double r2 = dx * dx + dy * dy + dz * dz;
             if (r2 < s->dmin2) s->enc = 1;
+            if (s->dmin2 > 0.0 && r2 / s->dmin2 < g_min_ratio) g_min_ratio = r2 / s->dmin2;
             const double ir3 = 1.0 / (r2 * sqrt(r2));
             acc[i][0] += s->m[j] * ir3 * dx;
             acc[i][1] += s->m[j] * ir3 * dy;

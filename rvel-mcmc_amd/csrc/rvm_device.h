@@ -11,47 +11,60 @@
 //     kick from the pairwise forces minus the Kepler part.
 //   * The encounter test of REBOUND's exit_min_distance (state.py:46) on every pair at every kick.
 //
-// Everything is fp64; one lane = one (walker, direction, extrapolation level).
+// Everything is fp64; one lane = one (walker, planet, direction, extrapolation level).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace rvm {
 
+// ---- fp64 reciprocal / reciprocal-sqrt: hardware estimate + two Newton steps --------------------
+// The compiler's IEEE division / sqrt expansions are ~10 dependent instructions each; the hot loop
+// only needs faithfully rounded results, which v_rcp_f64 / v_rsq_f64 plus two Newton-Raphson
+// refinements give in 5 dependent FMAs.
+__device__ __forceinline__ double rcp_nr(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
+__device__ __forceinline__ double rsq_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double e = fma(-x * y, y, 1.0);  // 1 - x y^2
+    y = fma(0.5 * y, e, y);
+    e = fma(-x * y, y, 1.0);
+    return fma(0.5 * y, e, y);
+}
+
 // ---- Stumpff functions c0..c3 (Danby): series for |z| <= 1, quartering+doubling otherwise ------
 __device__ __forceinline__ void stumpff(double z, double& c0, double& c1, double& c2, double& c3) {
-    // c2 = sum_j (-z)^j / (2j+2)!,  c3 = sum_j (-z)^j / (2j+3)!  (10 terms: error < z^10/22! )
+    // c2 = sum_j (-z)^j / (2j+2)!,  c3 = sum_j (-z)^j / (2j+3)!   (8 terms: error < z^8/18! <= 1e-19
+    // for |z| <= 0.5; the level-1 step keeps |z| = (n dt)^2 <~ 0.07 on the benchmark configs)
     int n = 0;
-    while (fabs(z) > 1.0 && n < 40) {  // rare: only for large steps / hyperbolic orbits
+    while (fabs(z) > 0.5 && n < 40) {  // rare: only for large steps / hyperbolic orbits
         z *= 0.25;
         n++;
     }
-    const double i2[10] = {1.0 / 2.0,
-                           1.0 / 24.0,
-                           1.0 / 720.0,
-                           1.0 / 40320.0,
-                           1.0 / 3628800.0,
-                           1.0 / 479001600.0,
-                           1.0 / 87178291200.0,
-                           1.0 / 20922789888000.0,
-                           1.0 / 6402373705728000.0,
-                           1.0 / 2432902008176640000.0};
-    const double i3[10] = {1.0 / 6.0,
-                           1.0 / 120.0,
-                           1.0 / 5040.0,
-                           1.0 / 362880.0,
-                           1.0 / 39916800.0,
-                           1.0 / 6227020800.0,
-                           1.0 / 1307674368000.0,
-                           1.0 / 355687428096000.0,
-                           1.0 / 121645100408832000.0,
-                           1.0 / 51090942171709440000.0};
-    double a2 = i2[9], a3 = i3[9];
-#pragma unroll
-    for (int j = 8; j >= 0; j--) {
-        a2 = i2[j] - z * a2;
-        a3 = i3[j] - z * a3;
-    }
+    double a2 = 1.0 / 6402373705728000.0;     // 1/18!
+    double a3 = 1.0 / 121645100408832000.0;   // 1/19!
+    a2 = 1.0 / 20922789888000.0 - z * a2;     // 1/16!
+    a3 = 1.0 / 355687428096000.0 - z * a3;    // 1/17!
+    a2 = 1.0 / 87178291200.0 - z * a2;        // 1/14!
+    a3 = 1.0 / 1307674368000.0 - z * a3;      // 1/15!
+    a2 = 1.0 / 479001600.0 - z * a2;          // 1/12!
+    a3 = 1.0 / 6227020800.0 - z * a3;         // 1/13!
+    a2 = 1.0 / 3628800.0 - z * a2;            // 1/10!
+    a3 = 1.0 / 39916800.0 - z * a3;           // 1/11!
+    a2 = 1.0 / 40320.0 - z * a2;              // 1/8!
+    a3 = 1.0 / 362880.0 - z * a3;             // 1/9!
+    a2 = 1.0 / 720.0 - z * a2;                // 1/6!
+    a3 = 1.0 / 5040.0 - z * a3;               // 1/7!
+    a2 = 1.0 / 24.0 - z * a2;                 // 1/4!
+    a3 = 1.0 / 120.0 - z * a3;                // 1/5!
+    a2 = 0.5 - z * a2;                        // 1/2!
+    a3 = 1.0 / 6.0 - z * a3;                  // 1/3!
     double C2 = a2, C3 = a3;
     double C1 = 1.0 - z * C3;
     double C0 = 1.0 - z * C2;
@@ -98,81 +111,198 @@ __device__ __forceinline__ void pal_to_cart(double mu, double a, double lam, dou
     VY = fac * ((1.0 - k * k * beta) * cF - h * k * beta * sF);
 }
 
-// ---- the Jacobi-coordinate state of one lane ---------------------------------------------------
+// ---- lane layout: the planets of one walker live on L adjacent lanes ----------------------------
+// L = lanes per walker (1, 2 or 4): planet p of a walker runs on lane (group base + p), so every
+// Kepler drift runs on its own lane and the kick exchanges positions inside the lane group with
+// DPP quad permutes (no LDS).  NP = 3 uses L = 4 with the 4th lane shadowing planet 3.
 template <int NP>
-struct Sys {
-    double rx[NP], ry[NP], vx[NP], vy[NP];  // Jacobi coordinates of planets 1..NP
-    double m[NP];                           // planet masses
-    double Mi[NP + 1];                      // interior masses, Mi[0] = M_star = 1
-    double dmin2;                           // (hill_factor * max r_Hill)^2
-    int enc;                                // encounter flag
+struct LanesPerWalker {
+    static constexpr int value = NP == 1 ? 1 : (NP == 2 ? 2 : 4);
 };
 
-// Kepler drift of every Jacobi coordinate by dt, jointly (independent chains -> ILP).
-template <int NP>
-__device__ __forceinline__ void drift(Sys<NP>& s, double dt) {
-    double r0[NP], eta[NP], beta[NP], zeta[NP], X[NP], GM[NP];
-#pragma unroll
-    for (int p = 0; p < NP; p++) {
-        GM[p] = s.Mi[p + 1];
-        const double rr = s.rx[p] * s.rx[p] + s.ry[p] * s.ry[p];
-        r0[p] = sqrt(rr);
-        const double v2 = s.vx[p] * s.vx[p] + s.vy[p] * s.vy[p];
-        eta[p] = s.rx[p] * s.vx[p] + s.ry[p] * s.vy[p];
-        beta[p] = 2.0 * GM[p] / r0[p] - v2;
-        zeta[p] = GM[p] - beta[p] * r0[p];
-        X[p] = dt / r0[p] - dt * dt * eta[p] / (2.0 * r0[p] * r0[p] * r0[p]);
-    }
-    // Halley iterations; each (lane, planet) freezes at its own convergence so that results are
-    // independent of the wave's other lanes (bit-reproducible across batch compositions).
-    bool done[NP];
-#pragma unroll
-    for (int p = 0; p < NP; p++) done[p] = false;
-    for (int it = 0; it < 50; it++) {
-        bool all = true;
-#pragma unroll
-        for (int p = 0; p < NP; p++) {
-            double c0, c1, c2, c3;
-            stumpff(beta[p] * X[p] * X[p], c0, c1, c2, c3);
-            const double x = X[p];
-            const double G1 = x * c1, G2 = x * x * c2, G3 = x * x * x * c3;
-            const double f = r0[p] * G1 + eta[p] * G2 + GM[p] * G3 - dt;
-            const double fp = r0[p] * c0 + eta[p] * G1 + GM[p] * G2;
-            const double fpp = eta[p] * c0 + zeta[p] * G1;
-            const double dX = f * fp / (fp * fp - 0.5 * f * fpp);
-            const double Xn = x - dX;
-            const bool conv = !(fabs(dX) > 2e-16 * fabs(Xn));
-            X[p] = done[p] ? x : Xn;
-            done[p] = done[p] || conv;
-            all = all && done[p];
-        }
-        if (__all(all)) break;
-    }
-#pragma unroll
-    for (int p = 0; p < NP; p++) {
-        double c0, c1, c2, c3;
-        const double x = X[p];
-        stumpff(beta[p] * x * x, c0, c1, c2, c3);
-        const double G1 = x * c1, G2 = x * x * c2, G3 = x * x * x * c3;
-        const double rr = r0[p] * c0 + eta[p] * G1 + GM[p] * G2;
-        const double f = 1.0 - GM[p] * G2 / r0[p];
-        const double g = dt - GM[p] * G3;
-        const double fd = -GM[p] * G1 / (rr * r0[p]);
-        const double gd = 1.0 - GM[p] * G2 / rr;
-        const double nrx = f * s.rx[p] + g * s.vx[p];
-        const double nry = f * s.ry[p] + g * s.vy[p];
-        const double nvx = fd * s.rx[p] + gd * s.vx[p];
-        const double nvy = fd * s.ry[p] + gd * s.vy[p];
-        s.rx[p] = nrx;
-        s.ry[p] = nry;
-        s.vx[p] = nvx;
-        s.vy[p] = nvy;
+// value of `v` held by lane Q of this lane's group (Q is a compile-time planet index)
+template <int L, int Q>
+__device__ __forceinline__ double grp_get(double v) {
+    if constexpr (L == 1) {
+        return v;
+    } else {
+        // quad_perm selects: L = 2 groups are lanes {0,1} and {2,3} of each quad, L = 4 the quad
+        constexpr int q = Q % L;
+        constexpr int ctrl = (L == 2) ? (q | (q << 2) | ((q + 2) << 4) | ((q + 2) << 6))
+                                      : (q | (q << 2) | (q << 4) | (q << 6));
+        const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, false);
+        const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, false);
+        return __hiloint2double(hi, lo);
     }
 }
 
-// Interaction kick by dt (and the encounter test on every pair at the kick positions).
+// runtime planet index (folds to a constant inside unrolled loops)
+template <int L>
+__device__ __forceinline__ double grp_get(double v, int q) {
+    switch (q) {
+        case 0:
+            return grp_get<L, 0>(v);
+        case 1:
+            return grp_get<L, 1>(v);
+        case 2:
+            return grp_get<L, 2>(v);
+        default:
+            return grp_get<L, 3>(v);
+    }
+}
+
+// One lane: one planet's Jacobi coordinate plus the walker-wide constants every lane needs.
 template <int NP>
-__device__ __forceinline__ void kick(Sys<NP>& s, double dt) {
+struct Lane {
+    double rx, ry, vx, vy;  // own Jacobi coordinate
+    double r, ir;           // |r'| and 1/|r'| at the current positions (carried from the drift)
+    double GM;              // interior mass M_p (G = 1) of the own Jacobi coordinate
+    double m[NP];           // planet masses
+    double iMi[NP + 1];     // 1 / interior masses, iMi[0] = 1 (M_star = 1)
+    double mu[NP];          // m_q / M_q: star barycentric velocity weights
+    double dmin2;           // (hill_factor * max r_Hill)^2
+    int p;                  // own planet index (lane % L, clamped to NP-1)
+    int enc;                // encounter flag (identical on all lanes of the group)
+};
+
+// Safeguarded universal-Kepler solve for the rare hard cases (a step spanning a large part of an
+// orbit, a poor initial guess): f(X) = r0 G1 + eta0 G2 + GM G3 - dt is increasing in X (f' = r > 0)
+// with f(0) = -dt, so the root is bracketed by doubling from dt/r0 and Halley steps that leave
+// the bracket are replaced by bisection.  Returns the G-functions at the converged X.
+__device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, double beta, double GM, double dt,
+                                         double& Xo, double& G0, double& G1, double& G2, double& G3) {
+    const double sgn = dt >= 0.0 ? 1.0 : -1.0;
+    double lo = 0.0, hi = dt / r0;
+    double c0, c1, c2, c3;
+    for (int i = 0; i < 200; i++) {  // expand until sgn*f(hi) > 0
+        stumpff(beta * hi * hi, c0, c1, c2, c3);
+        const double f = r0 * hi * c1 + eta * hi * hi * c2 + GM * hi * hi * hi * c3 - dt;
+        if (sgn * f > 0.0 || !(f == f)) break;
+        lo = hi;
+        hi *= 2.0;
+    }
+    double X = 0.5 * (lo + hi);
+    for (int i = 0; i < 200; i++) {
+        stumpff(beta * X * X, c0, c1, c2, c3);
+        const double g1 = X * c1, g2 = X * X * c2, g3 = X * X * X * c3;
+        const double f = r0 * g1 + eta * g2 + GM * g3 - dt;
+        const double fp = r0 * c0 + eta * g1 + GM * g2;
+        const double fpp = eta * c0 + zeta * g1;
+        if (sgn * f > 0.0)
+            hi = X;
+        else
+            lo = X;
+        double Xn = X - f * fp / (fp * fp - 0.5 * f * fpp);
+        if (!(sgn * (Xn - lo) > 0.0 && sgn * (hi - Xn) > 0.0)) Xn = 0.5 * (lo + hi);
+        const bool conv = !(fabs(Xn - X) > 2e-16 * fabs(Xn)) || lo == hi;
+        X = Xn;
+        if (conv) break;
+    }
+    stumpff(beta * X * X, c0, c1, c2, c3);
+    Xo = X;
+    G0 = c0;
+    G1 = X * c1;
+    G2 = X * X * c2;
+    G3 = X * X * X * c3;
+}
+
+// Kepler drift of the own Jacobi coordinate by dt in universal variables (Danby): solve
+// r0 G1 + eta0 G2 + GM G3 = dt for X by Halley iterations from the third-order Taylor guess
+//   X = dt/r0 - eta0 dt^2/(2 r0^3) + dt^3 (3 eta0^2/r0^5 - v0^2/r0^3 + GM/r0^4)/6.
+// Halley converges cubically, so for small steps (|beta X^2| <= 0.5) once a correction is
+// <= 1e-6 |X| the remaining error is below 1e-18 |X| and the lane stops (large steps iterate to
+// full convergence) (each lane at its own convergence: results do not depend on the
+// other lanes of the wave).  The G-functions at the final X = x + d are Taylor-updated from the
+// last evaluation at x (dG0/dX = -beta G1, dG_k/dX = G_{k-1}), and |r| after the drift comes out
+// of the solution (r = r0 G0 + eta0 G1 + GM G2): no square root anywhere in the step.
+template <int NP>
+__device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
+    const double GM = s.GM, r0 = s.r, ir0 = s.ir;
+    const double v2 = s.vx * s.vx + s.vy * s.vy;
+    const double eta = s.rx * s.vx + s.ry * s.vy;
+    const double beta = 2.0 * GM * ir0 - v2;
+    const double zeta = GM - beta * r0;
+    const double i2 = ir0 * ir0;
+    const double e = eta * i2;
+    double X = dt * ir0 * (1.0 + dt * (-0.5 * e + dt * (3.0 * e * e - v2 * i2 + GM * i2 * ir0) * (1.0 / 6.0)));
+    double G0, G1, G2, G3, D, tol;
+    bool done;
+    {
+        const double x = X;
+        double c0, c1, c2, c3;
+        stumpff(beta * x * x, c0, c1, c2, c3);
+        const double g1 = x * c1, g2 = x * x * c2, g3 = x * x * x * c3;
+        const double f = r0 * g1 + eta * g2 + GM * g3 - dt;
+        const double fp = r0 * c0 + eta * g1 + GM * g2;
+        const double fpp = eta * c0 + zeta * g1;
+        const double dX = f * fp * rcp_nr(fp * fp - 0.5 * f * fpp);
+        G0 = c0;
+        G1 = g1;
+        G2 = g2;
+        G3 = g3;
+        D = -dX;
+        X = x - dX;
+        // small steps (|beta X^2| <= 0.5): a 1e-6 correction leaves < 1e-18; large steps (a step
+        // covering a sizeable part of an orbit) iterate to full convergence
+        tol = fabs(beta * X * X) <= 0.5 ? 1e-6 : 2e-16;
+        done = !(fabs(dX) > tol * fabs(X));
+    }
+    for (int it = 1; it < 8 && !__all(done); it++) {  // rare extra iterations (pericentre, big steps)
+        const double x = X;
+        double c0, c1, c2, c3;
+        stumpff(beta * x * x, c0, c1, c2, c3);
+        const double g1 = x * c1, g2 = x * x * c2, g3 = x * x * x * c3;
+        const double f = r0 * g1 + eta * g2 + GM * g3 - dt;
+        const double fp = r0 * c0 + eta * g1 + GM * g2;
+        const double fpp = eta * c0 + zeta * g1;
+        const double dX = f * fp * rcp_nr(fp * fp - 0.5 * f * fpp);
+        if (!done) {
+            G0 = c0;
+            G1 = g1;
+            G2 = g2;
+            G3 = g3;
+            D = -dX;
+            X = x - dX;
+            done = !(fabs(dX) > tol * fabs(X));
+        }
+    }
+    // hard cases: steps spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) or no
+    // convergence above -> bracketed solve (divergent, rare; same regime split as the oracle)
+    if (!done || fabs(beta) * (dt * ir0) * (dt * ir0) > 0.5) {
+        kepler_safe(r0, eta, zeta, beta, GM, dt, X, G0, G1, G2, G3);
+        D = 0.0;
+    }
+    const double d = D, d2 = 0.5 * d * d;
+    const double H0 = G0 - beta * (d * G1 + d2 * G0);
+    const double H1 = G1 + d * G0 - d2 * beta * G1;
+    const double H2 = G2 + d * G1 + d2 * G0;
+    const double H3 = G3 + d * G2 + d2 * G1 + (d2 * d * (1.0 / 3.0)) * G0;
+    const double rr = r0 * H0 + eta * H1 + GM * H2;
+    const double irr = rcp_nr(rr);
+    const double gG2 = GM * H2;
+    const double f = 1.0 - gG2 * ir0;
+    const double g = dt - GM * H3;
+    const double fd = -GM * H1 * irr * ir0;
+    const double gd = 1.0 - gG2 * irr;
+    const double nrx = f * s.rx + g * s.vx;
+    const double nry = f * s.ry + g * s.vy;
+    const double nvx = fd * s.rx + gd * s.vx;
+    const double nvy = fd * s.ry + gd * s.vy;
+    s.rx = nrx;
+    s.ry = nry;
+    s.vx = nvx;
+    s.vy = nvy;
+    s.r = rr;
+    s.ir = irr;
+}
+
+// Interaction kick of the own Jacobi velocity by dt (and the encounter test on every pair):
+//   gather every planet's Jacobi position from the lane group, heliocentric positions
+//   x_i = r'_i + (sum_{j<i} m_j x_j)/M_{i-1}, pairwise accelerations (1/r^3 from rsq), the Jacobi
+//   acceleration a'_i = a_i - (sum_{j<i} m_j a_j)/M_{i-1}, and v'_i += dt (a'_i + M_i r'_i/|r'_i|^3)
+//   (the Kepler part is removed because the drift integrates it exactly).
+template <int NP, int L>
+__device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
     constexpr int NB = NP + 1;
     double x[NB], y[NB], ax[NB], ay[NB];
     x[0] = 0.0;
@@ -180,8 +310,16 @@ __device__ __forceinline__ void kick(Sys<NP>& s, double dt) {
     double cmx = 0.0, cmy = 0.0;
 #pragma unroll
     for (int i = 1; i < NB; i++) {
-        x[i] = s.rx[i - 1] + cmx / s.Mi[i - 1];
-        y[i] = s.ry[i - 1] + cmy / s.Mi[i - 1];
+        double Rx, Ry;
+        if constexpr (NP == 1) {
+            Rx = s.rx;
+            Ry = s.ry;
+        } else {
+            Rx = grp_get<L>(s.rx, i - 1);
+            Ry = grp_get<L>(s.ry, i - 1);
+        }
+        x[i] = Rx + cmx * s.iMi[i - 1];
+        y[i] = Ry + cmy * s.iMi[i - 1];
         cmx += s.m[i - 1] * x[i];
         cmy += s.m[i - 1] * y[i];
     }
@@ -198,7 +336,8 @@ __device__ __forceinline__ void kick(Sys<NP>& s, double dt) {
             const double dx = x[j] - x[i], dy = y[j] - y[i];
             const double r2 = dx * dx + dy * dy;
             enc |= (r2 < s.dmin2);
-            const double ir3 = 1.0 / (r2 * sqrt(r2));
+            const double ir = rsq_nr(r2);
+            const double ir3 = ir * ir * ir;
             const double mj = (j == 0) ? 1.0 : s.m[j - 1];
             const double mi = (i == 0) ? 1.0 : s.m[i - 1];
             ax[i] += mj * ir3 * dx;
@@ -208,26 +347,34 @@ __device__ __forceinline__ void kick(Sys<NP>& s, double dt) {
         }
     }
     s.enc |= enc;
+    // Jacobi acceleration of the own coordinate (index i = p + 1)
     double max_ = ax[0], may_ = ay[0];  // M_star = 1
+    double ajx = 0.0, ajy = 0.0;
 #pragma unroll
     for (int i = 1; i < NB; i++) {
-        const double rx = s.rx[i - 1], ry = s.ry[i - 1];
-        const double rj2 = rx * rx + ry * ry;
-        const double kep = s.Mi[i] / (rj2 * sqrt(rj2));
-        const double ajx = ax[i] - max_ / s.Mi[i - 1];
-        const double ajy = ay[i] - may_ / s.Mi[i - 1];
-        s.vx[i - 1] += dt * (ajx + kep * rx);
-        s.vy[i - 1] += dt * (ajy + kep * ry);
+        const double tx = ax[i] - max_ * s.iMi[i - 1];
+        const double ty = ay[i] - may_ * s.iMi[i - 1];
+        if (s.p == i - 1) {
+            ajx = tx;
+            ajy = ty;
+        }
         max_ += s.m[i - 1] * ax[i];
         may_ += s.m[i - 1] * ay[i];
     }
+    const double kep = s.GM * (s.ir * s.ir * s.ir);
+    s.vx += dt * (ajx + kep * s.rx);
+    s.vy += dt * (ajy + kep * s.ry);
 }
 
-template <int NP>
-__device__ __forceinline__ double star_vx(const Sys<NP>& s) {
+// star barycentric x-velocity: v0 = -sum_q (m_q / M_q) v'_q (gathered over the lane group)
+template <int NP, int L>
+__device__ __forceinline__ double star_vx(const Lane<NP>& s) {
     double v = 0.0;
 #pragma unroll
-    for (int p = 0; p < NP; p++) v -= (s.m[p] / s.Mi[p + 1]) * s.vx[p];
+    for (int q = 0; q < NP; q++) {
+        const double vq = (NP == 1) ? s.vx : grp_get<L>(s.vx, q);
+        v -= s.mu[q] * vq;
+    }
     return v;
 }
 

@@ -5,14 +5,15 @@
 //   -> get_rv x2 (:61-73) -> setup_sim (:36-47) + REBOUND IAS15 integrate + Encounter.
 //
 // Work decomposition:
-//   workgroup = 64 walkers x one direction (blockIdx.y: 0 = epochs t >= 0, 1 = t < 0)
+//   workgroup = 64/L walkers x one direction (blockIdx.y: 0 = epochs t >= 0, 1 = t < 0)
 //               x n_levels waves; wave L integrates the same 64 walkers with (L+1)x the steps
 //               (Wisdom-Holman DKD, epoch-aligned segments).  At every epoch each wave drops its
 //               64 model RVs into LDS, one barrier, and wave 0 forms the Richardson-extrapolated
 //               RV (sum_L w_L rv_L, the h^2 -> 0 limit) and accumulates chi2 in registers.
-//   lane      = one walker; Kepler solver state in registers; the epoch schedule is wave-uniform
-//               (scalar loads), walker parameters are read once, coalesced, from SoA
-//               [n_params][n_walkers].
+//   lanes     = the planets of one walker sit on L = 1/2/4 adjacent lanes (one Kepler drift per
+//               lane, positions exchanged by DPP quad permutes for the kick); solver state in
+//               registers; the epoch schedule is wave-uniform (scalar loads); walker parameters
+//               are read once from SoA [n_params][n_walkers].
 // A second tiny kernel (finalize) combines the two directions: logl = -(chi2_b + chi2_f)/Npoints.
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -29,10 +30,14 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
                                                                    double* __restrict__ chi2_part,
                                                                    int32_t* __restrict__ status_part,
                                                                    double* __restrict__ rv_out) {
-    const int lvl = threadIdx.x >> 6;  // wave-uniform
+    constexpr int L = LanesPerWalker<NP>::value;  // lanes per walker (one per planet)
+    constexpr int WPB = 64 / L;                    // walkers per block (= per wave)
+    const int lvl = threadIdx.x >> 6;              // wave-uniform extrapolation level
     const int lane = threadIdx.x & 63;
+    const int slot = lane / L;                     // walker slot within the block
+    const int pl_idx = lane % L;
     const int d = blockIdx.y;
-    const int w = blockIdx.x * 64 + lane;
+    const int w = blockIdx.x * WPB + slot;
     const bool valid = w < W;
     const int wl = valid ? w : (W - 1);
     const int nl = P.n_levels;
@@ -44,7 +49,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     const int mult = P.mult[lvl];
 
     // ---- walker parameters (m, a, h, k, l per planet), prior (state.py:299-315) ----------------
-    Sys<NP> s;
+    Lane<NP> s;
     double pa[NP], ph[NP], pk[NP], pl[NP];
     int status = RVM_STATUS_OK;
 #pragma unroll
@@ -69,31 +74,67 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         }
     }
 
-    // ---- setup_sim: Pal -> heliocentric -> Jacobi; Hill-radius exit distance -------------------
-    s.Mi[0] = 1.0;
+    // ---- setup_sim: Pal -> heliocentric (own planet) -> Jacobi; Hill-radius exit distance -------
+    s.p = pl_idx < NP ? pl_idx : NP - 1;
+    double Mi[NP + 1];
+    Mi[0] = 1.0;
     double hill = 0.0;
-    double sx = 0.0, sy = 0.0, svx = 0.0, svy = 0.0;
 #pragma unroll
     for (int p = 0; p < NP; p++) {
-        s.Mi[p + 1] = s.Mi[p] + s.m[p];
-        double X, Y, VX, VY;
-        pal_to_cart(1.0 + s.m[p], pa[p], pl[p], pk[p], ph[p], X, Y, VX, VY);
-        s.rx[p] = X - sx / s.Mi[p];
-        s.ry[p] = Y - sy / s.Mi[p];
-        s.vx[p] = VX - svx / s.Mi[p];
-        s.vy[p] = VY - svy / s.Mi[p];
-        sx += s.m[p] * X;
-        sy += s.m[p] * Y;
-        svx += s.m[p] * VX;
-        svy += s.m[p] * VY;
+        Mi[p + 1] = Mi[p] + s.m[p];
         const double rh = pa[p] * cbrt(s.m[p] / 3.0);
         hill = rh > hill ? rh : hill;
     }
+#pragma unroll
+    for (int p = 0; p <= NP; p++) s.iMi[p] = 1.0 / Mi[p];
+#pragma unroll
+    for (int p = 0; p < NP; p++) s.mu[p] = s.m[p] / Mi[p + 1];
     s.dmin2 = (hill_factor * hill) * (hill_factor * hill);
+    double own_m = s.m[0], own_a = pa[0], own_h = ph[0], own_k = pk[0], own_l = pl[0], own_M = Mi[1];
+#pragma unroll
+    for (int p = 1; p < NP; p++) {
+        if (s.p == p) {
+            own_m = s.m[p];
+            own_a = pa[p];
+            own_h = ph[p];
+            own_k = pk[p];
+            own_l = pl[p];
+            own_M = Mi[p + 1];
+        }
+    }
+    s.GM = own_M;
+    double X, Y, VX, VY;
+    pal_to_cart(1.0 + own_m, own_a, own_l, own_k, own_h, X, Y, VX, VY);
+    {
+        // r'_p = x_p - (sum_{q<p} m_q x_q) / M_{p-1}   (heliocentric -> Jacobi)
+        double sx = 0.0, sy = 0.0, svx = 0.0, svy = 0.0;
+        double jx = X, jy = Y, jvx = VX, jvy = VY;
+#pragma unroll
+        for (int q = 0; q < NP - 1; q++) {
+            const double xq = grp_get<L>(X, q), yq = grp_get<L>(Y, q);
+            const double vxq = grp_get<L>(VX, q), vyq = grp_get<L>(VY, q);
+            sx += s.m[q] * xq;
+            sy += s.m[q] * yq;
+            svx += s.m[q] * vxq;
+            svy += s.m[q] * vyq;
+            if (s.p == q + 1) {
+                jx = X - sx * s.iMi[q + 1];
+                jy = Y - sy * s.iMi[q + 1];
+                jvx = VX - svx * s.iMi[q + 1];
+                jvy = VY - svy * s.iMi[q + 1];
+            }
+        }
+        s.rx = jx;
+        s.ry = jy;
+        s.vx = jvx;
+        s.vy = jvy;
+    }
+    s.r = sqrt(s.rx * s.rx + s.ry * s.ry);
+    s.ir = 1.0 / s.r;
     s.enc = 0;
     {
-        Sys<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
-        kick(t0, 0.0);
+        Lane<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
+        kick<NP, L>(t0, 0.0);
         s.enc = t0.enc;
     }
 
@@ -106,31 +147,37 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
             const double h = S.seg_len[e] / (double)ns;
             drift(s, 0.5 * h);
             for (int j = 0; j < ns - 1; j++) {
-                kick(s, h);
+                kick<NP, L>(s, h);
                 drift(s, h);
             }
-            kick(s, h);
+            kick<NP, L>(s, h);
             drift(s, 0.5 * h);
         }
-        s_rv[e & 1][lvl][lane] = star_vx(s);
+        const double v0 = star_vx<NP, L>(s);
+        if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
         __syncthreads();
-        if (lvl == 0) {
+        if (lvl == 0 && lane < WPB) {  // lane `lane` of wave 0 owns walker slot `lane`
             double rvx = 0.0;
             for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv[e & 1][k][lane];
             const double r = rvx - S.obs_rv[e];
             chi2 += (r * r) / S.obs_s2[e];
-            if (rv_out != nullptr && valid) rv_out[(size_t)S.obs_idx[e] * W + w] = rvx;
+            const int wo = blockIdx.x * WPB + lane;
+            if (rv_out != nullptr && wo < W) rv_out[(size_t)S.obs_idx[e] * W + wo] = rvx;
         }
     }
-    s_enc[lvl][lane] = s.enc;
+    if (pl_idx == 0) s_enc[lvl][slot] = s.enc | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
-    if (lvl == 0 && valid) {
-        int enc = 0;
-        for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
-        if (status == RVM_STATUS_OK && enc) status = RVM_STATUS_ENCOUNTER;
-        if (status == RVM_STATUS_OK && !isfinite(chi2)) status = RVM_STATUS_NONFINITE;
-        chi2_part[(size_t)d * W + w] = chi2;
-        status_part[(size_t)d * W + w] = status;
+    if (lvl == 0 && lane < WPB) {
+        const int wo = blockIdx.x * WPB + lane;
+        if (wo < W) {
+            int enc = 0;
+            for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
+            int st = (enc & 2) ? RVM_STATUS_PRIOR : RVM_STATUS_OK;
+            if (st == RVM_STATUS_OK && (enc & 1)) st = RVM_STATUS_ENCOUNTER;
+            if (st == RVM_STATUS_OK && !isfinite(chi2)) st = RVM_STATUS_NONFINITE;
+            chi2_part[(size_t)d * W + wo] = chi2;
+            status_part[(size_t)d * W + wo] = st;
+        }
     }
 }
 
@@ -149,7 +196,9 @@ __global__ void finalize_kernel(const int W, const double npoints, const double*
 
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, double* chi2_part,
                        int32_t* status_part, double* logl, int32_t* status, double* rv_out, hipStream_t stream) {
-    const dim3 grid((W + 63) / 64, 2);
+    const int lpw = P.n_planets == 1 ? 1 : (P.n_planets == 2 ? 2 : 4);  // LanesPerWalker
+    const int wpb = 64 / lpw;
+    const dim3 grid((W + wpb - 1) / wpb, 2);
     const dim3 block(64 * P.n_levels);
     switch (P.n_planets) {
         case 1:

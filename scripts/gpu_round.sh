@@ -10,5 +10,6 @@ timeout -k 10 420 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2
 tail -3 gpurun_out/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
 cat gpurun_out/smoke.log
+timeout -k 10 200 python scripts/kbench.py 2048 4096 2>&1 | grep -v amdgpu.ids | tee gpurun_out/kbench.log
 timeout -k 10 300 python bench.py --steps "$STEPS" --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json

@@ -1,0 +1,20 @@
+#!/bin/bash
+# PMC passes (counters only with --kernel-trace, one group per run) over the kernel micro-bench,
+# then scripts/pmc_summary.py turns them into profiles/pmc_latest.json (per-launch HBM bytes,
+# FP64 flops, issue efficiency).
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$PWD
+export TMPDIR=/tmp
+mkdir -p gpurun_out/pmc
+cd /tmp
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS SQ_INSTS_SMEM" \
+           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_THREAD_CYCLES_VALU" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc/p$i" -o run --output-format csv -- python3 "$R/scripts/kbench.py" 2048 > "$R/gpurun_out/pmc/p$i.log" 2>&1
+done
+cd "$R"
+python3 scripts/pmc_summary.py gpurun_out/pmc 2048 | tee gpurun_out/pmc/summary.txt
