@@ -164,3 +164,27 @@ def test_smala_chains_run():
     assert sm.iteration == 5
     assert np.isfinite(sm.cache["lp"].cpu().numpy()).all()
     assert int(sm.accepted.sum()) > 0
+
+
+def test_device_philox_matches_restatement():
+    """rvm_stretch_propose with the built-in Philox draws == tests/philox_ref.py restatement."""
+    torch = _torch()
+    from philox_ref import stretch_uniforms
+    from rvmcmc import _lib
+
+    lib = _lib.load()
+    dim, n0, n1, seed, it, half, begin = 10, 96, 96, 987654321987, 5, 1, 1000
+    rng = np.random.default_rng(2)
+    x = torch.as_tensor(rng.standard_normal((dim, n0)), device="cuda")
+    c = torch.as_tensor(rng.standard_normal((dim, n1)), device="cuda")
+    q = torch.empty_like(x)
+    z = torch.empty(n0, dtype=torch.float64, device="cuda")
+    _lib.check(lib.rvm_stretch_propose(dim, n0, begin, x.data_ptr(), n1, c.data_ptr(), 2.0, seed, it, half, 0,
+                                       q.data_ptr(), z.data_ptr(), _lib.stream_handle()), "propose")
+    torch.cuda.synchronize()
+    u1, u2, _ = stretch_uniforms(seed, begin, n0, it, half)
+    zz = ((2.0 - 1.0) * u1 + 1.0) * ((2.0 - 1.0) * u1 + 1.0) / 2.0
+    j = np.floor(u2 * n1).astype(int)
+    C, X = c.cpu().numpy(), x.cpu().numpy()
+    np.testing.assert_array_equal(z.cpu().numpy(), zz)
+    np.testing.assert_array_equal(q.cpu().numpy(), C[:, j] - zz[None] * (C[:, j] - X))
