@@ -52,6 +52,7 @@ extern "C" {
 
 #define RVM_MAX_PLANETS 4
 #define RVM_MAX_LEVELS 6
+#define RVM_MAX_EPOCHS_PER_DIRECTION 1700 /* epochs with t >= 0, and with t < 0, per plan */
 
 /* Integrator configuration of a plan. */
 typedef struct {
@@ -110,9 +111,11 @@ int rvm_mh_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, doubl
                   const double* lnp_new, uint64_t seed, uint64_t iteration, const double* draws, int32_t* accepted,
                   void* stream);
 
-/* Central finite-difference stencil for SMALA's gradient/metric: for each chain c and parameter p,
- * out[(1 + 2p + s)*n_chains + c] (s = 0: +eps_p, 1: -eps_p) and out[0*n_chains + c] = x;
- * eps_p = rel_step * max(|x_p|, floor[p]).  out layout: [(2P+1)] blocks of [n_params][n_chains]. */
+/* Central finite-difference stencil for SMALA's gradient/metric (x: [n_params][n_chains]).
+ * out: SoA [n_params][(2P+1) * n_chains]; stencil point s of chain c is walker s*n_chains + c with
+ * s = 0: x, s = 1+2p: x + eps_p e_p, s = 2+2p: x - eps_p e_p, eps_p = rel_step*max(|x_p|, floor[p]).
+ * One rvm_logl_batch over (2P+1)*n_chains walkers then gives logp, its gradient and (rv_out) the
+ * per-epoch RV Jacobian. */
 int rvm_fd_params(int32_t n_params, int32_t n_chains, const double* x, double rel_step, const double* floor_,
                   double* out, void* stream);
 

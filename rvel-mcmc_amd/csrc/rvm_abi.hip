@@ -95,6 +95,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         }
         if (total_steps[dd] * (long long)cfg->n_levels > (1LL << 30))
             return fail(-1, "rvm_plan_create: dt too small for the epoch span");
+        if (D.idx.size() > (size_t)RVM_MAX_EPOCHS_PER_DIRECTION)
+            return fail(-1, "rvm_plan_create: too many epochs in one direction (the schedule is staged in LDS)");
     }
 
     // device layout: per direction [seg_n | obs_idx] int32 and [seg_len | obs_rv | obs_s2] f64, + workspace

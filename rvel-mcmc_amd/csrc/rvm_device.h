@@ -18,24 +18,23 @@
 
 namespace rvm {
 
-// ---- fp64 reciprocal / reciprocal-sqrt: hardware estimate + two Newton steps --------------------
+// ---- fp64 reciprocal / reciprocal-sqrt: hardware estimate + one cubic refinement ----------------
 // The compiler's IEEE division / sqrt expansions are ~10 dependent instructions each; the hot loop
-// only needs faithfully rounded results, which v_rcp_f64 / v_rsq_f64 plus two Newton-Raphson
-// refinements give in 5 dependent FMAs.
+// only needs faithfully rounded results.  v_rcp_f64 / v_rsq_f64 are good to ~5e-8 relative
+// (measured, scripts/probe/rcp_precision.hip); one third-order correction
+//   1/a    = r (1 + e + e^2),             e = 1 - a r
+//   1/sqrt = y (1 + e/2 + 3 e^2 / 8),     e = 1 - a y^2
+// leaves an error ~e^3 ~ 1e-22, i.e. the result is limited by rounding only.
 __device__ __forceinline__ double rcp_nr(double x) {
-    double r = __builtin_amdgcn_rcp(x);
-    double e = fma(-x, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-x, r, 1.0);
-    return fma(r, e, r);
+    const double r = __builtin_amdgcn_rcp(x);
+    const double e = fma(-x, r, 1.0);
+    return fma(r, fma(e, e, e), r);
 }
 
 __device__ __forceinline__ double rsq_nr(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    double e = fma(-x * y, y, 1.0);  // 1 - x y^2
-    y = fma(0.5 * y, e, y);
-    e = fma(-x * y, y, 1.0);
-    return fma(0.5 * y, e, y);
+    const double y = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x * y, y, 1.0);
+    return fma(y, e * fma(0.375, e, 0.5), y);
 }
 
 // ---- Stumpff functions c0..c3 (Danby): series for |z| <= 1, quartering+doubling otherwise ------
@@ -47,25 +46,18 @@ __device__ __forceinline__ void stumpff(double z, double& c0, double& c1, double
         z *= 0.25;
         n++;
     }
-    double a2 = 1.0 / 6402373705728000.0;     // 1/18!
-    double a3 = 1.0 / 121645100408832000.0;   // 1/19!
-    a2 = 1.0 / 20922789888000.0 - z * a2;     // 1/16!
-    a3 = 1.0 / 355687428096000.0 - z * a3;    // 1/17!
-    a2 = 1.0 / 87178291200.0 - z * a2;        // 1/14!
-    a3 = 1.0 / 1307674368000.0 - z * a3;      // 1/15!
-    a2 = 1.0 / 479001600.0 - z * a2;          // 1/12!
-    a3 = 1.0 / 6227020800.0 - z * a3;         // 1/13!
-    a2 = 1.0 / 3628800.0 - z * a2;            // 1/10!
-    a3 = 1.0 / 39916800.0 - z * a3;           // 1/11!
-    a2 = 1.0 / 40320.0 - z * a2;              // 1/8!
-    a3 = 1.0 / 362880.0 - z * a3;             // 1/9!
-    a2 = 1.0 / 720.0 - z * a2;                // 1/6!
-    a3 = 1.0 / 5040.0 - z * a3;               // 1/7!
-    a2 = 1.0 / 24.0 - z * a2;                 // 1/4!
-    a3 = 1.0 / 120.0 - z * a3;                // 1/5!
-    a2 = 0.5 - z * a2;                        // 1/2!
-    a3 = 1.0 / 6.0 - z * a3;                  // 1/3!
-    double C2 = a2, C3 = a3;
+    // Estrin evaluation in w = -z (dependency depth 4 instead of 8 for Horner)
+    const double w = -z, w2 = w * w, w4 = w2 * w2;
+    const double a2 = fma(w4,
+                          fma(w2, fma(w, 1.0 / 6402373705728000.0, 1.0 / 20922789888000.0),
+                              fma(w, 1.0 / 87178291200.0, 1.0 / 479001600.0)),
+                          fma(w2, fma(w, 1.0 / 3628800.0, 1.0 / 40320.0), fma(w, 1.0 / 720.0, 1.0 / 24.0)));
+    const double a3 = fma(w4,
+                          fma(w2, fma(w, 1.0 / 121645100408832000.0, 1.0 / 355687428096000.0),
+                              fma(w, 1.0 / 1307674368000.0, 1.0 / 6227020800.0)),
+                          fma(w2, fma(w, 1.0 / 39916800.0, 1.0 / 362880.0), fma(w, 1.0 / 5040.0, 1.0 / 120.0)));
+    // c2 = 1/2! + w (1/4! + w (1/6! + ...)) ; c3 = 1/3! + w (1/5! + ...)
+    double C2 = fma(w, a2, 0.5), C3 = fma(w, a3, 1.0 / 6.0);
     double C1 = 1.0 - z * C3;
     double C0 = 1.0 - z * C2;
     for (; n > 0; n--) {
@@ -302,7 +294,7 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
 //   acceleration a'_i = a_i - (sum_{j<i} m_j a_j)/M_{i-1}, and v'_i += dt (a'_i + M_i r'_i/|r'_i|^3)
 //   (the Kepler part is removed because the drift integrates it exactly).
 template <int NP, int L>
-__device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
+__device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
     constexpr int NB = NP + 1;
     double x[NB], y[NB], ax[NB], ay[NB];
     x[0] = 0.0;
@@ -329,14 +321,22 @@ __device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
         ay[i] = 0.0;
     }
     int enc = 0;
+    // star -- planet 1 distance is |r'_1|, already known to planet 1's lane from its drift
+    const double ir01 = (NP == 1) ? s.ir : grp_get<L>(s.ir, 0);
 #pragma unroll
     for (int i = 0; i < NB; i++) {
 #pragma unroll
         for (int j = i + 1; j < NB; j++) {
             const double dx = x[j] - x[i], dy = y[j] - y[i];
-            const double r2 = dx * dx + dy * dy;
-            enc |= (r2 < s.dmin2);
-            const double ir = rsq_nr(r2);
+            double ir;
+            if (i == 0 && j == 1) {
+                ir = ir01;
+                enc |= (ir * ir * s.dmin2 > 1.0);
+            } else {
+                const double r2 = dx * dx + dy * dy;
+                enc |= (r2 < s.dmin2);
+                ir = rsq_nr(r2);
+            }
             const double ir3 = ir * ir * ir;
             const double mj = (j == 0) ? 1.0 : s.m[j - 1];
             const double mi = (i == 0) ? 1.0 : s.m[i - 1];
@@ -364,6 +364,43 @@ __device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
     const double kep = s.GM * (s.ir * s.ir * s.ir);
     s.vx += dt * (ajx + kep * s.rx);
     s.vy += dt * (ajy + kep * s.ry);
+}
+
+// Two-planet kick in closed form (same interaction as the generic kick; G = M_star = 1):
+//   dv'_1 = dt m_2 (d12/r12^3 - d02/r02^3)
+//   dv'_2 = dt [ M_2 r'_2/|r'_2|^3 - (M_2/M_1)(d02/r02^3 + m_1 d12/r12^3) ]
+// with heliocentric x_1 = r'_1, x_2 = r'_2 + (m_1/M_1) r'_1, d02 = x_2, d12 = x_2 - x_1.  The
+// star--planet-1 distance |r'_1| and the own |r'| are carried from the drift: 2 rsq per kick.
+template <int L>
+__device__ __forceinline__ void kick2(Lane<2>& s, double dt) {
+    const double x1 = grp_get<L, 0>(s.rx), y1 = grp_get<L, 0>(s.ry);
+    const double R2x = grp_get<L, 1>(s.rx), R2y = grp_get<L, 1>(s.ry);
+    const double ir01 = grp_get<L, 0>(s.ir);
+    const double c = s.m[0] * s.iMi[1];  // m_1 / M_1
+    const double x2 = fma(c, x1, R2x), y2 = fma(c, y1, R2y);
+    const double dx12 = x2 - x1, dy12 = y2 - y1;
+    const double r02sq = x2 * x2 + y2 * y2;
+    const double r12sq = dx12 * dx12 + dy12 * dy12;
+    s.enc |= (r02sq < s.dmin2) | (r12sq < s.dmin2) | (ir01 * ir01 * s.dmin2 > 1.0);
+    const double i02 = rsq_nr(r02sq), i12 = rsq_nr(r12sq);
+    const double i02c = i02 * i02 * i02, i12c = i12 * i12 * i12;
+    // lane of planet 1: (A, B, C) = (0, -m2, m2); lane of planet 2: (M2/r'^3, -M2/M1, -m1 M2/M1)
+    const bool p1 = s.p == 0;
+    const double q = s.GM * s.iMi[1];
+    const double A = p1 ? 0.0 : s.GM * (s.ir * s.ir * s.ir);
+    const double B = p1 ? -s.m[1] : -q;
+    const double C = p1 ? s.m[1] : -q * s.m[0];
+    const double bx = B * i02c, cx = C * i12c;
+    s.vx = fma(dt, fma(A, s.rx, fma(bx, x2, cx * dx12)), s.vx);
+    s.vy = fma(dt, fma(A, s.ry, fma(bx, y2, cx * dy12)), s.vy);
+}
+
+template <int NP, int L>
+__device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
+    if constexpr (NP == 2)
+        kick2<L>(s, dt);
+    else
+        kick_generic<NP, L>(s, dt);
 }
 
 // star barycentric x-velocity: v0 = -sum_q (m_q / M_q) v'_q (gathered over the lane group)

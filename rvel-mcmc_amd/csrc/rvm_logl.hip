@@ -44,9 +44,24 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
 
     __shared__ double s_rv[2][RVM_MAX_LEVELS][64];
     __shared__ int s_enc[RVM_MAX_LEVELS][64];
+    // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
+    extern __shared__ double s_sched[];  // [E] seg_len | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
 
     const DirSched S = d ? P.bwd : P.fwd;
     const int mult = P.mult[lvl];
+    const int E = S.n_epochs;
+    double* l_len = s_sched;
+    double* l_rv = s_sched + E;
+    double* l_s2 = s_sched + 2 * E;
+    int* l_n = reinterpret_cast<int*>(s_sched + 3 * E);
+    int* l_idx = l_n + E;
+    for (int i = threadIdx.x; i < E; i += blockDim.x) {
+        l_len[i] = S.seg_len[i];
+        l_rv[i] = S.obs_rv[i];
+        l_s2[i] = S.obs_s2[i];
+        l_n[i] = S.seg_n[i];
+        l_idx[i] = S.obs_idx[i];
+    }
 
     // ---- walker parameters (m, a, h, k, l per planet), prior (state.py:299-315) ----------------
     Lane<NP> s;
@@ -139,12 +154,17 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     }
 
     // ---- integrate outward from t = 0 through this direction's epochs -------------------------
+    __syncthreads();  // schedule staged
     double chi2 = 0.0;
-    for (int e = 0; e < S.n_epochs; e++) {
-        const int n1 = S.seg_n[e];
+    int n1 = E > 0 ? l_n[0] : 0;
+    double len = E > 0 ? l_len[0] : 0.0;
+    for (int e = 0; e < E; e++) {
+        // prefetch the next segment while this one integrates
+        const int n1_next = e + 1 < E ? l_n[e + 1] : 0;
+        const double len_next = e + 1 < E ? l_len[e + 1] : 0.0;
         const int ns = n1 * mult;
         if (ns > 0) {
-            const double h = S.seg_len[e] / (double)ns;
+            const double h = len / (double)ns;
             drift(s, 0.5 * h);
             for (int j = 0; j < ns - 1; j++) {
                 kick<NP, L>(s, h);
@@ -159,11 +179,13 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         if (lvl == 0 && lane < WPB) {  // lane `lane` of wave 0 owns walker slot `lane`
             double rvx = 0.0;
             for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv[e & 1][k][lane];
-            const double r = rvx - S.obs_rv[e];
-            chi2 += (r * r) / S.obs_s2[e];
+            const double r = rvx - l_rv[e];
+            chi2 += (r * r) / l_s2[e];
             const int wo = blockIdx.x * WPB + lane;
-            if (rv_out != nullptr && wo < W) rv_out[(size_t)S.obs_idx[e] * W + wo] = rvx;
+            if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[e] * W + wo] = rvx;
         }
+        n1 = n1_next;
+        len = len_next;
     }
     if (pl_idx == 0) s_enc[lvl][slot] = s.enc | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
@@ -200,18 +222,20 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
     const int wpb = 64 / lpw;
     const dim3 grid((W + wpb - 1) / wpb, 2);
     const dim3 block(64 * P.n_levels);
+    const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
+    const size_t smem = (size_t)emax * (3 * sizeof(double) + 2 * sizeof(int32_t)) + 16;
     switch (P.n_planets) {
         case 1:
-            logl_kernel<1><<<grid, block, 0, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            logl_kernel<1><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
             break;
         case 2:
-            logl_kernel<2><<<grid, block, 0, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            logl_kernel<2><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
             break;
         case 3:
-            logl_kernel<3><<<grid, block, 0, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            logl_kernel<3><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
             break;
         case 4:
-            logl_kernel<4><<<grid, block, 0, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            logl_kernel<4><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
             break;
         default:
             return hipErrorInvalidValue;
