@@ -38,7 +38,28 @@ __device__ __forceinline__ double rsq_nr(double x) {
 }
 
 // ---- Stumpff functions c0..c3 (Danby): series for |z| <= 1, quartering+doubling otherwise ------
+__device__ __forceinline__ void stumpff_full(double z, double& c0, double& c1, double& c2, double& c3);
+
+// Short series for the small arguments of the fine levels: |z| <= 0.01 needs 5 terms per function
+// (remainder z^5/12! < 1e-19 relative), which is what the finest Richardson level sees
+// (z ~ (n h)^2 ~ 0.004 at the default P/96); larger |z| takes the 9-term path.
 __device__ __forceinline__ void stumpff(double z, double& c0, double& c1, double& c2, double& c3) {
+    if (fabs(z) <= 0.01) {
+        const double w = -z, w2 = w * w;
+        const double C2 = fma(w2 * w2, 1.0 / 3628800.0,
+                              fma(w2, fma(w, 1.0 / 40320.0, 1.0 / 720.0), fma(w, 1.0 / 24.0, 0.5)));
+        const double C3 = fma(w2 * w2, 1.0 / 39916800.0,
+                              fma(w2, fma(w, 1.0 / 362880.0, 1.0 / 5040.0), fma(w, 1.0 / 120.0, 1.0 / 6.0)));
+        c2 = C2;
+        c3 = C3;
+        c1 = 1.0 - z * C3;
+        c0 = 1.0 - z * C2;
+    } else {
+        stumpff_full(z, c0, c1, c2, c3);
+    }
+}
+
+__device__ __forceinline__ void stumpff_full(double z, double& c0, double& c1, double& c2, double& c3) {
     // c2 = sum_j (-z)^j / (2j+2)!,  c3 = sum_j (-z)^j / (2j+3)!   (8 terms: error < z^8/18! <= 1e-19
     // for |z| <= 0.5; the level-1 step keeps |z| = (n dt)^2 <~ 0.07 on the benchmark configs)
     int n = 0;

@@ -198,11 +198,15 @@ class ParamMap:
                     slots.append(5 * i + KERNEL_KEYS.index(k))
         self.slots = np.asarray(slots, dtype=np.int64)
         self.n_free = len(slots)
+        # free parameters already in kernel order (m,a,h,k,l per planet, all free): no remapping
+        self.identity = self.n_free == 5 * self.n_planets and bool(np.all(self.slots == np.arange(self.n_free)))
         self._dev_cache = {}
 
     def to_kernel(self, X):
         """X: float64 device tensor [n_free][W] -> kernel params [5*np][W]."""
         torch = _torch()
+        if self.identity and X.is_contiguous():
+            return X
         key = str(X.device)
         if key not in self._dev_cache:
             self._dev_cache[key] = (torch.as_tensor(self.base, device=X.device),

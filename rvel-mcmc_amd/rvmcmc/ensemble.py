@@ -47,6 +47,7 @@ class DeviceOps:
         self.plan = engine.plan_for(sampler.obs, sampler.pmap.n_planets, dt, st.integrator.n_levels, sampler.nloc,
                                     sampler.device)
         self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
+        self.track_status = False  # set True to histogram per-walker statuses (costs a small kernel)
         self.status_counts = torch.zeros(4, dtype=torch.int64, device=sampler.device)
 
     def propose(self, X0, c, half, q, z, draws=None):
@@ -66,7 +67,8 @@ class DeviceOps:
         if self.timing is not None:
             e1.record()
             self.timing.append((e0, e1, X.shape[1]))
-        self.status_counts.index_add_(0, st.long(), torch.ones_like(st, dtype=torch.int64))
+        if self.track_status:
+            self.status_counts.index_add_(0, st.long(), torch.ones_like(st, dtype=torch.int64))
         return lp, st
 
     def accept(self, X0, lnp0, q, lnp_new, z, half, accepted, draws=None):

@@ -44,6 +44,12 @@ def lnprob(x, e):
 
 
 def _scales_vector(state, scales):
+    """mcmc.py:70-75 / 98-103: dict keyed by parameter name -> vector; an array is taken as is."""
+    if not isinstance(scales, dict):
+        v = np.asarray(scales, dtype=np.float64)
+        if v.shape != (state.Nvars,):
+            raise ValueError("scales array must have Nvars entries")
+        return v.copy()
     out = np.ones(state.Nvars)
     for i, k in enumerate(state.get_rawkeys()):
         if k in scales:
