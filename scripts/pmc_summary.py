@@ -34,7 +34,9 @@ if fs is not None and ws is not None:
     out["hbm_bytes_per_launch_uncorrected"] = (fs + ws) * 1024.0
 fl, flt = mean("SQ_INSTS_VALU_FLOPS_FP64"), mean("SQ_INSTS_VALU_FLOPS_FP64_TRANS")
 if fl is not None:
-    out["fp64_flops_per_launch"] = fl + (flt or 0.0)
+    # SQ_INSTS_VALU_FLOPS_FP64 counts per wave-instruction (FMA = 2; it equals 2*FMA_F64 + MUL_F64 +
+    # ADD_F64 instruction counts), so x64 lanes gives fp64 flops (all lanes active in this kernel)
+    out["fp64_flops_per_launch"] = 64.0 * (fl + (flt or 0.0))
     out["fp64_flops_per_eval"] = out["fp64_flops_per_launch"] / W
 print(json.dumps(out, indent=1))
 
