@@ -1,0 +1,119 @@
+"""Throughput of every BASELINE.json config on one GPU (bench.py keeps the headline config).
+
+  config 2: affine stretch, 1024 walkers, 2-planet synthetic (101 epochs)
+  config 3: affine stretch, 4096 walkers, HD155358.vels (122 epochs)
+  config 4: SMALA, 256 chains, 10-dim 2-planet, FD gradient/metric (21 logL per chain-step)
+  config 5: affine stretch, 3-planet synthetic, 8192 walkers per GPU (= 65536 over 8 GPUs);
+            the third planet is named here (not in the reference): {m 1e-3, a 2.6, h 0.05, k 0, l 1}
+  config 1: the reference-API single-chain Mh (mcmc_benchmark_mh.py), steps/s
+
+Prints one JSON line per config.  Usage: python scripts/configs_bench.py [config ...]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "rvel-mcmc_amd")]
+import torch  # noqa: E402
+
+from rvmcmc import mcmc  # noqa: E402
+from rvmcmc.ensemble import EnsembleSampler  # noqa: E402
+from rvmcmc.observations import FakeObservation, Observation_FromFile  # noqa: E402
+from rvmcmc.smala import SmalaChains  # noqa: E402
+from rvmcmc.state import State  # noqa: E402
+
+S2 = [{"m": 1.2e-3, "a": 0.88, "h": 0.218, "k": 0.015, "l": 0.3},
+      {"m": 2.1e-3, "a": 1.55, "h": 0.16, "k": 0.02, "l": 2.2}]
+THIRD = {"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}
+SCALES = {"m": 1.5e-3, "a": 0.3, "h": 0.1, "k": 0.1, "l": np.pi / 2.}
+
+
+def _affine(state, obs, W, steps=20, warmup=3):
+    sc = np.array([SCALES[k] for k in state.get_rawkeys()])
+    X0 = state.get_params()[None] + 1e-3 * sc * np.random.normal(size=(W, state.Nvars))
+    ens = EnsembleSampler(W, state, obs, seed=1)
+    ens.set_positions(X0)
+    ens.compute_lnprob()
+    for _ in range(warmup):
+        ens.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ens.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"walker_logl_evals_per_s": W * steps / dt, "ms_per_iteration": 1e3 * dt / steps,
+            "acceptance": float(ens.acceptance_fraction().mean().item()), "plan_steps": ens.plan.info()}
+
+
+def config2():
+    np.random.seed(2017)
+    s = State(planets=[dict(p) for p in S2])
+    obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    return {"config": "2: affine, 1024 walkers, 2-planet synthetic", **_affine(s, obs, 1024)}
+
+
+def config3():
+    np.random.seed(2017)
+    sol = [6.57730330e-01, -9.72263877e-02, -7.82798396e-02, 8.84031737e-04, 4.42804990e+00,
+           1.04404207e+00, -2.05622789e-02, -1.08797961e-01, 8.30379710e-04, 1.49919861e+00]
+    s = State(planets=[{"m": sol[3], "a": sol[0], "h": sol[1], "k": sol[2], "l": sol[4]},
+                       {"m": sol[8], "a": sol[5], "h": sol[6], "k": sol[7], "l": sol[9]}])
+    obs = Observation_FromFile(os.path.join(ROOT, "tests", "golden", "HD155358.vels"), Npoints=100)
+    return {"config": "3: affine, 4096 walkers, HD155358.vels", **_affine(s, obs, 4096)}
+
+
+def config4(chains=256, steps=10):
+    np.random.seed(2017)
+    s = State(planets=[dict(p) for p in S2])
+    obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=chains, seed=0)
+    sm.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sm.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    P = s.Nvars
+    return {"config": "4: SMALA, 256 chains, 10-dim, FD (2P+1 = 21 logL per chain-step)",
+            "chain_steps_per_s": chains * steps / dt, "walker_logl_evals_per_s": chains * steps * (2 * P + 1) / dt,
+            "ms_per_step": 1e3 * dt / steps, "acceptance": float(sm.accepted.double().mean().item() / sm.iteration)}
+
+
+def config5(W=8192):
+    np.random.seed(2017)
+    s = State(planets=[dict(p) for p in S2] + [dict(THIRD)])
+    obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    return {"config": "5: affine, 3-planet synthetic, 8192 walkers per GPU (65536 / 8)", **_affine(s, obs, W)}
+
+
+def config1(steps=200):
+    np.random.seed(2017)
+    s = State(planets=[dict(p) for p in S2])
+    obs = FakeObservation(s, Npoints=200, error=1.5e-4, errorVar=2.5e-5, tmax=120.)   # mcmc_benchmark_mh.py:34
+    mh = mcmc.Mh(s, obs)
+    mh.set_scales({"m": 1.e-3, "a": 0.3, "h": 0.5, "k": 0.5, "l": np.pi / 2.})       # :52
+    mh.step_size = 10.0e-3                                                            # :53
+    tries = 0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tries += mh.step_force()
+    dt = time.perf_counter() - t0
+    return {"config": "1: reference-API Mh, single chain (mcmc_benchmark_mh.py)", "accepted_steps_per_s": steps / dt,
+            "logl_evals_per_s": tries / dt, "acceptance": steps / tries}
+
+
+def main():
+    which = sys.argv[1:] or ["2", "3", "4", "5", "1"]
+    for c in which:
+        out = {"1": config1, "2": config2, "3": config3, "4": config4, "5": config5}[c]()
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
