@@ -37,48 +37,66 @@ __device__ __forceinline__ double rsq_nr(double x) {
     return fma(y, e * fma(0.375, e, 0.5), y);
 }
 
-// ---- Stumpff functions c0..c3 (Danby): series for |z| <= 1, quartering+doubling otherwise ------
-__device__ __forceinline__ void stumpff_full(double z, double& c0, double& c1, double& c2, double& c3);
-
-// Short series for the small arguments of the fine levels: |z| <= 0.01 needs 5 terms per function
-// (remainder z^5/12! < 1e-19 relative), which is what the finest Richardson level sees
-// (z ~ (n h)^2 ~ 0.004 at the default P/96); larger |z| takes the 9-term path.
-__device__ __forceinline__ void stumpff(double z, double& c0, double& c1, double& c2, double& c3) {
-    if (fabs(z) <= 0.01) {
-        const double w = -z, w2 = w * w;
-        const double C2 = fma(w2 * w2, 1.0 / 3628800.0,
-                              fma(w2, fma(w, 1.0 / 40320.0, 1.0 / 720.0), fma(w, 1.0 / 24.0, 0.5)));
-        const double C3 = fma(w2 * w2, 1.0 / 39916800.0,
-                              fma(w2, fma(w, 1.0 / 362880.0, 1.0 / 5040.0), fma(w, 1.0 / 120.0, 1.0 / 6.0)));
-        c2 = C2;
-        c3 = C3;
-        c1 = 1.0 - z * C3;
-        c0 = 1.0 - z * C2;
-    } else {
-        stumpff_full(z, c0, c1, c2, c3);
-    }
+// a*b + k with k wave-uniform (an SGPR pair): a three-address v_fma_f64.  Plain fma() with a
+// constant addend is selected as the two-address v_fmac_f64 plus a copy of the constant into the
+// destination on every use; the hot polynomials below avoid that copy.
+__device__ __forceinline__ double fma_sk(double a, double b, double k) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
 }
 
+// x^(-3/2) straight from v_rsq_f64: with y = rsq(x), e = 1 - x y^2,
+//   x^(-3/2) = y^3 (1 - e)^(-3/2) = y^3 (1 + 3e/2 + 15e^2/8 + O(e^3))      (|e| ~ 5e-8)
+__device__ __forceinline__ double rcube_nr(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    const double y2 = y * y;
+    const double y3 = y2 * y;
+    const double e = fma(-x, y2, 1.0);
+    return fma(y3, e * fma_sk(e, 1.875, 1.5), y3);
+}
+
+// ---- Stumpff functions (Danby) ------------------------------------------------------------------
+// c2 = sum_j (-z)^j / (2j+2)!,  c3 = sum_j (-z)^j / (2j+3)!;  c1 = 1 - z c3,  c0 = 1 - z c2.
+//
+// Hot path: c2, c3 by Horner in z with NT terms (one fma per term with the coefficient in an
+// SGPR: no constant copies).  The truncation error is below 1e-19 relative for |z| <= B(NT):
+//   NT = 6: B = 0.04   (z^6/14! <= 5e-20)      NT = 8: B = 0.3   (z^8/18! <= 1e-20)
+// The term count is chosen per extrapolation level (wave-uniform, see logl_kernel), and lanes
+// with |z| > B(NT) redo the evaluation with stumpff_full, so a walker's result depends only on
+// its own (z, level), never on the other lanes of the wave.
+template <int NT>
+__device__ __forceinline__ constexpr double stumpff_bound() {
+    return NT >= 8 ? 0.3 : 0.04;
+}
+
+template <int NT>
+__device__ __forceinline__ void stumpff23(double z, double& c2, double& c3) {
+    constexpr double K2[9] = {1.0 / 2.0,         -1.0 / 24.0,           1.0 / 720.0,
+                              -1.0 / 40320.0,    1.0 / 3628800.0,       -1.0 / 479001600.0,
+                              1.0 / 87178291200.0, -1.0 / 20922789888000.0, 1.0 / 6402373705728000.0};
+    constexpr double K3[9] = {1.0 / 6.0,           -1.0 / 120.0,           1.0 / 5040.0,
+                              -1.0 / 362880.0,     1.0 / 39916800.0,       -1.0 / 6227020800.0,
+                              1.0 / 1307674368000.0, -1.0 / 355687428096000.0, 1.0 / 121645100408832000.0};
+    double a = fma_sk(z, K2[NT - 1], K2[NT - 2]), b = fma_sk(z, K3[NT - 1], K3[NT - 2]);
+#pragma unroll
+    for (int j = NT - 3; j >= 0; j--) {
+        a = fma_sk(a, z, K2[j]);
+        b = fma_sk(b, z, K3[j]);
+    }
+    c2 = a;
+    c3 = b;
+}
+
+// Any |z|: quarter z until |z| <= 0.3, 8-term series, then the double-angle recurrences.
 __device__ __forceinline__ void stumpff_full(double z, double& c0, double& c1, double& c2, double& c3) {
-    // c2 = sum_j (-z)^j / (2j+2)!,  c3 = sum_j (-z)^j / (2j+3)!   (8 terms: error < z^8/18! <= 1e-19
-    // for |z| <= 0.5; the level-1 step keeps |z| = (n dt)^2 <~ 0.07 on the benchmark configs)
     int n = 0;
-    while (fabs(z) > 0.5 && n < 40) {  // rare: only for large steps / hyperbolic orbits
+    while (fabs(z) > 0.3 && n < 40) {  // rare: only for large steps / hyperbolic orbits
         z *= 0.25;
         n++;
     }
-    // Estrin evaluation in w = -z (dependency depth 4 instead of 8 for Horner)
-    const double w = -z, w2 = w * w, w4 = w2 * w2;
-    const double a2 = fma(w4,
-                          fma(w2, fma(w, 1.0 / 6402373705728000.0, 1.0 / 20922789888000.0),
-                              fma(w, 1.0 / 87178291200.0, 1.0 / 479001600.0)),
-                          fma(w2, fma(w, 1.0 / 3628800.0, 1.0 / 40320.0), fma(w, 1.0 / 720.0, 1.0 / 24.0)));
-    const double a3 = fma(w4,
-                          fma(w2, fma(w, 1.0 / 121645100408832000.0, 1.0 / 355687428096000.0),
-                              fma(w, 1.0 / 1307674368000.0, 1.0 / 6227020800.0)),
-                          fma(w2, fma(w, 1.0 / 39916800.0, 1.0 / 362880.0), fma(w, 1.0 / 5040.0, 1.0 / 120.0)));
-    // c2 = 1/2! + w (1/4! + w (1/6! + ...)) ; c3 = 1/3! + w (1/5! + ...)
-    double C2 = fma(w, a2, 0.5), C3 = fma(w, a3, 1.0 / 6.0);
+    double C2, C3;
+    stumpff23<8>(z, C2, C3);
     double C1 = 1.0 - z * C3;
     double C0 = 1.0 - z * C2;
     for (; n > 0; n--) {
@@ -169,14 +187,32 @@ template <int NP>
 struct Lane {
     double rx, ry, vx, vy;  // own Jacobi coordinate
     double r, ir;           // |r'| and 1/|r'| at the current positions (carried from the drift)
-    double GM;              // interior mass M_p (G = 1) of the own Jacobi coordinate
+    double GM, GM2;         // interior mass M_p (G = 1) of the own Jacobi coordinate, and 2 M_p
     double m[NP];           // planet masses
     double iMi[NP + 1];     // 1 / interior masses, iMi[0] = 1 (M_star = 1)
     double mu[NP];          // m_q / M_q: star barycentric velocity weights
-    double dmin2;           // (hill_factor * max r_Hill)^2
+    double dmin2, idmin2;   // (hill_factor * max r_Hill)^2 and its reciprocal
+    double kA, kB, kC;      // closed-form 2-planet kick coefficients of the own lane (kick2)
     int p;                  // own planet index (lane % L, clamped to NP-1)
-    int enc;                // encounter flag (identical on all lanes of the group)
+    bool enc;               // encounter flag (identical on all lanes of the group)
 };
+
+// Derived per-lane constants (after p, GM, m, iMi, dmin2 are set).
+template <int NP>
+__device__ __forceinline__ void lane_finish(Lane<NP>& s) {
+    s.GM2 = 2.0 * s.GM;
+    s.idmin2 = 1.0 / s.dmin2;  // +inf for dmin2 = 0 (no exit distance)
+    if constexpr (NP == 2) {
+        // kick2: lane of planet 1: (A, B, C) = (0, -m2, m2); planet 2: (M2, -M2/M1, -m1 M2/M1)
+        const bool p1 = s.p == 0;
+        const double q = s.GM * s.iMi[1];
+        s.kA = p1 ? 0.0 : s.GM;
+        s.kB = p1 ? -s.m[1] : -q;
+        s.kC = p1 ? s.m[1] : -q * s.m[0];
+    } else {
+        s.kA = s.kB = s.kC = 0.0;
+    }
+}
 
 // Safeguarded universal-Kepler solve for the rare hard cases (a step spanning a large part of an
 // orbit, a poor initial guess): f(X) = r0 G1 + eta0 G2 + GM G3 - dt is increasing in X (f' = r > 0)
@@ -188,7 +224,7 @@ __device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, 
     double lo = 0.0, hi = dt / r0;
     double c0, c1, c2, c3;
     for (int i = 0; i < 200; i++) {  // expand until sgn*f(hi) > 0
-        stumpff(beta * hi * hi, c0, c1, c2, c3);
+        stumpff_full(beta * hi * hi, c0, c1, c2, c3);
         const double f = r0 * hi * c1 + eta * hi * hi * c2 + GM * hi * hi * hi * c3 - dt;
         if (sgn * f > 0.0 || !(f == f)) break;
         lo = hi;
@@ -196,7 +232,7 @@ __device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, 
     }
     double X = 0.5 * (lo + hi);
     for (int i = 0; i < 200; i++) {
-        stumpff(beta * X * X, c0, c1, c2, c3);
+        stumpff_full(beta * X * X, c0, c1, c2, c3);
         const double g1 = X * c1, g2 = X * X * c2, g3 = X * X * X * c3;
         const double f = r0 * g1 + eta * g2 + GM * g3 - dt;
         const double fp = r0 * c0 + eta * g1 + GM * g2;
@@ -211,7 +247,7 @@ __device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, 
         X = Xn;
         if (conv) break;
     }
-    stumpff(beta * X * X, c0, c1, c2, c3);
+    stumpff_full(beta * X * X, c0, c1, c2, c3);
     Xo = X;
     G0 = c0;
     G1 = X * c1;
@@ -219,88 +255,133 @@ __device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, 
     G3 = X * X * X * c3;
 }
 
+// One Halley step for the universal Kepler equation f(X) = r0 G1 + eta0 G2 + GM G3 - dt at X = x
+// with the NT-term Stumpff series: returns the G-functions at x, f'(x), f''(x), the correction q
+// (X_new = x - q), z = beta x^2 and x^3.  Valid only for |z| <= stumpff_bound<NT>() (the caller
+// sends other lanes to the general solver).
+template <int NT>
+__device__ __forceinline__ void halley(double x, double beta, double r0, double eta, double zeta, double GM,
+                                       double dt, double& G0, double& G1, double& G2, double& G3, double& fp,
+                                       double& fpp, double& q, double& z, double& x3) {
+    const double x2 = x * x;
+    z = beta * x2;
+    x3 = x2 * x;
+    double c2, c3;
+    stumpff23<NT>(z, c2, c3);
+    G3 = x3 * c3;
+    G2 = x2 * c2;
+    G1 = fma(-beta, G3, x);  // x c1 = x (1 - z c3)
+    G0 = fma(-z, c2, 1.0);
+    const double f = fma(GM, G3, fma(eta, G2, fma(r0, G1, -dt)));
+    fp = fma(GM, G2, fma(eta, G1, r0 * G0));
+    fpp = fma(zeta, G1, eta * G0);
+    const double den = fma(-0.5 * f, fpp, fp * fp);
+    const double num = f * fp;
+    // num/den: v_rcp_f64 (~5e-8) + one residual correction (error ~2e-15 of the correction)
+    const double rd = __builtin_amdgcn_rcp(den);
+    const double q0 = num * rd;
+    q = fma(rd, fma(-den, q0, num), q0);
+}
+
+// Acceptance of a Halley step with relative correction qt = q/x: the error left in X is
+// ~ c z qt^3 (c << 1; Halley is cubic and its constant scales with z = beta x^2), and the Taylor
+// update of the G-functions over the correction (below) truncates at ~ z qt^3 / 3 relative.  Both
+// stay below ~1e-17 when |q^3 z| <= 3e-17 |x^3|.  At the default step (P/24 .. P/96) and
+// e <~ 0.3 the finest level passes after one step; the coarse levels take a second one.
+__device__ __forceinline__ bool halley_done(double q, double z, double x3) {
+    return !(fabs((q * q) * (q * z)) > 3e-17 * fabs(x3));
+}
+
 // Kepler drift of the own Jacobi coordinate by dt in universal variables (Danby): solve
-// r0 G1 + eta0 G2 + GM G3 = dt for X by Halley iterations from the third-order Taylor guess
-//   X = dt/r0 - eta0 dt^2/(2 r0^3) + dt^3 (3 eta0^2/r0^5 - v0^2/r0^3 + GM/r0^4)/6.
-// Halley converges cubically, so for small steps (|beta X^2| <= 0.5) once a correction is
-// <= 1e-6 |X| the remaining error is below 1e-18 |X| and the lane stops (large steps iterate to
-// full convergence) (each lane at its own convergence: results do not depend on the
-// other lanes of the wave).  The G-functions at the final X = x + d are Taylor-updated from the
-// last evaluation at x (dG0/dX = -beta G1, dG_k/dX = G_{k-1}), and |r| after the drift comes out
-// of the solution (r = r0 G0 + eta0 G1 + GM G2): no square root anywhere in the step.
-template <int NP>
+// r0 G1 + eta0 G2 + GM G3 = dt for X by Halley steps from the third-order Taylor guess
+//   X = u (1 - u s/2 + u^2 (s^2/2 + (beta - v0^2)/12)),   u = dt/r0, s = eta0/r0
+// (= dt/r0 - eta0 dt^2/(2 r0^3) + dt^3 (3 eta0^2/r0^5 - v0^2/r0^3 + GM/r0^4)/6), accepted by
+// halley_done.  Lanes that need a second step take it with the same short series; lanes still
+// unconverged after that (pericentre passages of very eccentric orbits) iterate in a per-lane
+// loop, and steps spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) take the bracketed
+// solver -- each lane at its own convergence, so results never depend on the other lanes of the
+// wave.  The G-functions at the final X = x - q are Taylor-updated from the evaluation at x
+// (dG0/dX = -beta G1, dG_k/dX = G_{k-1}), and |r| after the drift comes out of the solution
+// (r = r0 G0 + eta0 G1 + GM G2): no square root anywhere in the step.
+template <int NT, int NP>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;
-    const double v2 = s.vx * s.vx + s.vy * s.vy;
-    const double eta = s.rx * s.vx + s.ry * s.vy;
-    const double beta = 2.0 * GM * ir0 - v2;
-    const double zeta = GM - beta * r0;
-    const double i2 = ir0 * ir0;
-    const double e = eta * i2;
-    double X = dt * ir0 * (1.0 + dt * (-0.5 * e + dt * (3.0 * e * e - v2 * i2 + GM * i2 * ir0) * (1.0 / 6.0)));
-    double G0, G1, G2, G3, D, tol;
-    bool done;
-    {
-        const double x = X;
-        double c0, c1, c2, c3;
-        stumpff(beta * x * x, c0, c1, c2, c3);
-        const double g1 = x * c1, g2 = x * x * c2, g3 = x * x * x * c3;
-        const double f = r0 * g1 + eta * g2 + GM * g3 - dt;
-        const double fp = r0 * c0 + eta * g1 + GM * g2;
-        const double fpp = eta * c0 + zeta * g1;
-        const double dX = f * fp * rcp_nr(fp * fp - 0.5 * f * fpp);
-        G0 = c0;
-        G1 = g1;
-        G2 = g2;
-        G3 = g3;
-        D = -dX;
-        X = x - dX;
-        // small steps (|beta X^2| <= 0.5): a 1e-6 correction leaves < 1e-18; large steps (a step
-        // covering a sizeable part of an orbit) iterate to full convergence
-        tol = fabs(beta * X * X) <= 0.5 ? 1e-6 : 2e-16;
-        done = !(fabs(dX) > tol * fabs(X));
-    }
-    for (int it = 1; it < 8 && !__all(done); it++) {  // rare extra iterations (pericentre, big steps)
-        const double x = X;
-        double c0, c1, c2, c3;
-        stumpff(beta * x * x, c0, c1, c2, c3);
-        const double g1 = x * c1, g2 = x * x * c2, g3 = x * x * x * c3;
-        const double f = r0 * g1 + eta * g2 + GM * g3 - dt;
-        const double fp = r0 * c0 + eta * g1 + GM * g2;
-        const double fpp = eta * c0 + zeta * g1;
-        const double dX = f * fp * rcp_nr(fp * fp - 0.5 * f * fpp);
-        if (!done) {
-            G0 = c0;
-            G1 = g1;
-            G2 = g2;
-            G3 = g3;
-            D = -dX;
-            X = x - dX;
-            done = !(fabs(dX) > tol * fabs(X));
+    const double v2 = fma(s.vx, s.vx, s.vy * s.vy);
+    const double eta = fma(s.rx, s.vx, s.ry * s.vy);
+    const double beta = fma(s.GM2, ir0, -v2);
+    const double zeta = fma(-beta, r0, GM);
+    const double u = dt * ir0, sg = eta * ir0;
+    const double hs = 0.5 * sg;
+    const double t6 = fma(hs, sg, (beta - v2) * (1.0 / 12.0));
+    const double x = u * fma(u, fma(u, t6, -hs), 1.0);
+    double G0, G1, G2, G3, fp, fpp, Q, z, x3;
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3);
+    double X = x - Q;
+    bool zok = fabs(z) <= stumpff_bound<NT>();
+    bool done = zok && halley_done(Q, z, x3);
+    const bool hard = fabs(beta) * (u * u) > 0.5;
+    if constexpr (NT >= 8) {  // coarse levels: a second Halley step is the common case
+        if (__any(!done)) {
+            if (!done && zok) {
+                double q2;
+                halley<NT>(X, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, q2, z, x3);
+                Q = q2;
+                X = X - q2;
+                zok = fabs(z) <= stumpff_bound<NT>();
+                done = zok && halley_done(q2, z, x3);
+            }
         }
     }
-    // hard cases: steps spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) or no
-    // convergence above -> bracketed solve (divergent, rare; same regime split as the oracle)
-    if (!done || fabs(beta) * (dt * ir0) * (dt * ir0) > 0.5) {
-        kepler_safe(r0, eta, zeta, beta, GM, dt, X, G0, G1, G2, G3);
-        D = 0.0;
+    if (__builtin_expect(__any(!done || hard), 0)) {
+        // general solver for this lane: Halley with the full Stumpff evaluation (any z), then the
+        // bracketed solve for large steps or no convergence
+        if (!hard && !done) {
+            double xi = zok ? X : x;
+            for (int it = 0; it < 8 && !done; it++) {
+                double c0, c1, cc2, cc3;
+                const double zi = beta * xi * xi;
+                stumpff_full(zi, c0, c1, cc2, cc3);
+                const double g1 = xi * c1, g2 = xi * xi * cc2, g3 = xi * xi * xi * cc3;
+                const double ff = r0 * g1 + eta * g2 + GM * g3 - dt;
+                const double ffp = r0 * c0 + eta * g1 + GM * g2;
+                const double ffpp = eta * c0 + zeta * g1;
+                const double dX = ff * ffp / (ffp * ffp - 0.5 * ff * ffpp);
+                G0 = c0;
+                G1 = g1;
+                G2 = g2;
+                G3 = g3;
+                fp = ffp;
+                fpp = ffpp;
+                Q = dX;
+                done = halley_done(dX, zi, xi * xi * xi);
+                xi = xi - dX;
+            }
+            X = xi;
+        }
+        if (hard || !done) {
+            kepler_safe(r0, eta, zeta, beta, GM, dt, X, G0, G1, G2, G3);
+            fp = r0 * G0 + eta * G1 + GM * G2;
+            fpp = eta * G0 + zeta * G1;
+            Q = 0.0;
+        }
     }
-    const double d = D, d2 = 0.5 * d * d;
-    const double H0 = G0 - beta * (d * G1 + d2 * G0);
-    const double H1 = G1 + d * G0 - d2 * beta * G1;
-    const double H2 = G2 + d * G1 + d2 * G0;
-    const double H3 = G3 + d * G2 + d2 * G1 + (d2 * d * (1.0 / 3.0)) * G0;
-    const double rr = r0 * H0 + eta * H1 + GM * H2;
+    // Taylor update of the G-functions (and of r = f') from the last evaluation point to X
+    const double d = -Q, d2 = (0.5 * Q) * Q;
+    const double H1 = fma(d, G0, fma(-d2 * beta, G1, G1));
+    const double H2 = fma(d2, G0, fma(d, G1, G2));
+    const double H3 = fma(d2 * d * (1.0 / 3.0), G0, fma(d2, G1, fma(d, G2, G3)));
+    const double f3 = fma(zeta, G0, -(beta * eta) * G1);  // third derivative of f
+    const double rr = fma(d2, f3, fma(d, fpp, fp));
     const double irr = rcp_nr(rr);
     const double gG2 = GM * H2;
-    const double f = 1.0 - gG2 * ir0;
-    const double g = dt - GM * H3;
-    const double fd = -GM * H1 * irr * ir0;
-    const double gd = 1.0 - gG2 * irr;
-    const double nrx = f * s.rx + g * s.vx;
-    const double nry = f * s.ry + g * s.vy;
-    const double nvx = fd * s.rx + gd * s.vx;
-    const double nvy = fd * s.ry + gd * s.vy;
+    const double f_ = fma(-gG2, ir0, 1.0);
+    const double g_ = fma(-GM, H3, dt);
+    const double fd = -(GM * H1) * (irr * ir0);
+    const double gd = fma(-gG2, irr, 1.0);
+    const double nrx = fma(f_, s.rx, g_ * s.vx);
+    const double nry = fma(f_, s.ry, g_ * s.vy);
+    const double nvx = fma(fd, s.rx, gd * s.vx);
+    const double nvy = fma(fd, s.ry, gd * s.vy);
     s.rx = nrx;
     s.ry = nry;
     s.vx = nvx;
@@ -341,7 +422,7 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
         ax[i] = 0.0;
         ay[i] = 0.0;
     }
-    int enc = 0;
+    bool enc = false;
     // star -- planet 1 distance is |r'_1|, already known to planet 1's lane from its drift
     const double ir01 = (NP == 1) ? s.ir : grp_get<L>(s.ir, 0);
 #pragma unroll
@@ -352,10 +433,10 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
             double ir;
             if (i == 0 && j == 1) {
                 ir = ir01;
-                enc |= (ir * ir * s.dmin2 > 1.0);
+                enc = enc | (ir * ir > s.idmin2);
             } else {
                 const double r2 = dx * dx + dy * dy;
-                enc |= (r2 < s.dmin2);
+                enc = enc | (r2 < s.dmin2);
                 ir = rsq_nr(r2);
             }
             const double ir3 = ir * ir * ir;
@@ -367,7 +448,7 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
             ay[j] -= mi * ir3 * dy;
         }
     }
-    s.enc |= enc;
+    s.enc = s.enc | enc;
     // Jacobi acceleration of the own coordinate (index i = p + 1)
     double max_ = ax[0], may_ = ay[0];  // M_star = 1
     double ajx = 0.0, ajy = 0.0;
@@ -400,18 +481,12 @@ __device__ __forceinline__ void kick2(Lane<2>& s, double dt) {
     const double c = s.m[0] * s.iMi[1];  // m_1 / M_1
     const double x2 = fma(c, x1, R2x), y2 = fma(c, y1, R2y);
     const double dx12 = x2 - x1, dy12 = y2 - y1;
-    const double r02sq = x2 * x2 + y2 * y2;
-    const double r12sq = dx12 * dx12 + dy12 * dy12;
-    s.enc |= (r02sq < s.dmin2) | (r12sq < s.dmin2) | (ir01 * ir01 * s.dmin2 > 1.0);
-    const double i02 = rsq_nr(r02sq), i12 = rsq_nr(r12sq);
-    const double i02c = i02 * i02 * i02, i12c = i12 * i12 * i12;
-    // lane of planet 1: (A, B, C) = (0, -m2, m2); lane of planet 2: (M2/r'^3, -M2/M1, -m1 M2/M1)
-    const bool p1 = s.p == 0;
-    const double q = s.GM * s.iMi[1];
-    const double A = p1 ? 0.0 : s.GM * (s.ir * s.ir * s.ir);
-    const double B = p1 ? -s.m[1] : -q;
-    const double C = p1 ? s.m[1] : -q * s.m[0];
-    const double bx = B * i02c, cx = C * i12c;
+    const double r02sq = fma(x2, x2, y2 * y2);
+    const double r12sq = fma(dx12, dx12, dy12 * dy12);
+    s.enc = s.enc | (r02sq < s.dmin2) | (r12sq < s.dmin2) | (ir01 * ir01 > s.idmin2);
+    const double i02c = rcube_nr(r02sq), i12c = rcube_nr(r12sq);
+    const double A = s.kA * (s.ir * (s.ir * s.ir));
+    const double bx = s.kB * i02c, cx = s.kC * i12c;
     s.vx = fma(dt, fma(A, s.rx, fma(bx, x2, cx * dx12)), s.vx);
     s.vy = fma(dt, fma(A, s.ry, fma(bx, y2, cx * dy12)), s.vy);
 }

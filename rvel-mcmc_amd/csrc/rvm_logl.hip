@@ -23,6 +23,19 @@
 
 namespace rvm {
 
+// One epoch-to-epoch segment of ns Wisdom-Holman DKD steps of size h.
+template <int NT, int NP, int L>
+__device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
+    drift<NT>(s, 0.5 * h);
+#pragma unroll 2
+    for (int j = 0; j < ns - 1; j++) {
+        kick<NP, L>(s, h);
+        drift<NT>(s, h);
+    }
+    kick<NP, L>(s, h);
+    drift<NT>(s, 0.5 * h);
+}
+
 template <int NP>
 __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan P, const int W,
                                                                    const double* __restrict__ params,
@@ -48,7 +61,9 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     extern __shared__ double s_sched[];  // [E] seg_len | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
 
     const DirSched S = d ? P.bwd : P.fwd;
-    const int mult = P.mult[lvl];
+    // wave-uniform copies (SGPRs): the level picks the Stumpff series length (rvm_device.h)
+    const int mult = P.mult[__builtin_amdgcn_readfirstlane(lvl)];
+    const bool fine = mult >= 3;
     const int E = S.n_epochs;
     double* l_len = s_sched;
     double* l_rv = s_sched + E;
@@ -146,7 +161,8 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     }
     s.r = sqrt(s.rx * s.rx + s.ry * s.ry);
     s.ir = 1.0 / s.r;
-    s.enc = 0;
+    s.enc = false;
+    lane_finish(s);
     {
         Lane<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
         kick<NP, L>(t0, 0.0);
@@ -165,13 +181,10 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         const int ns = n1 * mult;
         if (ns > 0) {
             const double h = len / (double)ns;
-            drift(s, 0.5 * h);
-            for (int j = 0; j < ns - 1; j++) {
-                kick<NP, L>(s, h);
-                drift(s, h);
-            }
-            kick<NP, L>(s, h);
-            drift(s, 0.5 * h);
+            if (fine)
+                segment<6, NP, L>(s, h, ns);
+            else
+                segment<8, NP, L>(s, h, ns);
         }
         const double v0 = star_vx<NP, L>(s);
         if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
@@ -187,7 +200,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         n1 = n1_next;
         len = len_next;
     }
-    if (pl_idx == 0) s_enc[lvl][slot] = s.enc | (status == RVM_STATUS_PRIOR ? 2 : 0);
+    if (pl_idx == 0) s_enc[lvl][slot] = (s.enc ? 1 : 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
     if (lvl == 0 && lane < WPB) {
         const int wo = blockIdx.x * WPB + lane;
