@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 1
+#define RVM_ABI_VERSION 2
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -57,10 +57,15 @@ extern "C" {
 /* Integrator configuration of a plan. */
 typedef struct {
     int32_t n_planets;     /* 1..RVM_MAX_PLANETS                                                  */
-    double dt;             /* base (level-1) step in code units (yr/2pi); segments between epochs
-                              are cut into ceil(len/dt) equal steps                                */
-    int32_t n_levels;      /* Richardson levels, 1..RVM_MAX_LEVELS; level k runs (k+1)x the steps   */
+    double dt;             /* base step in code units (yr/2pi); the segment between two epochs is
+                              cut into n = ceil(len/dt) base steps                                 */
+    int32_t n_levels;      /* Richardson levels, 1..RVM_MAX_LEVELS                                  */
     double npoints_norm;   /* obs.Npoints: chi2 is divided by this (state.py:98), NOT the epoch count */
+    int32_t level_mult[RVM_MAX_LEVELS]; /* level k integrates each segment with n * level_mult[k]
+                              steps (distinct, >= 1, at most 64); all zero = harmonic 1, 2, ..., n_levels */
+    double period_hint;    /* shortest orbital period the walkers are expected to have (code units):
+                              sizes the per-level Stumpff series (performance only, results are
+                              exact for any orbit); 0 = longest series on every level              */
 } rvm_config;
 
 typedef struct rvm_plan rvm_plan;

@@ -64,6 +64,13 @@ def lib():
         L.rvo_whx_rv.restype = C.c_int
         L.rvo_logl_whx_batch.argtypes = [C.c_int, C.c_int, dp, C.c_int, C.c_int, C.c_double, dp, dp, dp, C.c_int,
                                          C.c_double, C.c_double, C.c_int, dp, C.POINTER(C.c_int32)]
+        ip = C.POINTER(C.c_int)
+        L.rvo_richardson_weights_seq.argtypes = [C.c_int, ip, dp]
+        L.rvo_whx_rv_seq.argtypes = [C.c_int, dp, C.c_double, dp, C.c_int, C.c_double, C.c_int, ip, dp]
+        L.rvo_whx_rv_seq.restype = C.c_int
+        L.rvo_logl_whx_seq_batch.argtypes = [C.c_int, C.c_int, dp, C.c_int, C.c_int, C.c_double, dp, dp, dp,
+                                             C.c_int, C.c_double, C.c_double, C.c_int, ip, dp,
+                                             C.POINTER(C.c_int32)]
         _LIB = L
     return _LIB
 
@@ -160,6 +167,8 @@ def logl_wh(planets, obs, h_target, sub=1, hill_factor=1.0):
 
 
 def richardson_weights(nl):
+    if not isinstance(nl, (int, np.integer)):
+        return richardson_weights_seq(nl)
     w = np.zeros(nl)
     lib().rvo_richardson_weights(int(nl), _p(w))
     return w
@@ -170,12 +179,20 @@ def whx_rv(planets, times, dt, n_levels, hill_factor=0.0):
     pl = _f64(pal_params(planets))
     t = _f64(times)
     rv = np.full(len(t), np.nan)
+    if not isinstance(n_levels, (int, np.integer)):
+        m, mp = _mult(n_levels)
+        st = lib().rvo_whx_rv_seq(len(planets), _p(pl), float(hill_factor), _p(t), len(t), float(dt), len(m), mp,
+                                  _p(rv))
+        return rv, st
     st = lib().rvo_whx_rv(len(planets), _p(pl), float(hill_factor), _p(t), len(t), float(dt), int(n_levels), _p(rv))
     return rv, st
 
 
 def logl_whx_batch(params, np_, obs, dt, n_levels, hill_factor=1.0, has_hk=1, has_inc=0):
-    """params [W][np][7] -> (logl[W], status[W]) with the kernel's algorithm (T1 reference)."""
+    """params [W][np][7] -> (logl[W], status[W]) with the kernel's algorithm (T1 reference).
+    n_levels: int (harmonic levels 1..n) or a sequence of level multipliers."""
+    if not isinstance(n_levels, (int, np.integer)):
+        return logl_whx_seq_batch(params, np_, obs, dt, n_levels, hill_factor, has_hk, has_inc)
     pl = _f64(params)
     W = pl.shape[0]
     t = _f64(np.concatenate([obs.tf, obs.tb]))
@@ -186,6 +203,34 @@ def logl_whx_batch(params, np_, obs, dt, n_levels, hill_factor=1.0, has_hk=1, ha
     lib().rvo_logl_whx_batch(W, np_, _p(pl), has_hk, has_inc, float(hill_factor), _p(t), _p(rv), _p(er), len(t),
                              float(obs.Npoints), float(dt), int(n_levels), _p(out),
                              st.ctypes.data_as(C.POINTER(C.c_int32)))
+    return out, st
+
+
+def _mult(mult):
+    m = np.ascontiguousarray(np.asarray(mult, dtype=np.int32))
+    return m, m.ctypes.data_as(C.POINTER(C.c_int))
+
+
+def richardson_weights_seq(mult):
+    m, mp = _mult(mult)
+    w = np.zeros(len(m))
+    lib().rvo_richardson_weights_seq(len(m), mp, _p(w))
+    return w
+
+
+def logl_whx_seq_batch(params, np_, obs, dt, mult, hill_factor=1.0, has_hk=1, has_inc=0):
+    """As logl_whx_batch with level k stepping dt/mult[k] (general extrapolation sequence)."""
+    pl = _f64(params)
+    W = pl.shape[0]
+    t = _f64(np.concatenate([obs.tf, obs.tb]))
+    rv = _f64(np.concatenate([obs.rvf, obs.rvb]))
+    er = _f64(np.concatenate([obs.errorf, obs.errorb]))
+    out = np.zeros(W)
+    st = np.zeros(W, dtype=np.int32)
+    m, mp = _mult(mult)
+    lib().rvo_logl_whx_seq_batch(W, np_, _p(pl), has_hk, has_inc, float(hill_factor), _p(t), _p(rv), _p(er),
+                                 len(t), float(obs.Npoints), float(dt), len(m), mp, _p(out),
+                                 st.ctypes.data_as(C.POINTER(C.c_int32)))
     return out, st
 
 

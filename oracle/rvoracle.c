@@ -891,28 +891,36 @@ int rvo_logl_wh(int np, const double* pl, int has_hk, int has_inc, double hill_f
 /*   sum_L w_L rv_L with w the Lagrange-at-zero weights in x = 1/(L+1)^2; an encounter seen by   */
 /*   any level marks the walker.                                                                */
 /* ------------------------------------------------------------------------------------------ */
-void rvo_richardson_weights(int nl, double* w) {
+/* Lagrange-at-zero weights for an arbitrary multiplier sequence: level k steps dt/mult[k],
+ * x_k = 1/mult[k]^2 (the harmonic default is mult = 1, 2, ..., nl). */
+void rvo_richardson_weights_seq(int nl, const int* mult, double* w) {
     for (int k = 0; k < nl; k++) {
-        const double xk = 1.0 / ((double)(k + 1) * (k + 1));
+        const double xk = 1.0 / ((double)mult[k] * mult[k]);
         double wk = 1.0;
         for (int j = 0; j < nl; j++) {
             if (j == k) continue;
-            const double xj = 1.0 / ((double)(j + 1) * (j + 1));
+            const double xj = 1.0 / ((double)mult[j] * mult[j]);
             wk *= xj / (xj - xk);
         }
         w[k] = wk;
     }
 }
 
-int rvo_whx_rv(int np, const double* pl, double hill_factor, const double* t, int n, double dt, int nl,
-               double* rv) {
+void rvo_richardson_weights(int nl, double* w) {
+    int mult[8];
+    for (int k = 0; k < nl && k < 8; k++) mult[k] = k + 1;
+    rvo_richardson_weights_seq(nl, mult, w);
+}
+
+int rvo_whx_rv_seq(int np, const double* pl, double hill_factor, const double* t, int n, double dt, int nl,
+                   const int* mult, double* rv) {
     double w[8];
-    rvo_richardson_weights(nl, w);
+    rvo_richardson_weights_seq(nl, mult, w);
     double* tmp = (double*)malloc(sizeof(double) * (size_t)(n + 1));
     for (int i = 0; i < n; i++) rv[i] = 0.0;
     int st = RVO_OK;
     for (int k = 0; k < nl; k++) {
-        const int s = rvo_wh_rv(np, pl, hill_factor, t, n, dt, k + 1, tmp);
+        const int s = rvo_wh_rv(np, pl, hill_factor, t, n, dt, mult[k], tmp);
         if (s != RVO_OK) {
             if (st == RVO_OK || s == RVO_ENCOUNTER) st = s;
             continue;
@@ -923,14 +931,22 @@ int rvo_whx_rv(int np, const double* pl, double hill_factor, const double* t, in
     return st;
 }
 
-int rvo_logl_whx(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
-                 const double* rvobs, const double* err, int n, double npoints, double dt, int nl, double* logl) {
+int rvo_whx_rv(int np, const double* pl, double hill_factor, const double* t, int n, double dt, int nl,
+               double* rv) {
+    int mult[8];
+    for (int k = 0; k < nl && k < 8; k++) mult[k] = k + 1;
+    return rvo_whx_rv_seq(np, pl, hill_factor, t, n, dt, nl, mult, rv);
+}
+
+int rvo_logl_whx_seq(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
+                     const double* rvobs, const double* err, int n, double npoints, double dt, int nl, const int* mult,
+                     double* logl) {
     if (rvo_prior_hard(np, pl, has_hk, has_inc)) {
         *logl = -INFINITY;
         return RVO_PRIOR;
     }
     double* rv = (double*)malloc(sizeof(double) * (size_t)(n + 1));
-    int st = rvo_whx_rv(np, pl, hill_factor, t, n, dt, nl, rv);
+    int st = rvo_whx_rv_seq(np, pl, hill_factor, t, n, dt, nl, mult, rv);
     double chi2 = 0.0;
     if (st == RVO_OK)
         for (int i = 0; i < n; i++) chi2 += ((rv[i] - rvobs[i]) * (rv[i] - rvobs[i])) / (err[i] * err[i]);
@@ -947,6 +963,13 @@ int rvo_logl_whx(int np, const double* pl, int has_hk, int has_inc, double hill_
     return RVO_OK;
 }
 
+int rvo_logl_whx(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
+                 const double* rvobs, const double* err, int n, double npoints, double dt, int nl, double* logl) {
+    int mult[8];
+    for (int k = 0; k < nl && k < 8; k++) mult[k] = k + 1;
+    return rvo_logl_whx_seq(np, pl, has_hk, has_inc, hill_factor, t, rvobs, err, n, npoints, dt, nl, mult, logl);
+}
+
 /* batch over walkers: params [W][np][7]; threads: OpenMP-free (callers parallelise if they wish) */
 void rvo_logl_whx_batch(int W, int np, const double* pl, int has_hk, int has_inc, double hill_factor,
                         const double* t, const double* rvobs, const double* err, int n, double npoints, double dt,
@@ -954,4 +977,12 @@ void rvo_logl_whx_batch(int W, int np, const double* pl, int has_hk, int has_inc
     for (int w = 0; w < W; w++)
         status[w] = rvo_logl_whx(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs, err,
                                  n, npoints, dt, nl, logl + w);
+}
+
+void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has_inc, double hill_factor,
+                            const double* t, const double* rvobs, const double* err, int n, double npoints, double dt,
+                            int nl, const int* mult, double* logl, int32_t* status) {
+    for (int w = 0; w < W; w++)
+        status[w] = rvo_logl_whx_seq(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs,
+                                     err, n, npoints, dt, nl, mult, logl + w);
 }

@@ -63,6 +63,19 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     if (!(cfg->dt > 0.0) || !std::isfinite(cfg->dt)) return fail(-1, "rvm_plan_create: dt must be > 0");
     if (n_obs < 0 || max_walkers < 1) return fail(-1, "rvm_plan_create: bad sizes");
     if (!(cfg->npoints_norm != 0.0)) return fail(-1, "rvm_plan_create: npoints_norm must be nonzero");
+    int mult[RVM_MAX_LEVELS];
+    bool harmonic = true;
+    for (int k = 0; k < cfg->n_levels; k++) harmonic = harmonic && cfg->level_mult[k] == 0;
+    int max_mult = 1;
+    for (int k = 0; k < cfg->n_levels; k++) {
+        mult[k] = harmonic ? k + 1 : cfg->level_mult[k];
+        if (mult[k] < 1 || mult[k] > 64) return fail(-1, "rvm_plan_create: level_mult out of range (1..64)");
+        for (int j = 0; j < k; j++)
+            if (mult[j] == mult[k]) return fail(-1, "rvm_plan_create: level_mult entries must be distinct");
+        max_mult = mult[k] > max_mult ? mult[k] : max_mult;
+    }
+    if (!(cfg->period_hint >= 0.0) || !std::isfinite(cfg->period_hint))
+        return fail(-1, "rvm_plan_create: period_hint must be >= 0");
     for (int i = 0; i < n_obs; i++) {
         if (!std::isfinite(t[i]) || !std::isfinite(rv[i]) || !std::isfinite(sigma[i]))
             return fail(-1, "rvm_plan_create: non-finite observation");
@@ -93,7 +106,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             D.os2.push_back(sigma[i] * sigma[i]);
             total_steps[dd] += n;
         }
-        if (total_steps[dd] * (long long)cfg->n_levels > (1LL << 30))
+        if (total_steps[dd] * (long long)max_mult > (1LL << 30))
             return fail(-1, "rvm_plan_create: dt too small for the epoch span");
         if (D.idx.size() > (size_t)RVM_MAX_EPOCHS_PER_DIRECTION)
             return fail(-1, "rvm_plan_create: too many epochs in one direction (the schedule is staged in LDS)");
@@ -153,20 +166,29 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.n_levels = cfg->n_levels;
     P.npoints = cfg->npoints_norm;
     P.n_obs = n_obs;
-    // Richardson weights for the h^2 expansion: level k uses step h/(k+1); Lagrange at 0 in x = 1/n^2
+    // Richardson weights for the h^2 expansion: level k steps dt/mult[k]; Lagrange at 0 in x = 1/mult^2
     for (int k = 0; k < RVM_MAX_LEVELS; k++) {
-        P.mult[k] = k + 1;
+        P.mult[k] = k < cfg->n_levels ? mult[k] : 1;
         P.lw[k] = 0.0;
+        P.nt[k] = 8;
     }
     for (int k = 0; k < cfg->n_levels; k++) {
-        const double xk = 1.0 / ((double)(k + 1) * (k + 1));
+        const double xk = 1.0 / ((double)mult[k] * mult[k]);
         double wk = 1.0;
         for (int j = 0; j < cfg->n_levels; j++) {
             if (j == k) continue;
-            const double xj = 1.0 / ((double)(j + 1) * (j + 1));
+            const double xj = 1.0 / ((double)mult[j] * mult[j]);
             wk *= xj / (xj - xk);
         }
         P.lw[k] = wk;
+        // Stumpff series length (rvm_device.h stumpff_bound): nominal z = (2 pi h / P)^2 on a
+        // circular orbit, x3 for the pericentre of e ~ 0.3 orbits; lanes beyond the bound take the
+        // general evaluation, so this choice only affects speed
+        if (cfg->period_hint > 0.0) {
+            const double nh = 2.0 * M_PI * cfg->dt / (mult[k] * cfg->period_hint);
+            const double zn = 3.0 * nh * nh;
+            P.nt[k] = zn <= 0.04 ? 6 : (zn <= 0.12 ? 7 : 8);
+        }
     }
     *out = plan;
     return 0;

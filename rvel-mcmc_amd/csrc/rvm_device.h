@@ -37,6 +37,11 @@ __device__ __forceinline__ double rsq_nr(double x) {
     return fma(y, e * fma(0.375, e, 0.5), y);
 }
 
+// Wave-wide vote straight from the compare mask (s_cmp on the ballot, no VGPR round trip as
+// with __any, whose int argument is materialised with v_cndmask and compared again).
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 // a*b + k with k wave-uniform (an SGPR pair): a three-address v_fma_f64.  Plain fma() with a
 // constant addend is selected as the two-address v_fmac_f64 plus a copy of the constant into the
 // destination on every use; the hot polynomials below avoid that copy.
@@ -61,13 +66,13 @@ __device__ __forceinline__ double rcube_nr(double x) {
 //
 // Hot path: c2, c3 by Horner in z with NT terms (one fma per term with the coefficient in an
 // SGPR: no constant copies).  The truncation error is below 1e-19 relative for |z| <= B(NT):
-//   NT = 6: B = 0.04   (z^6/14! <= 5e-20)      NT = 8: B = 0.3   (z^8/18! <= 1e-20)
+//   NT = 6: B = 0.04 (z^6/14! <= 5e-20)   NT = 7: B = 0.12 (z^7/16! <= 2e-20)   NT = 8: B = 0.3 (z^8/18! <= 1e-20)
 // The term count is chosen per extrapolation level (wave-uniform, see logl_kernel), and lanes
 // with |z| > B(NT) redo the evaluation with stumpff_full, so a walker's result depends only on
 // its own (z, level), never on the other lanes of the wave.
 template <int NT>
 __device__ __forceinline__ constexpr double stumpff_bound() {
-    return NT >= 8 ? 0.3 : 0.04;
+    return NT >= 8 ? 0.3 : (NT == 7 ? 0.12 : 0.04);
 }
 
 template <int NT>
@@ -293,9 +298,10 @@ __device__ __forceinline__ bool halley_done(double q, double z, double x3) {
 }
 
 // Kepler drift of the own Jacobi coordinate by dt in universal variables (Danby): solve
-// r0 G1 + eta0 G2 + GM G3 = dt for X by Halley steps from the third-order Taylor guess
-//   X = u (1 - u s/2 + u^2 (s^2/2 + (beta - v0^2)/12)),   u = dt/r0, s = eta0/r0
-// (= dt/r0 - eta0 dt^2/(2 r0^3) + dt^3 (3 eta0^2/r0^5 - v0^2/r0^3 + GM/r0^4)/6), accepted by
+// r0 G1 + eta0 G2 + GM G3 = dt for X by Halley steps from the fourth-order Taylor guess
+//   X = u (1 - u s/2 + u^2 T3 + u^3 T4),   u = dt/r0, s = eta0/r0, g = GM/r0,
+//   T3 = s^2/2 + (beta - g)/6,  T4 = s (5g/12 - 3 beta/8 - 5 s^2/8)
+// (series inversion of dt = r0 X + eta0 X^2/2 + zeta X^3/6 - beta eta0 X^4/24 + ...), accepted by
 // halley_done.  Lanes that need a second step take it with the same short series; lanes still
 // unconverged after that (pericentre passages of very eccentric orbits) iterate in a per-lane
 // loop, and steps spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) take the bracketed
@@ -310,29 +316,33 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
     const double eta = fma(s.rx, s.vx, s.ry * s.vy);
     const double beta = fma(s.GM2, ir0, -v2);
     const double zeta = fma(-beta, r0, GM);
-    const double u = dt * ir0, sg = eta * ir0;
+    const double u = dt * ir0, sg = eta * ir0, g = GM * ir0;
     const double hs = 0.5 * sg;
-    const double t6 = fma(hs, sg, (beta - v2) * (1.0 / 12.0));
-    const double x = u * fma(u, fma(u, t6, -hs), 1.0);
+    const double T3 = fma(hs, sg, (beta - g) * (1.0 / 6.0));
+    const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
+    const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
     double G0, G1, G2, G3, fp, fpp, Q, z, x3;
     halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3);
     double X = x - Q;
-    bool zok = fabs(z) <= stumpff_bound<NT>();
-    bool done = zok && halley_done(Q, z, x3);
     const bool hard = fabs(beta) * (u * u) > 0.5;
-    if constexpr (NT >= 8) {  // coarse levels: a second Halley step is the common case
-        if (__any(!done)) {
-            if (!done && zok) {
+    constexpr double B = stumpff_bound<NT>();
+    // wave votes straight from the compare masks (SALU only on the common path)
+    uint64_t bad = ballot(!(fabs(z) <= B)) | ballot(!halley_done(Q, z, x3));
+    {  // a second Halley step (coarse levels, pericentre passages) with the same short series
+        if (bad != 0) {
+            if (fabs(z) <= B && !halley_done(Q, z, x3)) {
                 double q2;
                 halley<NT>(X, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, q2, z, x3);
                 Q = q2;
                 X = X - q2;
-                zok = fabs(z) <= stumpff_bound<NT>();
-                done = zok && halley_done(q2, z, x3);
             }
+            bad = ballot(!(fabs(z) <= B)) | ballot(!halley_done(Q, z, x3));
         }
     }
-    if (__builtin_expect(__any(!done || hard), 0)) {
+    bad |= ballot(hard);
+    if (__builtin_expect(bad != 0, 0)) {
+        const bool zok = fabs(z) <= B;
+        bool done = zok && halley_done(Q, z, x3);
         // general solver for this lane: Halley with the full Stumpff evaluation (any z), then the
         // bracketed solve for large steps or no convergence
         if (!hard && !done) {

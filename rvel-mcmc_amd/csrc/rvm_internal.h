@@ -20,7 +20,8 @@ struct DirSched {
 struct DevPlan {
     int32_t n_planets;
     int32_t n_levels;
-    int32_t mult[RVM_MAX_LEVELS];  // level step multipliers (1, 2, 3, ...)
+    int32_t mult[RVM_MAX_LEVELS];  // level step multipliers (steps per base step)
+    int32_t nt[RVM_MAX_LEVELS];    // Stumpff series terms per level (6, 7 or 8)
     double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
     double npoints;
     int32_t n_obs;

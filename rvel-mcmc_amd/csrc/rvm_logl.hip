@@ -6,7 +6,7 @@
 //
 // Work decomposition:
 //   workgroup = 64/L walkers x one direction (blockIdx.y: 0 = epochs t >= 0, 1 = t < 0)
-//               x n_levels waves; wave L integrates the same 64 walkers with (L+1)x the steps
+//               x n_levels waves; wave L integrates the same walkers with mult[L]x the base steps
 //               (Wisdom-Holman DKD, epoch-aligned segments).  At every epoch each wave drops its
 //               64 model RVs into LDS, one barrier, and wave 0 forms the Richardson-extrapolated
 //               RV (sum_L w_L rv_L, the h^2 -> 0 limit) and accumulates chi2 in registers.
@@ -23,12 +23,20 @@
 
 namespace rvm {
 
-// One epoch-to-epoch segment of ns Wisdom-Holman DKD steps of size h.
+// One epoch-to-epoch segment of ns Wisdom-Holman DKD steps of size h (ns is wave-uniform; the
+// step loop is unrolled by hand because the compiler will not unroll a runtime trip count around
+// the convergent DPP / ballot operations).
 template <int NT, int NP, int L>
 __device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
     drift<NT>(s, 0.5 * h);
-#pragma unroll 2
-    for (int j = 0; j < ns - 1; j++) {
+    int j = 0;
+    for (; j + 2 <= ns - 1; j += 2) {
+        kick<NP, L>(s, h);
+        drift<NT>(s, h);
+        kick<NP, L>(s, h);
+        drift<NT>(s, h);
+    }
+    if (j < ns - 1) {
         kick<NP, L>(s, h);
         drift<NT>(s, h);
     }
@@ -61,9 +69,10 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     extern __shared__ double s_sched[];  // [E] seg_len | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
 
     const DirSched S = d ? P.bwd : P.fwd;
-    // wave-uniform copies (SGPRs): the level picks the Stumpff series length (rvm_device.h)
-    const int mult = P.mult[__builtin_amdgcn_readfirstlane(lvl)];
-    const bool fine = mult >= 3;
+    // wave-uniform copies (SGPRs): the level's step divisor and Stumpff series length (rvm_device.h)
+    const int lvl_u = __builtin_amdgcn_readfirstlane(lvl);
+    const int mult = P.mult[lvl_u];
+    const int nt = P.nt[lvl_u];
     const int E = S.n_epochs;
     double* l_len = s_sched;
     double* l_rv = s_sched + E;
@@ -181,8 +190,10 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         const int ns = n1 * mult;
         if (ns > 0) {
             const double h = len / (double)ns;
-            if (fine)
+            if (nt <= 6)
                 segment<6, NP, L>(s, h, ns);
+            else if (nt == 7)
+                segment<7, NP, L>(s, h, ns);
             else
                 segment<8, NP, L>(s, h, ns);
         }

@@ -17,6 +17,7 @@ RVM_STATUS_ENCOUNTER = 2
 RVM_STATUS_NONFINITE = 3
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
+ABI_VERSION = 2  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):
@@ -25,6 +26,8 @@ class RvmConfig(C.Structure):
         ("dt", C.c_double),
         ("n_levels", C.c_int32),
         ("npoints_norm", C.c_double),
+        ("level_mult", C.c_int32 * RVM_MAX_LEVELS),
+        ("period_hint", C.c_double),
     ]
 
 
@@ -74,7 +77,7 @@ def load():
         fn = getattr(lib, name)  # AttributeError here means the .so lacks an ABI symbol
         fn.restype = res
         fn.argtypes = args
-    if lib.rvm_abi_version() != 1:
+    if lib.rvm_abi_version() != ABI_VERSION:
         raise RvmError("librvmcmc.so ABI version mismatch")
     _lib = lib
     return lib

@@ -20,25 +20,53 @@ KERNEL_KEYS = ("m", "a", "h", "k", "l")
 SUPPORTED_KEYS = set(KERNEL_KEYS) | {"ix", "iy"}
 
 
+def level_multipliers(levels) -> tuple:
+    """int n -> the harmonic sequence (1, ..., n); a sequence -> its distinct positive ints."""
+    if isinstance(levels, (int, np.integer)):
+        mult = tuple(range(1, int(levels) + 1))
+    else:
+        mult = tuple(int(m) for m in levels)
+    if not 1 <= len(mult) <= _lib.RVM_MAX_LEVELS:
+        raise ValueError(f"1..{_lib.RVM_MAX_LEVELS} Richardson levels supported, got {len(mult)}")
+    if len(set(mult)) != len(mult) or min(mult) < 1 or max(mult) > 64:
+        raise ValueError("level multipliers must be distinct integers in 1..64")
+    return mult
+
+
 @dataclass(frozen=True)
 class IntegratorConfig:
     """Wisdom-Holman + Richardson settings.
 
-    steps_per_orbit: level-1 steps per shortest orbital period of the reference state
+    steps_per_orbit: base steps per shortest orbital period of the reference state
                      (dt = P_min / steps_per_orbit) unless `dt` is given explicitly.
-    n_levels:        Richardson levels; level L integrates with dt/(L+1).  n_levels=4 at
-                     steps_per_orbit=24 keeps |logL - logL_IAS15| <= ~1e-9 on the benchmark
-                     configs (T2 tier; tests/test_gpu_logl.py enforces 5e-9).
+    levels:          Richardson level multipliers: level k integrates every epoch-to-epoch
+                     segment with mult[k] x its base steps (step dt/mult[k]); an int n means the
+                     harmonic sequence 1..n.  The default (4, 5, 6, 7) at steps_per_orbit = 8
+                     (steps P/32 .. P/56) keeps |logL - logL_IAS15| <= ~2e-9 on the benchmark
+                     configs (T2 tier; the tests enforce 5e-9) with the shortest longest-level
+                     integration of the sequences we measured.
     """
 
-    steps_per_orbit: float = 24.0
-    n_levels: int = 4
+    steps_per_orbit: float = 8.0
+    levels: tuple = (4, 5, 6, 7)
     dt: Optional[float] = None
+
+    @property
+    def mult(self) -> tuple:
+        return level_multipliers(self.levels)
+
+    @property
+    def n_levels(self) -> int:
+        return len(self.mult)
 
     def step_for(self, planets) -> float:
         if self.dt is not None:
             return float(self.dt)
         return min_period(planets) / float(self.steps_per_orbit)
+
+    def plan_args(self, planets):
+        """(dt, level multipliers, period hint) for plan_for / LoglPlan."""
+        return self.step_for(planets), self.mult, min_period(planets)
 
 
 DEFAULT_CONFIG = IntegratorConfig()
@@ -73,7 +101,8 @@ def default_device():
 class LoglPlan:
     """rvm_plan for one observation set on one device."""
 
-    def __init__(self, t, rv, sigma, npoints, n_planets, dt, n_levels=4, max_walkers=4096, device=None):
+    def __init__(self, t, rv, sigma, npoints, n_planets, dt, levels=4, max_walkers=4096, device=None,
+                 period_hint=0.0):
         torch = _torch()
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else default_device()
@@ -85,10 +114,13 @@ class LoglPlan:
         self.n_obs = len(t)
         self.n_planets = int(n_planets)
         self.dt = float(dt)
-        self.n_levels = int(n_levels)
+        self.mult = level_multipliers(levels)
+        self.n_levels = len(self.mult)
+        self.period_hint = float(period_hint)
         self.npoints = float(npoints)
         self.max_walkers = int(max_walkers)
-        cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints)
+        lm = (C.c_int32 * _lib.RVM_MAX_LEVELS)(*self.mult)
+        cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints, lm, self.period_hint)
         handle = C.c_void_p()
         dp = C.POINTER(C.c_double)
         with torch.cuda.device(self.device):
@@ -151,16 +183,17 @@ def obs_arrays(obs):
     return t, rv, er
 
 
-def plan_for(obs, n_planets, dt, n_levels, max_walkers, device=None) -> LoglPlan:
+def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0.0) -> LoglPlan:
     """Cached LoglPlan on an Observation object (keyed by device and integrator settings)."""
     dev = _torch().device(device) if device is not None else default_device()
     cache = obs.__dict__.setdefault("_rvm_plans", {})
-    key = (str(dev), int(n_planets), float(dt), int(n_levels))
+    mult = level_multipliers(levels)
+    key = (str(dev), int(n_planets), float(dt), mult, float(period_hint))
     plan = cache.get(key)
     if plan is None or plan.max_walkers < max_walkers:
         t, rv, er = obs_arrays(obs)
         cap = max(int(max_walkers), plan.max_walkers * 2 if plan else 0, 64)
-        plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, n_levels, cap, dev)
+        plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, mult, cap, dev, period_hint)
         cache[key] = plan
     return plan
 

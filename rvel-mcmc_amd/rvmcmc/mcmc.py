@@ -143,8 +143,8 @@ class MhChains:
         self.device = torch.device(device) if device is not None else engine.default_device()
         self.lib = _lib.load()
         self.pmap = self.state.param_map()
-        dt = self.state.integrator.step_for(self.state.planets)
-        self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, self.state.integrator.n_levels, self.n, self.device)
+        dt, mult, hint = self.state.integrator.plan_args(self.state.planets)
+        self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, mult, self.n, self.device, hint)
         self.scales = torch.as_tensor(_scales_vector(self.state, scales), device=self.device)
         if X0 is None:
             X0 = np.tile(self.state.get_params()[:, None], (1, self.n))

@@ -149,8 +149,8 @@ class State(object):
         return r
 
     def _plan(self, obs, max_walkers=1, device=None):
-        dt = self.integrator.step_for(self.planets)
-        return engine.plan_for(obs, len(self.planets), dt, self.integrator.n_levels, max_walkers, device)
+        dt, mult, hint = self.integrator.plan_args(self.planets)
+        return engine.plan_for(obs, len(self.planets), dt, mult, max_walkers, device, hint)
 
     def get_rv(self, times):
         """state.py:61-73: model RV (star barycentric vx) at `times`; raises Encounter."""

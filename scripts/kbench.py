@@ -17,12 +17,15 @@ from rvmcmc import engine  # noqa: E402
 
 def main():
     Ws = [int(a) for a in sys.argv[1:]] or [2048, 4096]
-    nl = int(os.environ.get("NL", "4"))
-    spo = float(os.environ.get("SPO", "24"))
+    # LEVELS: "4" (harmonic 1..4) or "4,5,6,7" (multipliers); SPO: base steps per shortest orbit
+    lv = os.environ.get("LEVELS", "4,5,6,7")
+    nl = tuple(int(v) for v in lv.split(",")) if "," in lv else int(lv)
+    spo = float(os.environ.get("SPO", "8"))
     obs = s2_obs_oracle()
-    dt = engine.min_period(S2_PLANETS) / spo
+    pmin = engine.min_period(S2_PLANETS)
+    dt = pmin / spo
     t, rv, er = engine.obs_arrays(obs)
-    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, nl, max(Ws))
+    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, nl, max(Ws), period_hint=pmin)
     rng = np.random.default_rng(0)
     for W in Ws:
         P = np.repeat(O.pal_params(S2_PLANETS)[None], W, 0)

@@ -3,7 +3,7 @@
 Tiers:
   T1  kernel vs oracle/rvoracle.c's restatement of the SAME algorithm (Richardson-extrapolated
       Wisdom-Holman, identical schedule):  |dlogL| <= 1e-11 sum|w| max(1, |logL|), model RV within
-      5e-14 absolute, identical status codes.  Chaotic walkers (wide ball) are compared within
+      1e-14 sum|w| absolute, identical status codes.  Chaotic walkers (wide ball) are compared within
       their own roundoff sensitivity, measured on the oracle.
   T2  kernel vs the IAS15 restatement of the reference (reference-equivalent physics):
       |dlogL| <= 5e-9 absolute at the default integrator settings; golden G2/G3 reproduced.
@@ -23,15 +23,20 @@ pytestmark = pytest.mark.gpu
 # 6.2 at 4 levels, 26 at 6) and by the likelihood's conditioning (dlogL/drv ~ 2 sum|r|/(N sigma^2)
 # ~ 1e4).  Tolerance: 1e-11 * sum|w| * max(1, |logL|)  (measured max 4e-11 at 4 levels).
 T1_REL_PER_W = 1e-11
-T1_RV_ABS = 5e-14
 T2_ABS = 5e-9
+# default integrator (rvmcmc.engine.IntegratorConfig): level multipliers and base steps per orbit
+LEVELS = (4, 5, 6, 7)
+SPO = 8.0
+# model RV: per-level differences of ~1e-14 absolute (roundoff accumulated over thousands of
+# steps) times the weights' sum|w| (6.2 harmonic 4 levels, 35 for 4..7)
+T1_RV_ABS = 1e-14 * float(np.abs(O.richardson_weights(LEVELS)).sum())
 
 
-def t1_tol(nl=4):
+def t1_tol(nl=LEVELS):
     return T1_REL_PER_W * float(np.abs(O.richardson_weights(nl)).sum())
 
 
-T1_REL = t1_tol(4)
+T1_REL = t1_tol(LEVELS)
 
 
 def _torch():
@@ -41,12 +46,14 @@ def _torch():
     return torch
 
 
-def _plan(obs, planets, n_levels=4, steps=24.0, max_walkers=4096):
+def _plan(obs, planets, n_levels=LEVELS, steps=SPO, max_walkers=4096):
     from rvmcmc import engine
 
-    dt = engine.min_period(planets) / steps
+    pmin = engine.min_period(planets)
+    dt = pmin / steps
     t, rv, er = engine.obs_arrays(obs)
-    return engine.LoglPlan(t, rv, er, obs.Npoints, len(planets), dt, n_levels, max_walkers), dt
+    return engine.LoglPlan(t, rv, er, obs.Npoints, len(planets), dt, n_levels, max_walkers,
+                           period_hint=pmin), dt
 
 
 def _ball(planets, W, rel=1e-3, seed=0):
@@ -70,7 +77,7 @@ def _run(plan, P, hill=1.0, want_rv=False):
     return lp.cpu().numpy(), st.cpu().numpy(), (rv.cpu().numpy() if rv is not None else None)
 
 
-def _assert_t1(got, st, ref, st_ref, nl=4):
+def _assert_t1(got, st, ref, st_ref, nl=LEVELS):
     np.testing.assert_array_equal(st, st_ref)
     ok = st == 0
     err = np.abs(got[ok] - ref[ok]) / np.maximum(1.0, np.abs(ref[ok]))
@@ -84,7 +91,7 @@ def test_t1_s2_tight_ball(W):
     plan, dt = _plan(obs, S2_PLANETS)
     P = _ball(S2_PLANETS, W, seed=W)
     got, st, _ = _run(plan, P)
-    ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, 4)
+    ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, LEVELS)
     _assert_t1(got, st, ref, st_ref)
 
 
@@ -98,7 +105,7 @@ def test_t1_wide_ball_statuses():
     P[2, 0, 2], P[2, 0, 3] = 0.8, 0.6   # h^2 + k^2 = 1
     P[3, 1, 1] = P[3, 0, 1] * 1.01      # near-coorbital -> encounter
     got, st, _ = _run(plan, P)
-    ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, 4)
+    ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, LEVELS)
     assert (st == 1).sum() >= 3 and (st == 2).sum() >= 1
     # roundoff sensitivity of each walker: the oracle's own response to a 1e-15 relative nudge.
     # Chaotic walkers (close approaches) may flip a borderline encounter or move logL far beyond
@@ -108,12 +115,12 @@ def test_t1_wide_ball_statuses():
     for k, (pl, par, sgn) in enumerate([(0, 4, 1), (1, 4, -1), (0, 1, 1), (1, 1, -1), (0, 2, 1)]):
         P2 = P.copy()
         P2[:, pl, par] *= 1 + sgn * 1e-15
-        ref2, st2 = O.logl_whx_batch(P2, 2, obs, dt, 4)
+        ref2, st2 = O.logl_whx_batch(P2, 2, obs, dt, LEVELS)
         flips |= st2 != st_ref
         both = (st_ref == 0) & (st2 == 0)
         sens[both] = np.maximum(sens[both], np.abs(ref2[both] - ref[both]) / np.maximum(1.0, np.abs(ref[both])))
     # borderline encounters: the oracle's closest approach within 1e-6 of the exit distance
-    ratio = np.array([O.min_distance_ratio(P[i:i + 1], 2, obs, dt, 4) for i in range(len(P))])
+    ratio = np.array([O.min_distance_ratio(P[i:i + 1], 2, obs, dt, LEVELS) for i in range(len(P))])
     sensitive = flips | (sens > 1e-9) | (np.abs(ratio - 1.0) < 1e-6)
     mism = st != st_ref
     assert np.all(~mism | sensitive), np.nonzero(mism & ~sensitive)
@@ -127,11 +134,14 @@ def test_t1_wide_ball_statuses():
     assert np.all(np.isneginf(got[st != 0]))
 
 
-@pytest.mark.parametrize("nl", [1, 2, 3, 4, 5, 6])
-def test_t1_levels(nl):
+@pytest.mark.parametrize("nl,spo", [(1, 24.0), (2, 24.0), (3, 24.0), (4, 24.0), (5, 24.0), (6, 24.0),
+                                    ((2, 3, 4, 5), 16.0), ((3, 4, 5, 6), 12.0), ((4, 5, 6, 7), 8.0),
+                                    ((4, 5, 6, 7, 8, 9), 6.0), ((1, 3, 5), 12.0)])
+def test_t1_levels(nl, spo):
+    """Harmonic levels 1..6 and general multiplier sequences, each against the oracle."""
     obs = s2_obs_oracle()
-    plan, dt = _plan(obs, S2_PLANETS, n_levels=nl)
-    P = _ball(S2_PLANETS, 96, seed=nl)
+    plan, dt = _plan(obs, S2_PLANETS, n_levels=nl, steps=spo)
+    P = _ball(S2_PLANETS, 96, seed=int(np.sum(nl)))
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, nl)
     _assert_t1(got, st, ref, st_ref, nl)
@@ -147,7 +157,7 @@ def test_t1_planet_counts(n_planets):
     plan, dt = _plan(obs, planets)
     P = _ball(planets, 70, seed=n_planets)
     got, st, _ = _run(plan, P)
-    ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, 4)
+    ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS)
     _assert_t1(got, st, ref, st_ref)
 
 
@@ -184,7 +194,7 @@ def test_g3_rv_out(golden):
     plan, dt = _plan(o, g["planets"])
     _, st, rv = _run(plan, O.pal_params(g["planets"])[None], hill=0.0, want_rv=True)
     assert st[0] == 0
-    rv_whx, _ = O.whx_rv(g["planets"], times, dt, 4)
+    rv_whx, _ = O.whx_rv(g["planets"], times, dt, LEVELS)
     np.testing.assert_allclose(rv[:, 0], rv_whx, rtol=0, atol=T1_RV_ABS)   # T1
     np.testing.assert_allclose(rv[:, 0], d["rv"], rtol=0, atol=1e-12)      # T2 vs the stored curve
 
@@ -200,7 +210,7 @@ def test_epoch_edge_cases():
     assert info["epochs_fwd"] == 7 and info["epochs_bwd"] == 0
     P = _ball(planets, 5, seed=9)
     got, st, rv = _run(plan, P, want_rv=True)
-    ref, st_ref = O.logl_whx_batch(P, 2, o, dt, 4)
+    ref, st_ref = O.logl_whx_batch(P, 2, o, dt, LEVELS)
     _assert_t1(got, st, ref, st_ref)
     assert np.all(rv[1] == rv[2]) and np.all(rv[0] == rv[4])
 
@@ -229,10 +239,10 @@ def test_fake_observation_matches_oracle():
     o = observations.FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
     from rvmcmc import engine
 
-    dt = engine.min_period(S2_PLANETS) / 24.0
+    dt = engine.min_period(S2_PLANETS) / SPO
     np.random.seed(2017)
     r = O.fake_obs(S2_PLANETS, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.,
-                   rv_fn=lambda pl, t: O.whx_rv(pl, t, dt, 4)[0])
+                   rv_fn=lambda pl, t: O.whx_rv(pl, t, dt, LEVELS)[0])
     np.testing.assert_array_equal(o.tf, r.tf)
     np.testing.assert_array_equal(o.tb, r.tb)
     np.testing.assert_array_equal(o.errorf, r.errorf)

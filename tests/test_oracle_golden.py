@@ -106,9 +106,11 @@ def test_ias15_encounter_status():
     assert st == O.ORACLE_ENCOUNTER
 
 
+@pytest.mark.parametrize("levels,spo", [((4, 5, 6, 7), 8.0), (4, 24.0)])
 @pytest.mark.parametrize("which", ["HD", "S2"])
-def test_t2_kernel_algorithm_vs_ias15(which, hd_obs_oracle, golden):
-    """T2: Richardson-extrapolated WH (n_levels=4, dt = P_min/24) vs the IAS15 restatement."""
+def test_t2_kernel_algorithm_vs_ias15(which, levels, spo, hd_obs_oracle, golden):
+    """T2: Richardson-extrapolated WH vs the IAS15 restatement, at the default level sequence
+    (multipliers 4..7 on dt = P_min/8) and at the harmonic 4 levels on dt = P_min/24."""
     if which == "HD":
         planets, obs = _sol_planets(golden["G2"]["sol"]), hd_obs_oracle
     else:
@@ -120,7 +122,7 @@ def test_t2_kernel_algorithm_vs_ias15(which, hd_obs_oracle, golden):
     params = np.repeat(base[None], W, 0)
     params[:, :, :5] *= 1 + 1e-3 * rng.standard_normal((W, len(planets), 5))
     ref, st_ref = O.logl_ias15_batch(params, len(planets), obs, hill_factor=1.0)
-    got, st = O.logl_whx_batch(params, len(planets), obs, pmin / 24.0, 4, hill_factor=1.0)
+    got, st = O.logl_whx_batch(params, len(planets), obs, pmin / spo, levels, hill_factor=1.0)
     assert (st == st_ref).all()
     ok = st == 0
     assert ok.sum() >= W - 1
