@@ -182,11 +182,12 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         }
         P.lw[k] = wk;
         // Stumpff series length (rvm_device.h stumpff_bound): nominal z = (2 pi h / P)^2 on a
-        // circular orbit, x3 for the pericentre of e ~ 0.3 orbits; lanes beyond the bound take the
-        // general evaluation, so this choice only affects speed
+        // circular orbit, x2 for the pericentre of e ~ 0.25 orbits; lanes beyond the bound take
+        // the general evaluation, so this choice only affects speed.  NT = 6 levels also run
+        // their segments speculatively (rvm_logl.hip segment<>)
         if (cfg->period_hint > 0.0) {
             const double nh = 2.0 * M_PI * cfg->dt / (mult[k] * cfg->period_hint);
-            const double zn = 3.0 * nh * nh;
+            const double zn = 2.0 * nh * nh;
             P.nt[k] = zn <= 0.04 ? 6 : (zn <= 0.12 ? 7 : 8);
         }
     }

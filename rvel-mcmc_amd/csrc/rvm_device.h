@@ -290,92 +290,74 @@ __device__ __forceinline__ void halley(double x, double beta, double r0, double 
 
 // Acceptance of a Halley step with relative correction qt = q/x: the error left in X is
 // ~ c z qt^3 (c << 1; Halley is cubic and its constant scales with z = beta x^2), and the Taylor
-// update of the G-functions over the correction (below) truncates at ~ z qt^3 / 3 relative.  Both
-// stay below ~1e-17 when |q^3 z| <= 3e-17 |x^3|.  At the default step (P/24 .. P/96) and
-// e <~ 0.3 the finest level passes after one step; the coarse levels take a second one.
+// update of the G-functions over the correction (drift_apply) truncates at ~ z qt^3 / 3 relative.
+// Both stay below ~1e-17 when |q^3 z| <= 3e-17 |x^3|.  With |z| <= B(NT) (checked separately)
+// this holds whenever |q| <= (3e-17 / B)^(1/3) |x|, the cheap form used on the hot path:
+//   NT = 6: 9.0e-6   NT = 7: 6.2e-6   NT = 8: 4.6e-6
+// At the default steps (P/32 .. P/56) and e <~ 0.25 the finest levels pass after one step.
+template <int NT>
+__device__ __forceinline__ constexpr double halley_tol() {
+    return NT >= 8 ? 4.6e-6 : (NT == 7 ? 6.2e-6 : 9.0e-6);
+}
+
+template <int NT>
+__device__ __forceinline__ bool halley_ok(double q, double x) {
+    return !(fabs(q) > halley_tol<NT>() * fabs(x));
+}
+
+// general form (any z) for the rare solver
 __device__ __forceinline__ bool halley_done(double q, double z, double x3) {
     return !(fabs((q * q) * (q * z)) > 3e-17 * fabs(x3));
 }
 
-// Kepler drift of the own Jacobi coordinate by dt in universal variables (Danby): solve
-// r0 G1 + eta0 G2 + GM G3 = dt for X by Halley steps from the fourth-order Taylor guess
-//   X = u (1 - u s/2 + u^2 T3 + u^3 T4),   u = dt/r0, s = eta0/r0, g = GM/r0,
-//   T3 = s^2/2 + (beta - g)/6,  T4 = s (5g/12 - 3 beta/8 - 5 s^2/8)
-// (series inversion of dt = r0 X + eta0 X^2/2 + zeta X^3/6 - beta eta0 X^4/24 + ...), accepted by
-// halley_done.  Lanes that need a second step take it with the same short series; lanes still
-// unconverged after that (pericentre passages of very eccentric orbits) iterate in a per-lane
-// loop, and steps spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) take the bracketed
-// solver -- each lane at its own convergence, so results never depend on the other lanes of the
-// wave.  The G-functions at the final X = x - q are Taylor-updated from the evaluation at x
-// (dG0/dX = -beta G1, dG_k/dX = G_{k-1}), and |r| after the drift comes out of the solution
-// (r = r0 G0 + eta0 G1 + GM G2): no square root anywhere in the step.
-template <int NT, int NP>
-__device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
-    const double GM = s.GM, r0 = s.r, ir0 = s.ir;
-    const double v2 = fma(s.vx, s.vx, s.vy * s.vy);
-    const double eta = fma(s.rx, s.vx, s.ry * s.vy);
-    const double beta = fma(s.GM2, ir0, -v2);
-    const double zeta = fma(-beta, r0, GM);
-    const double u = dt * ir0, sg = eta * ir0, g = GM * ir0;
-    const double hs = 0.5 * sg;
-    const double T3 = fma(hs, sg, (beta - g) * (1.0 / 6.0));
-    const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
-    const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
-    double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3);
-    double X = x - Q;
-    const bool hard = fabs(beta) * (u * u) > 0.5;
-    constexpr double B = stumpff_bound<NT>();
-    // wave votes straight from the compare masks (SALU only on the common path)
-    uint64_t bad = ballot(!(fabs(z) <= B)) | ballot(!halley_done(Q, z, x3));
-    {  // a second Halley step (coarse levels, pericentre passages) with the same short series
-        if (bad != 0) {
-            if (fabs(z) <= B && !halley_done(Q, z, x3)) {
-                double q2;
-                halley<NT>(X, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, q2, z, x3);
-                Q = q2;
-                X = X - q2;
-            }
-            bad = ballot(!(fabs(z) <= B)) | ballot(!halley_done(Q, z, x3));
+// Universal-Kepler solve for the rare lanes: Halley with the full Stumpff evaluation (any z)
+// from the best estimate, then the bracketed solve for large steps or no convergence.  Returns
+// the G-functions, f', f'' at the last evaluation point and the final correction Q (X = x - Q).
+__device__ __forceinline__ void kepler_rare(double r0, double eta, double zeta, double beta, double GM, double dt,
+                                         double xi, bool hard, double& G0, double& G1, double& G2, double& G3,
+                                         double& fp, double& fpp, double& Q) {
+    bool done = false;
+    double X = xi;
+    if (!hard) {
+        for (int it = 0; it < 8 && !done; it++) {
+            double c0, c1, cc2, cc3;
+            const double zi = beta * X * X;
+            stumpff_full(zi, c0, c1, cc2, cc3);
+            const double g1 = X * c1, g2 = X * X * cc2, g3 = X * X * X * cc3;
+            const double ff = r0 * g1 + eta * g2 + GM * g3 - dt;
+            const double ffp = r0 * c0 + eta * g1 + GM * g2;
+            const double ffpp = eta * c0 + zeta * g1;
+            const double dX = ff * ffp / (ffp * ffp - 0.5 * ff * ffpp);
+            G0 = c0;
+            G1 = g1;
+            G2 = g2;
+            G3 = g3;
+            fp = ffp;
+            fpp = ffpp;
+            Q = dX;
+            done = halley_done(dX, zi, X * X * X);
+            X = X - dX;
         }
     }
-    bad |= ballot(hard);
-    if (__builtin_expect(bad != 0, 0)) {
-        const bool zok = fabs(z) <= B;
-        bool done = zok && halley_done(Q, z, x3);
-        // general solver for this lane: Halley with the full Stumpff evaluation (any z), then the
-        // bracketed solve for large steps or no convergence
-        if (!hard && !done) {
-            double xi = zok ? X : x;
-            for (int it = 0; it < 8 && !done; it++) {
-                double c0, c1, cc2, cc3;
-                const double zi = beta * xi * xi;
-                stumpff_full(zi, c0, c1, cc2, cc3);
-                const double g1 = xi * c1, g2 = xi * xi * cc2, g3 = xi * xi * xi * cc3;
-                const double ff = r0 * g1 + eta * g2 + GM * g3 - dt;
-                const double ffp = r0 * c0 + eta * g1 + GM * g2;
-                const double ffpp = eta * c0 + zeta * g1;
-                const double dX = ff * ffp / (ffp * ffp - 0.5 * ff * ffpp);
-                G0 = c0;
-                G1 = g1;
-                G2 = g2;
-                G3 = g3;
-                fp = ffp;
-                fpp = ffpp;
-                Q = dX;
-                done = halley_done(dX, zi, xi * xi * xi);
-                xi = xi - dX;
-            }
-            X = xi;
-        }
-        if (hard || !done) {
-            kepler_safe(r0, eta, zeta, beta, GM, dt, X, G0, G1, G2, G3);
-            fp = r0 * G0 + eta * G1 + GM * G2;
-            fpp = eta * G0 + zeta * G1;
-            Q = 0.0;
-        }
+    if (hard || !done) {
+        kepler_safe(r0, eta, zeta, beta, GM, dt, X, G0, G1, G2, G3);
+        fp = r0 * G0 + eta * G1 + GM * G2;
+        fpp = eta * G0 + zeta * G1;
+        Q = 0.0;
     }
-    // Taylor update of the G-functions (and of r = f') from the last evaluation point to X
+}
+
+// New position/velocity from the G-functions at the last evaluation point and the final Halley
+// correction Q (Taylor update of G1..G3 and of r = f' from there to X = x - Q), Gauss f and g.
+struct DriftOut {
+    double rx, ry, vx, vy, r, ir;
+};
+
+template <int NP>
+__device__ __forceinline__ DriftOut drift_apply(const Lane<NP>& s, double dt, double beta, double eta, double zeta,
+                                                double G0, double G1, double G2, double G3, double fp, double fpp,
+                                                double Q) {
+    const double GM = s.GM, ir0 = s.ir;
     const double d = -Q, d2 = (0.5 * Q) * Q;
     const double H1 = fma(d, G0, fma(-d2 * beta, G1, G1));
     const double H2 = fma(d2, G0, fma(d, G1, G2));
@@ -388,16 +370,84 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
     const double g_ = fma(-GM, H3, dt);
     const double fd = -(GM * H1) * (irr * ir0);
     const double gd = fma(-gG2, irr, 1.0);
-    const double nrx = fma(f_, s.rx, g_ * s.vx);
-    const double nry = fma(f_, s.ry, g_ * s.vy);
-    const double nvx = fma(fd, s.rx, gd * s.vx);
-    const double nvy = fma(fd, s.ry, gd * s.vy);
-    s.rx = nrx;
-    s.ry = nry;
-    s.vx = nvx;
-    s.vy = nvy;
-    s.r = rr;
-    s.ir = irr;
+    DriftOut o;
+    o.rx = fma(f_, s.rx, g_ * s.vx);
+    o.ry = fma(f_, s.ry, g_ * s.vy);
+    o.vx = fma(fd, s.rx, gd * s.vx);
+    o.vy = fma(fd, s.ry, gd * s.vy);
+    o.r = rr;
+    o.ir = irr;
+    return o;
+}
+
+// Kepler drift of the own Jacobi coordinate by dt in universal variables (Danby): solve
+// r0 G1 + eta0 G2 + GM G3 = dt for X by Halley steps from the fourth-order Taylor guess
+//   X = u (1 - u s/2 + u^2 T3 + u^3 T4),   u = dt/r0, s = eta0/r0, g = GM/r0,
+//   T3 = s^2/2 + (beta - g)/6,  T4 = s (5g/12 - 3 beta/8 - 5 s^2/8)
+// (series inversion of dt = r0 X + eta0 X^2/2 + zeta X^3/6 - beta eta0 X^4/24 + ...), accepted by
+// halley_ok.  A lane's step is "good" when one Halley step with the NT-term series is accepted.
+//
+// GATED = true: the wave votes on the good flags and lanes that are not good redo the solve with
+//   kepler_rare (a second short-series Halley step first on the coarse levels, NT >= 7).  Each
+//   lane at its own convergence, so results never depend on the other lanes of the wave.
+// GATED = false: no vote -- the vote is a VALU->SALU->branch round trip that costs ~100 cycles of
+//   a ~660-cycle step on one wave -- the result is only valid for good lanes and `bad` collects
+//   the others; the caller (segment<> in rvm_logl.hip) re-runs the whole segment gated when any
+//   lane was not good.  Good lanes compute bit-identical states either way.
+// No square root anywhere in the step.
+template <int NT, bool GATED, int NP>
+__device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad) {
+    const double GM = s.GM, r0 = s.r, ir0 = s.ir;
+    const double v2 = fma(s.vx, s.vx, s.vy * s.vy);
+    const double eta = fma(s.rx, s.vx, s.ry * s.vy);
+    const double beta = fma(s.GM2, ir0, -v2);
+    const double zeta = fma(-beta, r0, GM);
+    const double u = dt * ir0, sg = eta * ir0, g = GM * ir0;
+    const double hs = 0.5 * sg;
+    const double T3 = fma(hs, sg, (beta - g) * (1.0 / 6.0));
+    const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
+    const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
+    double G0, G1, G2, G3, fp, fpp, Q, z, x3;
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3);
+    constexpr double B = stumpff_bound<NT>();
+    // A step spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) that passes these tests has
+    // converged all the same; only kepler_rare treats such steps separately (bracketed solver).
+    if constexpr (GATED) {
+        double xe = x;  // point where the G-functions were evaluated (X = xe - Q)
+        uint64_t nb = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, x));
+        if constexpr (NT >= 7) {  // coarse levels: a second Halley step is common (pericentre passages)
+            if (nb != 0) {
+                if (fabs(z) <= B && !halley_ok<NT>(Q, x)) {
+                    xe = x - Q;
+                    halley<NT>(xe, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3);
+                }
+                nb = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, xe));
+            }
+        }
+        if (__builtin_expect(nb != 0, 0)) {
+            const bool zok = fabs(z) <= B;
+            if (!(zok && halley_ok<NT>(Q, xe))) {
+                const bool hard = fabs(beta) * (u * u) > 0.5;
+                kepler_rare(r0, eta, zeta, beta, GM, dt, zok ? xe - Q : x, hard, G0, G1, G2, G3, fp, fpp, Q);
+            }
+        }
+    } else {
+        bad = bad || !(fabs(z) <= B) || !halley_ok<NT>(Q, x);
+    }
+    const DriftOut o = drift_apply(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
+    s.rx = o.rx;
+    s.ry = o.ry;
+    s.vx = o.vx;
+    s.vy = o.vy;
+    s.r = o.r;
+    s.ir = o.ir;
+}
+
+// gated drift (no speculation)
+template <int NT, int NP>
+__device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
+    bool unused = false;
+    drift<NT, true>(s, dt, unused);
 }
 
 // Interaction kick of the own Jacobi velocity by dt (and the encounter test on every pair):

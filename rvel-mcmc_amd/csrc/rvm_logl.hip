@@ -23,25 +23,62 @@
 
 namespace rvm {
 
+#ifdef RVM_PROFILE
+// Timing build (make profile -> scripts/probe/librvmcmc_prof.so): per wave, s_memtime at kernel
+// start, after the prologue, accumulated inside segments, accumulated in epoch handling (incl.
+// the barrier), and at the end.  Read with rvm_prof_copy (scripts/probe/prof_kernel.py).
+#define RVM_PROF_SLOTS 8
+#define RVM_PROF_MAX_WAVES 4096
+__device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
+#define PROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#else
+#define PROF_T(v)
+#endif
+
 // One epoch-to-epoch segment of ns Wisdom-Holman DKD steps of size h (ns is wave-uniform; the
 // step loop is unrolled by hand because the compiler will not unroll a runtime trip count around
 // the convergent DPP / ballot operations).
-template <int NT, int NP, int L>
-__device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
-    drift<NT>(s, 0.5 * h);
+template <int NT, bool GATED, int NP, int L>
+__device__ __forceinline__ void segment_steps(Lane<NP>& s, double h, int ns, bool& bad) {
+    drift<NT, GATED>(s, 0.5 * h, bad);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
         kick<NP, L>(s, h);
-        drift<NT>(s, h);
+        drift<NT, GATED>(s, h, bad);
         kick<NP, L>(s, h);
-        drift<NT>(s, h);
+        drift<NT, GATED>(s, h, bad);
     }
     if (j < ns - 1) {
         kick<NP, L>(s, h);
-        drift<NT>(s, h);
+        drift<NT, GATED>(s, h, bad);
     }
     kick<NP, L>(s, h);
-    drift<NT>(s, 0.5 * h);
+    drift<NT, GATED>(s, 0.5 * h, bad);
+}
+
+// SPEC: run the segment with ungated drifts (rvm_device.h) and vote once at its end; if any lane
+// of the wave had a step that needs the general solver, restore the segment's initial state and
+// redo it gated.  Used on the fine levels, where such steps are rare.
+template <int NT, bool SPEC, int NP, int L>
+__device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
+    bool bad = false;
+    if constexpr (SPEC) {
+        const double rx = s.rx, ry = s.ry, vx = s.vx, vy = s.vy, r = s.r, ir = s.ir;
+        const bool enc = s.enc;
+        segment_steps<NT, false, NP, L>(s, h, ns, bad);
+        if (__builtin_expect(ballot(bad) != 0, 0)) {
+            s.rx = rx;
+            s.ry = ry;
+            s.vx = vx;
+            s.vy = vy;
+            s.r = r;
+            s.ir = ir;
+            s.enc = enc;
+            segment_steps<NT, true, NP, L>(s, h, ns, bad);
+        }
+    } else {
+        segment_steps<NT, true, NP, L>(s, h, ns, bad);
+    }
 }
 
 template <int NP>
@@ -53,6 +90,10 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
                                                                    double* __restrict__ rv_out) {
     constexpr int L = LanesPerWalker<NP>::value;  // lanes per walker (one per planet)
     constexpr int WPB = 64 / L;                    // walkers per block (= per wave)
+    PROF_T(t_start);
+#ifdef RVM_PROFILE
+    const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const int lvl = threadIdx.x >> 6;              // wave-uniform extrapolation level
     const int lane = threadIdx.x & 63;
     const int slot = lane / L;                     // walker slot within the block
@@ -180,6 +221,10 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
 
     // ---- integrate outward from t = 0 through this direction's epochs -------------------------
     __syncthreads();  // schedule staged
+    PROF_T(t_pro);
+#ifdef RVM_PROFILE
+    unsigned long long t_seg = 0, t_epo = 0;
+#endif
     double chi2 = 0.0;
     int n1 = E > 0 ? l_n[0] : 0;
     double len = E > 0 ? l_len[0] : 0.0;
@@ -188,15 +233,17 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         const int n1_next = e + 1 < E ? l_n[e + 1] : 0;
         const double len_next = e + 1 < E ? l_len[e + 1] : 0.0;
         const int ns = n1 * mult;
+        PROF_T(ta);
         if (ns > 0) {
             const double h = len / (double)ns;
             if (nt <= 6)
-                segment<6, NP, L>(s, h, ns);
+                segment<6, true, NP, L>(s, h, ns);
             else if (nt == 7)
-                segment<7, NP, L>(s, h, ns);
+                segment<7, false, NP, L>(s, h, ns);
             else
-                segment<8, NP, L>(s, h, ns);
+                segment<8, false, NP, L>(s, h, ns);
         }
+        PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
         if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
         __syncthreads();
@@ -210,6 +257,11 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         }
         n1 = n1_next;
         len = len_next;
+#ifdef RVM_PROFILE
+        PROF_T(tc);
+        t_seg += tb - ta;
+        t_epo += tc - tb;
+#endif
     }
     if (pl_idx == 0) s_enc[lvl][slot] = (s.enc ? 1 : 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
@@ -225,6 +277,21 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
             status_part[(size_t)d * W + wo] = st;
         }
     }
+#ifdef RVM_PROFILE
+    PROF_T(t_end);
+    const int gw = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + lvl;
+    if (lane == 0 && gw < RVM_PROF_MAX_WAVES) {
+        unsigned long long* o = rvm_prof + (size_t)gw * RVM_PROF_SLOTS;
+        o[0] = t_start;
+        o[1] = t_pro;
+        o[2] = t_seg;
+        o[3] = t_epo;
+        o[4] = t_end;
+        o[5] = rt_start;
+        o[6] = __builtin_amdgcn_s_memrealtime();
+        o[7] = (unsigned long long)lvl | ((unsigned long long)blockIdx.y << 8) | ((unsigned long long)mult << 16);
+    }
+#endif
 }
 
 __global__ void finalize_kernel(const int W, const double npoints, const double* __restrict__ chi2_part,
@@ -271,3 +338,14 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
 }
 
 }  // namespace rvm
+
+#ifdef RVM_PROFILE
+extern "C" int rvm_prof_copy(void* host, size_t bytes) {
+    const size_t n = bytes < sizeof(rvm::rvm_prof) ? bytes : sizeof(rvm::rvm_prof);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(rvm::rvm_prof), n, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int rvm_prof_clear(void) {
+    static unsigned long long zero[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(rvm::rvm_prof), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif

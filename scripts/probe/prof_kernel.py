@@ -1,0 +1,69 @@
+"""Per-wave timing breakdown of rvm::logl_kernel from the RVM_PROFILE build
+(make -C rvel-mcmc_amd profile -> scripts/probe/librvmcmc_prof.so).
+Usage: python scripts/probe/prof_kernel.py [W]   (S2 workload, default integrator)"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "rvel-mcmc_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")]
+import torch  # noqa: E402
+
+import oracle as O  # noqa: E402
+from conftest import S2_PLANETS, s2_obs_oracle  # noqa: E402
+from rvmcmc import _lib, engine  # noqa: E402
+
+SLOTS, MAXW = 8, 4096
+
+
+def main():
+    W = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+    _lib.LIB_PATH = os.path.join(ROOT, "scripts", "probe", "librvmcmc_prof.so")
+    lib = _lib.load()
+    lib.rvm_prof_copy.argtypes = [C.c_void_p, C.c_size_t]
+    obs = s2_obs_oracle()
+    cfg = engine.IntegratorConfig()
+    dt, mult, hint = cfg.plan_args(S2_PLANETS)
+    t, rv, er = engine.obs_arrays(obs)
+    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint)
+    rng = np.random.default_rng(0)
+    P = np.repeat(O.pal_params(S2_PLANETS)[None], W, 0)
+    P[:, :, :5] *= 1 + 1e-3 * rng.standard_normal((W, 2, 5))
+    K = torch.as_tensor(np.concatenate([P[:, p, :5].T for p in range(2)], 0).copy(), device="cuda")
+    for _ in range(3):
+        plan.logl(K)
+    torch.cuda.synchronize()
+    lib.rvm_prof_clear()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    plan.logl(K)
+    e1.record()
+    torch.cuda.synchronize()
+    buf = np.zeros(MAXW * SLOTS, dtype=np.uint64)
+    assert lib.rvm_prof_copy(buf.ctypes.data, buf.nbytes) == 0
+    b = buf.reshape(MAXW, SLOTS).astype(np.int64)
+    used = b[:, 4] != 0
+    b = b[used]
+    lvl = b[:, 7] & 0xFF
+    out = {"W": W, "event_ms": e0.elapsed_time(e1), "waves": int(used.sum()),
+           "realtime_span_us": float((b[:, 6].max() - b[:, 5].min()) / 100.0)}  # s_memrealtime: 100 MHz
+    for k in sorted(set(lvl.tolist())):
+        m = lvl == k
+        tot = b[m, 4] - b[m, 0]
+        out[f"level{k}"] = {"mult": int((b[m, 7][0] >> 16)), "total_kcyc": float(np.median(tot) / 1e3),
+                            "prologue_kcyc": float(np.median(b[m, 1] - b[m, 0]) / 1e3),
+                            "segments_kcyc": float(np.median(b[m, 2]) / 1e3),
+                            "epochs_kcyc": float(np.median(b[m, 3]) / 1e3),
+                            "tail_kcyc": float(np.median(tot - (b[m, 1] - b[m, 0]) - b[m, 2] - b[m, 3]) / 1e3),
+                            "max_total_kcyc": float(tot.max() / 1e3)}
+    rt = (b[:, 6] - b[:, 5]) / 100.0
+    out["wave_realtime_us"] = {"min": float(rt.min()), "median": float(np.median(rt)), "max": float(rt.max())}
+    out["start_spread_us"] = float((b[:, 5].max() - b[:, 5].min()) / 100.0)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -73,18 +73,20 @@ static void run(const char* name, double h, int blocks, long long* cyc, double* 
 }
 
 int main(int argc, char** argv) {
-    const double spo = argc > 1 ? atof(argv[1]) : 96.0;
-    const double h = 2.0 * M_PI * sqrt(0.88 * 0.88 * 0.88 / (1.0 + 1.2e-3)) / spo;
     long long* cyc;
     double* sink;
     hipMalloc(&cyc, 1024 * sizeof(long long));
     hipMalloc(&sink, 1024 * 64 * sizeof(double));
-    printf("steps per orbit %.0f, h = %.5f\n", spo, h);
-    for (int blocks : {1, 256, 512}) {
+    for (int a = 1; a < (argc > 1 ? argc : 2); a++) {
+        const double spo = argc > 1 ? atof(argv[a]) : 96.0;
+        const double h = 2.0 * M_PI * sqrt(0.88 * 0.88 * 0.88 / (1.0 + 1.2e-3)) / spo;
+        printf("steps per orbit %.0f, h = %.5f\n", spo, h);
+        const int blocks = 256;
         run<6, 0>("kick+drift<6>", h, blocks, cyc, sink);
+        run<7, 0>("kick+drift<7>", h, blocks, cyc, sink);
         run<8, 0>("kick+drift<8>", h, blocks, cyc, sink);
         run<6, 2>("drift<6>", h, blocks, cyc, sink);
-        run<6, 1>("kick", h, blocks, cyc, sink);
+        run<7, 2>("drift<7>", h, blocks, cyc, sink);
     }
     return 0;
 }
