@@ -807,11 +807,12 @@ static int wh_direction(int np, const double* pl, double hill_factor, const doub
     for (int i = 0; i < n; i++) {
         const double D = abs_t[i] - tprev;
         tprev = abs_t[i];
-        int ns = (D > 0.0) ? (int)ceil(D / h_target - 1e-9) : 0;
-        if (D > 0.0 && ns < 1) ns = 1;
-        ns *= sub;
+        int n1 = (D > 0.0) ? (int)ceil(D / h_target - 1e-9) : 0;
+        if (D > 0.0 && n1 < 1) n1 = 1;
+        const int ns = n1 * sub;
         if (ns > 0) {
-            const double h = sign * D / ns;
+            /* the segment's base step, then the level's: (sign D / n1) * (1/sub) */
+            const double h = (sign * D / n1) * (1.0 / sub);
             wh_drift(&s, 0.5 * h);
             for (int j = 0; j < ns; j++) {
                 wh_kick(&s, h);

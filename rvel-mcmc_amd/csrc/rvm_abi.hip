@@ -101,7 +101,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             int n = len > 0.0 ? (int)std::ceil(len / cfg->dt - 1e-9) : 0;
             if (len > 0.0 && n < 1) n = 1;
             D.seg_n.push_back(n);
-            D.seg_len.push_back(sign * len);
+            D.seg_len.push_back(n > 0 ? sign * len / n : 0.0);  // base step; level step = this / mult
             D.orv.push_back(rv[i]);
             D.os2.push_back(sigma[i] * sigma[i]);
             total_steps[dd] += n;
@@ -135,7 +135,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const size_t n = D.idx.size();
         S[dd]->n_epochs = (int32_t)n;
         std::memcpy(hd + od, D.seg_len.data(), n * sizeof(double));
-        S[dd]->seg_len = dd_base + od;
+        S[dd]->seg_h1 = dd_base + od;
         od += n;
         std::memcpy(hd + od, D.orv.data(), n * sizeof(double));
         S[dd]->obs_rv = dd_base + od;
@@ -169,6 +169,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     // Richardson weights for the h^2 expansion: level k steps dt/mult[k]; Lagrange at 0 in x = 1/mult^2
     for (int k = 0; k < RVM_MAX_LEVELS; k++) {
         P.mult[k] = k < cfg->n_levels ? mult[k] : 1;
+        P.inv_mult[k] = 1.0 / P.mult[k];
         P.lw[k] = 0.0;
         P.nt[k] = 8;
     }

@@ -198,9 +198,18 @@ struct Lane {
     double mu[NP];          // m_q / M_q: star barycentric velocity weights
     double dmin2, idmin2;   // (hill_factor * max r_Hill)^2 and its reciprocal
     double kA, kB, kC;      // closed-form 2-planet kick coefficients of the own lane (kick2)
+    double kAh, kBh, kCh;   // the same times the current step (lane_set_step)
     int p;                  // own planet index (lane % L, clamped to NP-1)
     bool enc;               // encounter flag (identical on all lanes of the group)
 };
+
+// Step-scaled kick coefficients: call whenever the step size changes (once per segment).
+template <int NP>
+__device__ __forceinline__ void lane_set_step(Lane<NP>& s, double h) {
+    s.kAh = s.kA * h;
+    s.kBh = s.kB * h;
+    s.kCh = s.kC * h;
+}
 
 // Derived per-lane constants (after p, GM, m, iMi, dmin2 are set).
 template <int NP>
@@ -217,6 +226,7 @@ __device__ __forceinline__ void lane_finish(Lane<NP>& s) {
     } else {
         s.kA = s.kB = s.kC = 0.0;
     }
+    lane_set_step(s, 0.0);
 }
 
 // Safeguarded universal-Kepler solve for the rare hard cases (a step spanning a large part of an
@@ -534,7 +544,7 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
 // with heliocentric x_1 = r'_1, x_2 = r'_2 + (m_1/M_1) r'_1, d02 = x_2, d12 = x_2 - x_1.  The
 // star--planet-1 distance |r'_1| and the own |r'| are carried from the drift: 2 rsq per kick.
 template <int L>
-__device__ __forceinline__ void kick2(Lane<2>& s, double dt) {
+__device__ __forceinline__ void kick2(Lane<2>& s) {
     const double x1 = grp_get<L, 0>(s.rx), y1 = grp_get<L, 0>(s.ry);
     const double R2x = grp_get<L, 1>(s.rx), R2y = grp_get<L, 1>(s.ry);
     const double ir01 = grp_get<L, 0>(s.ir);
@@ -545,16 +555,17 @@ __device__ __forceinline__ void kick2(Lane<2>& s, double dt) {
     const double r12sq = fma(dx12, dx12, dy12 * dy12);
     s.enc = s.enc | (r02sq < s.dmin2) | (r12sq < s.dmin2) | (ir01 * ir01 > s.idmin2);
     const double i02c = rcube_nr(r02sq), i12c = rcube_nr(r12sq);
-    const double A = s.kA * (s.ir * (s.ir * s.ir));
-    const double bx = s.kB * i02c, cx = s.kC * i12c;
-    s.vx = fma(dt, fma(A, s.rx, fma(bx, x2, cx * dx12)), s.vx);
-    s.vy = fma(dt, fma(A, s.ry, fma(bx, y2, cx * dy12)), s.vy);
+    // coefficients carry the step (lane_set_step): v += A r' + B x2/r02^3 + C d12/r12^3
+    const double A = s.kAh * (s.ir * (s.ir * s.ir));
+    const double bx = s.kBh * i02c, cx = s.kCh * i12c;
+    s.vx = fma(A, s.rx, fma(bx, x2, fma(cx, dx12, s.vx)));
+    s.vy = fma(A, s.ry, fma(bx, y2, fma(cx, dy12, s.vy)));
 }
 
 template <int NP, int L>
 __device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
     if constexpr (NP == 2)
-        kick2<L>(s, dt);
+        kick2<L>(s);  // step folded into the lane's coefficients (lane_set_step(s, dt) beforehand)
     else
         kick_generic<NP, L>(s, dt);
 }

@@ -10,7 +10,7 @@ namespace rvm {
 struct DirSched {
     int32_t n_epochs;
     const int32_t* seg_n;     // level-1 steps in the segment ending at this epoch (0: same time)
-    const double* seg_len;    // signed segment length (code time)
+    const double* seg_h1;     // signed base step of the segment: length / seg_n (0 if seg_n = 0)
     const double* obs_rv;     // observed RV
     const double* obs_s2;     // sigma^2
     const int32_t* obs_idx;   // index of the epoch in the plan's input order (rv_out rows)
@@ -22,6 +22,7 @@ struct DevPlan {
     int32_t n_levels;
     int32_t mult[RVM_MAX_LEVELS];  // level step multipliers (steps per base step)
     int32_t nt[RVM_MAX_LEVELS];    // Stumpff series terms per level (6, 7 or 8)
+    double inv_mult[RVM_MAX_LEVELS];  // 1 / mult: level step = seg_h1 * inv_mult
     double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
     double npoints;
     int32_t n_obs;

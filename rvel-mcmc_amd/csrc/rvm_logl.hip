@@ -40,6 +40,7 @@ __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 // the convergent DPP / ballot operations).
 template <int NT, bool GATED, int NP, int L>
 __device__ __forceinline__ void segment_steps(Lane<NP>& s, double h, int ns, bool& bad) {
+    lane_set_step(s, h);
     drift<NT, GATED>(s, 0.5 * h, bad);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
@@ -107,25 +108,31 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     __shared__ double s_rv[2][RVM_MAX_LEVELS][64];
     __shared__ int s_enc[RVM_MAX_LEVELS][64];
     // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
-    extern __shared__ double s_sched[];  // [E] seg_len | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
+    extern __shared__ double s_sched[];  // [E] seg_h1 | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
 
     const DirSched S = d ? P.bwd : P.fwd;
     // wave-uniform copies (SGPRs): the level's step divisor and Stumpff series length (rvm_device.h)
     const int lvl_u = __builtin_amdgcn_readfirstlane(lvl);
     const int mult = P.mult[lvl_u];
     const int nt = P.nt[lvl_u];
+    const double inv_mult = P.inv_mult[lvl_u];
     const int E = S.n_epochs;
     double* l_len = s_sched;
     double* l_rv = s_sched + E;
     double* l_s2 = s_sched + 2 * E;
     int* l_n = reinterpret_cast<int*>(s_sched + 3 * E);
     int* l_idx = l_n + E;
-    for (int i = threadIdx.x; i < E; i += blockDim.x) {
-        l_len[i] = S.seg_len[i];
-        l_rv[i] = S.obs_rv[i];
-        l_s2[i] = S.obs_s2[i];
-        l_n[i] = S.seg_n[i];
-        l_idx[i] = S.obs_idx[i];
+    // first chunk of the schedule: loads issued now, stored to LDS after the setup below so their
+    // latency hides behind the Pal conversion
+    const int i0 = threadIdx.x;
+    double st_h = 0.0, st_rv = 0.0, st_s2 = 0.0;
+    int st_n = 0, st_idx = 0;
+    if (i0 < E) {
+        st_h = S.seg_h1[i0];
+        st_rv = S.obs_rv[i0];
+        st_s2 = S.obs_s2[i0];
+        st_n = S.seg_n[i0];
+        st_idx = S.obs_idx[i0];
     }
 
     // ---- walker parameters (m, a, h, k, l per planet), prior (state.py:299-315) ----------------
@@ -219,6 +226,21 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         s.enc = t0.enc;
     }
 
+    if (i0 < E) {
+        l_len[i0] = st_h;
+        l_rv[i0] = st_rv;
+        l_s2[i0] = st_s2;
+        l_n[i0] = st_n;
+        l_idx[i0] = st_idx;
+    }
+    for (int i = i0 + blockDim.x; i < E; i += blockDim.x) {
+        l_len[i] = S.seg_h1[i];
+        l_rv[i] = S.obs_rv[i];
+        l_s2[i] = S.obs_s2[i];
+        l_n[i] = S.seg_n[i];
+        l_idx[i] = S.obs_idx[i];
+    }
+
     // ---- integrate outward from t = 0 through this direction's epochs -------------------------
     __syncthreads();  // schedule staged
     PROF_T(t_pro);
@@ -235,7 +257,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         const int ns = n1 * mult;
         PROF_T(ta);
         if (ns > 0) {
-            const double h = len / (double)ns;
+            const double h = len * inv_mult;  // len holds the segment's base step
             if (nt <= 6)
                 segment<6, true, NP, L>(s, h, ns);
             else if (nt == 7)

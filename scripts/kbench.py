@@ -34,7 +34,7 @@ def main():
         lp, st, _ = plan.logl(K)
         torch.cuda.synchronize()
         times = []
-        for _ in range(5):
+        for _ in range(int(os.environ.get("REPS", "20"))):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             plan.logl(K, out=lp, status=st)
