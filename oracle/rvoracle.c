@@ -746,7 +746,7 @@ static int wh_drift(wh_state* s, double h) {
 }
 
 /* diagnostics: smallest pair-distance^2 / exit-distance^2 seen by wh_kick since the last reset */
-static double g_min_ratio = 1e300;
+static _Thread_local double g_min_ratio = 1e300; /* diagnostic, per calling thread */
 double rvo_debug_min_ratio(int reset) {
     const double v = g_min_ratio;
     if (reset) g_min_ratio = 1e300;
