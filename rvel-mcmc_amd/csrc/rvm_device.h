@@ -200,7 +200,9 @@ struct Lane {
     double kA, kB, kC;      // closed-form 2-planet kick coefficients of the own lane (kick2)
     double kAh, kBh, kCh;   // the same times the current step (lane_set_step)
     int p;                  // own planet index (lane % L, clamped to NP-1)
-    bool enc;               // encounter flag (identical on all lanes of the group)
+    uint64_t encm;          // wave mask of lanes that saw a pair closer than the exit distance
+                            // (SGPRs: the kick's compares go straight into it; identical bits on
+                            // all lanes of a walker's group)
 };
 
 // Step-scaled kick coefficients: call whenever the step size changes (once per segment).
@@ -492,7 +494,7 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
         ax[i] = 0.0;
         ay[i] = 0.0;
     }
-    bool enc = false;
+    uint64_t enc = 0;
     // star -- planet 1 distance is |r'_1|, already known to planet 1's lane from its drift
     const double ir01 = (NP == 1) ? s.ir : grp_get<L>(s.ir, 0);
 #pragma unroll
@@ -503,10 +505,10 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
             double ir;
             if (i == 0 && j == 1) {
                 ir = ir01;
-                enc = enc | (ir * ir > s.idmin2);
+                enc |= ballot(ir * ir > s.idmin2);
             } else {
                 const double r2 = dx * dx + dy * dy;
-                enc = enc | (r2 < s.dmin2);
+                enc |= ballot(r2 < s.dmin2);
                 ir = rsq_nr(r2);
             }
             const double ir3 = ir * ir * ir;
@@ -518,7 +520,7 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
             ay[j] -= mi * ir3 * dy;
         }
     }
-    s.enc = s.enc | enc;
+    s.encm |= enc;
     // Jacobi acceleration of the own coordinate (index i = p + 1)
     double max_ = ax[0], may_ = ay[0];  // M_star = 1
     double ajx = 0.0, ajy = 0.0;
@@ -553,7 +555,7 @@ __device__ __forceinline__ void kick2(Lane<2>& s) {
     const double dx12 = x2 - x1, dy12 = y2 - y1;
     const double r02sq = fma(x2, x2, y2 * y2);
     const double r12sq = fma(dx12, dx12, dy12 * dy12);
-    s.enc = s.enc | (r02sq < s.dmin2) | (r12sq < s.dmin2) | (ir01 * ir01 > s.idmin2);
+    s.encm |= ballot(r02sq < s.dmin2) | ballot(r12sq < s.dmin2) | ballot(ir01 * ir01 > s.idmin2);
     const double i02c = rcube_nr(r02sq), i12c = rcube_nr(r12sq);
     // coefficients carry the step (lane_set_step): v += A r' + B x2/r02^3 + C d12/r12^3
     const double A = s.kAh * (s.ir * (s.ir * s.ir));

@@ -65,7 +65,7 @@ __device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
     bool bad = false;
     if constexpr (SPEC) {
         const double rx = s.rx, ry = s.ry, vx = s.vx, vy = s.vy, r = s.r, ir = s.ir;
-        const bool enc = s.enc;
+        const uint64_t encm = s.encm;
         segment_steps<NT, false, NP, L>(s, h, ns, bad);
         if (__builtin_expect(ballot(bad) != 0, 0)) {
             s.rx = rx;
@@ -74,7 +74,7 @@ __device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
             s.vy = vy;
             s.r = r;
             s.ir = ir;
-            s.enc = enc;
+            s.encm = encm;
             segment_steps<NT, true, NP, L>(s, h, ns, bad);
         }
     } else {
@@ -218,12 +218,12 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     }
     s.r = sqrt(s.rx * s.rx + s.ry * s.ry);
     s.ir = 1.0 / s.r;
-    s.enc = false;
+    s.encm = 0;
     lane_finish(s);
     {
         Lane<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
         kick<NP, L>(t0, 0.0);
-        s.enc = t0.enc;
+        s.encm = t0.encm;
     }
 
     if (i0 < E) {
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         t_epo += tc - tb;
 #endif
     }
-    if (pl_idx == 0) s_enc[lvl][slot] = (s.enc ? 1 : 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
+    if (pl_idx == 0) s_enc[lvl][slot] = (int)((s.encm >> lane) & 1) | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
     if (lvl == 0 && lane < WPB) {
         const int wo = blockIdx.x * WPB + lane;

@@ -38,7 +38,7 @@ __global__ void step_bench(double h, long long* cyc, double* sink) {
     s.vy = p ? VY - m[0] * vy1 * s.iMi[1] : VY;
     s.r = sqrt(s.rx * s.rx + s.ry * s.ry);
     s.ir = 1.0 / s.r;
-    s.enc = false;
+    s.encm = 0;
     lane_finish(s);
     __syncthreads();
     const long long t0 = clock64();
@@ -48,7 +48,7 @@ __global__ void step_bench(double h, long long* cyc, double* sink) {
         if (MODE != 1) drift<NT>(s, h);
     }
     const long long t1 = clock64();
-    sink[blockIdx.x * 64 + lane] = s.rx + s.vy + (s.enc ? 1.0 : 0.0);
+    sink[blockIdx.x * 64 + lane] = s.rx + s.vy + (s.encm ? 1.0 : 0.0);
     if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
