@@ -17,7 +17,8 @@
  *     move (EnsembleSampler._propose_stretch)
  *   mcmc.py:89-121 Mh.generate_proposal / Mh.step          rvm_mh_propose / rvm_mh_accept
  *   mcmc.py:144-187 Smala.generate_proposal/step           rvm_fd_params (finite-difference stencil)
- *                                                          + host-side metric
+ *     mcmc.py:135-139 Smala.softabs,                         + rvm_smala_derive / rvm_smala_propose /
+ *     mcmc.py:158-162 Smala.transitionProbability              rvm_smala_accept
  *
  * Conventions
  *   - All array pointers passed to launch functions are DEVICE pointers (hipMalloc / torch CUDA
@@ -53,6 +54,7 @@ extern "C" {
 #define RVM_MAX_PLANETS 4
 #define RVM_MAX_LEVELS 6
 #define RVM_MAX_EPOCHS_PER_DIRECTION 1700 /* epochs with t >= 0, and with t < 0, per plan */
+#define RVM_SMALA_MAX_PARAMS 20           /* free parameters per SMALA chain                 */
 
 /* Integrator configuration of a plan. */
 typedef struct {
@@ -123,6 +125,43 @@ int rvm_mh_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, doubl
  * per-epoch RV Jacobian. */
 int rvm_fd_params(int32_t n_params, int32_t n_chains, const double* x, double rel_step, const double* floor_,
                   double* out, void* stream);
+
+/* ---- SMALA (mcmc.py:126-187) on device, one thread per chain ---------------------------------
+ * Per-chain quantities a SMALA step needs at a point x; all device arrays, C = n_chains,
+ * P = n_params (<= RVM_SMALA_MAX_PARAMS), matrices row-major per chain: element (i, j) of chain c
+ * at [(i * P + j) * C + c]. */
+typedef struct {
+    double* lp;      /* [C]       logp(x)                                                          */
+    double* grad;    /* [P][C]    central-difference gradient of logp                              */
+    double* mu;      /* [P][C]    drift x + eps^2/2 G^-1 grad                  (mcmc.py:150)        */
+    double* L;       /* [P*P][C]  Cholesky factor of G^-1, lower                (mcmc.py:149)        */
+    double* G;       /* [P*P][C]  SoftAbs metric Q diag(lambda coth(alpha lambda)) Q^T of eig(-H)  */
+    double* logdet;  /* [C]       log det G^-1                                                     */
+    int32_t* ok;     /* [C]       1: clean stencil and positive-definite metric                    */
+} rvm_smala_cache;
+
+/* From one rvm_logl_batch launch over rvm_fd_params' stencil of x (same x, rel_step, floor_;
+ * walkers s * C + c, with rv_out): the gradient from the stencil's logp, the Gauss-Newton Hessian
+ * H = -(2/npoints) J^T diag(inv_sigma2) J from its per-epoch model RVs (rv_stencil
+ * [n_obs][(2P+1) C], rows in the plan's input epoch order; inv_sigma2 [n_obs] in the same order),
+ * the SoftAbs metric of -H (cyclic Jacobi eigen-solver), G^-1, its Cholesky factor and the drift.
+ * Replaces state.py:253-294 (variational derivatives) + mcmc.py:135-150. */
+int rvm_smala_derive(int32_t n_params, int32_t n_chains, int32_t n_obs, const double* x, double rel_step,
+                     const double* floor_, const double* lp_stencil, const int32_t* status_stencil,
+                     const double* rv_stencil, const double* inv_sigma2, double npoints_norm, double alpha,
+                     double eps, const rvm_smala_cache* out, void* stream);
+/* x_prop = mu + eps chol(G^-1) z (x where the cache is not ok); z ~ N(0,1) from Philox keyed by
+ * (seed, chain_begin + c, iteration, 5 | p << 8) or from draws [P][C].  mcmc.py:144-153. */
+int rvm_smala_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, const double* x,
+                      const rvm_smala_cache* cur, double eps, uint64_t seed, uint64_t iteration,
+                      const double* draws, double* x_prop, void* stream);
+/* exp(lp* - lp + log q(x | x*) - log q(x* | x)) > u  (u from Philox stream 6 or draws [C]), both
+ * caches ok and lp* finite -> x <- x_prop, cur <- prop (per chain), accepted[c] += 1.
+ * failures[c] += 1 (nullable) when the proposal's metric failed with a finite logp.
+ * mcmc.py:158-187. */
+int rvm_smala_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const rvm_smala_cache* cur,
+                     const double* x_prop, const rvm_smala_cache* prop, double eps, uint64_t seed,
+                     uint64_t iteration, const double* draws, int32_t* accepted, int32_t* failures, void* stream);
 
 const char* rvm_last_error(void);
 int rvm_abi_version(void);

@@ -28,6 +28,14 @@ hipError_t launch_mh_propose(int P, int n, int64_t b, const double* x, const dou
 hipError_t launch_mh_accept(int P, int n, int64_t b, double* x, double* lnp, const double* q, const double* lnp_new,
                             uint64_t seed, uint64_t it, const double* draws, int32_t* acc, hipStream_t st);
 hipError_t launch_fd_params(int P, int n, const double* x, double rel, const double* fl, double* out, hipStream_t st);
+hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,
+                               const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
+                               double npoints, double alpha, double eps, const SmalaCache& out, hipStream_t st);
+hipError_t launch_smala_propose(int P, int C, int64_t begin, const double* x, const SmalaCache& cur, double eps,
+                                uint64_t seed, uint64_t it, const double* draws, double* xs, hipStream_t st);
+hipError_t launch_smala_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
+                               const SmalaCache& prop, double eps, uint64_t seed, uint64_t it, const double* draws,
+                               int32_t* accepted, int32_t* failures, hipStream_t st);
 }  // namespace rvm
 
 struct rvm_plan {
@@ -275,6 +283,53 @@ int rvm_fd_params(int32_t n_params, int32_t n_chains, const double* x, double re
         return fail(-1, "rvm_fd_params: bad arguments");
     hipError_t e = rvm::launch_fd_params(n_params, n_chains, x, rel_step, floor_, out, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_fd_params");
+}
+
+static bool smala_cache_ok(const rvm_smala_cache* c) {
+    return c && c->lp && c->grad && c->mu && c->L && c->G && c->logdet && c->ok;
+}
+
+static rvm::SmalaCache smala_cache(const rvm_smala_cache* c) {
+    return rvm::SmalaCache{c->lp, c->grad, c->mu, c->L, c->G, c->logdet, c->ok};
+}
+
+int rvm_smala_derive(int32_t n_params, int32_t n_chains, int32_t n_obs, const double* x, double rel_step,
+                     const double* floor_, const double* lp_stencil, const int32_t* status_stencil,
+                     const double* rv_stencil, const double* inv_sigma2, double npoints_norm, double alpha,
+                     double eps, const rvm_smala_cache* out, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || n_obs < 0 || !x || !floor_ ||
+        !lp_stencil || !status_stencil || (n_obs > 0 && (!rv_stencil || !inv_sigma2)) || !smala_cache_ok(out) ||
+        !(rel_step > 0.0) || !(npoints_norm != 0.0) || !(alpha > 0.0))
+        return fail(-1, "rvm_smala_derive: bad arguments");
+    hipError_t e = rvm::launch_smala_derive(n_params, n_chains, n_obs, x, rel_step, floor_, lp_stencil,
+                                            status_stencil, rv_stencil, inv_sigma2, npoints_norm, alpha, eps,
+                                            smala_cache(out), (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_derive");
+}
+
+int rvm_smala_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, const double* x,
+                      const rvm_smala_cache* cur, double eps, uint64_t seed, uint64_t iteration,
+                      const double* draws, double* x_prop, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || !x || !x_prop || !smala_cache_ok(cur))
+        return fail(-1, "rvm_smala_propose: bad arguments");
+    hipError_t e = rvm::launch_smala_propose(n_params, n_chains, chain_begin, x, smala_cache(cur), eps, seed, iteration,
+                                             draws, x_prop, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_propose");
+}
+
+int rvm_smala_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const rvm_smala_cache* cur,
+                     const double* x_prop, const rvm_smala_cache* prop, double eps, uint64_t seed,
+                     uint64_t iteration, const double* draws, int32_t* accepted, int32_t* failures, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || !x || !x_prop || !smala_cache_ok(cur) ||
+        !smala_cache_ok(prop))
+        return fail(-1, "rvm_smala_accept: bad arguments");
+    hipError_t e = rvm::launch_smala_accept(n_params, n_chains, chain_begin, x, smala_cache(cur), x_prop,
+                                            smala_cache(prop), eps, seed, iteration, draws, accepted, failures,
+                                            (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_accept");
 }
 
 }  // extern "C"

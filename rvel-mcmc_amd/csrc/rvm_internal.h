@@ -29,4 +29,15 @@ struct DevPlan {
     DirSched fwd, bwd;
 };
 
+// rvm_smala_cache by value as a kernel argument (same layout)
+struct SmalaCache {
+    double* lp;
+    double* grad;
+    double* mu;
+    double* L;
+    double* G;
+    double* logdet;
+    int32_t* ok;
+};
+
 }  // namespace rvm

@@ -1,0 +1,344 @@
+// rvm_smala.hip -- device SMALA (simplified manifold MALA, SoftAbs metric), mcmc.py:126-187.
+//
+// Per step and chain the reference (mcmc.py:144-187) needs logp, its gradient and Hessian, the
+// SoftAbs metric G = Q diag(lambda coth(alpha lambda)) Q^T of eig(-H) (mcmc.py:135-139), its
+// inverse and the Cholesky factor of the inverse (the proposal's covariance eps^2 G^-1), the drift
+// mu = x + eps^2/2 G^-1 grad, and the Gaussian q-ratio of the proposal.  Derivatives come from one
+// likelihood launch over the central-difference stencil (rvm_fd_params): the gradient from the
+// stencil's logp, the Gauss-Newton Hessian H = -(2/N) J^T diag(1/sigma^2) J from its per-epoch
+// model RVs (rv_out).  Everything after the launch happens here; the per-chain math runs one
+// wave per chain with the chain's P x P matrices in LDS:
+//
+//   smala_derive_kernel   stencil -> lp, grad, mu, chol(G^-1), G, log det G^-1, ok
+//                         (cyclic Jacobi eigen-solver for the symmetric P x P -H, rows on lanes)
+//   smala_propose_kernel  x* = mu + eps chol(G^-1) z          (z: Philox Box-Muller or injected)
+//   smala_accept_kernel   q-ratio, accept, copy the proposal's cached derivatives on accept
+//
+// Compiled without FMA contraction like the other sampler kernels.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "rvm_device.h"
+#include "rvm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace rvm {
+
+enum : uint32_t {
+    RNG_SMALA_PROPOSE = 5,
+    RNG_SMALA_ACCEPT = 6,
+};
+
+// One wave per chain: the P x P matrices live in LDS, lanes own matrix rows / entries, and the
+// sequential parts (Jacobi rotations, Cholesky columns) run lock-step across the wave.
+__global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, const double* __restrict__ x,
+                                                          double rel, const double* __restrict__ fl,
+                                                          const double* __restrict__ lp_st,
+                                                          const int32_t* __restrict__ st_st,
+                                                          const double* __restrict__ rv,
+                                                          const double* __restrict__ w, double npoints,
+                                                          double alpha, double eps, SmalaCache out) {
+    constexpr int PM = RVM_SMALA_MAX_PARAMS;
+    constexpr int NTRI = PM * (PM + 1) / 2;        // upper-triangle entries
+    constexpr int PER_LANE = (NTRI + 63) / 64;     // accumulators per lane
+    __shared__ double A[PM * PM], Qm[PM * PM];
+    __shared__ double den[PM], gr[PM], lt[PM], inv[PM], xv[PM];
+    __shared__ double Jc[64];
+    __shared__ int okflag;
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int S = 2 * P + 1;
+    const size_t SC = (size_t)S * C;
+    const int ntri = P * (P + 1) / 2;
+    if (lane == 0) okflag = 1;
+    __syncthreads();
+    for (int s = lane; s < S; s += 64)
+        if (st_st[(size_t)s * C + c] != 0) okflag = 0;
+    // realised steps exactly as rvm_fd_params formed the stencil; gradient
+    if (lane < P) {
+        const double xp = x[(size_t)lane * C + c];
+        const double ax = fabs(xp) > fl[lane] ? fabs(xp) : fl[lane];
+        const double e = rel * ax;
+        const double d = (xp + e) - (xp - e);
+        const double g = (lp_st[(size_t)(1 + 2 * lane) * C + c] - lp_st[(size_t)(2 + 2 * lane) * C + c]) / d;
+        den[lane] = d;
+        gr[lane] = g;
+        xv[lane] = xp;
+        out.grad[(size_t)lane * C + c] = g;
+    }
+    __syncthreads();
+    // -H = (2/N) sum_e J_e^T (1/sigma_e^2) J_e, J_e[p] = (rv_e(x+e_p) - rv_e(x-e_p)) / den_p:
+    // K = 64/P epochs of J per chunk in LDS, each lane accumulates its upper-triangle entries
+    int tp[PER_LANE], tq[PER_LANE];
+    double acc[PER_LANE];
+#pragma unroll
+    for (int j = 0; j < PER_LANE; j++) {
+        const int idx = lane + 64 * j;
+        int p = 0, rem = idx;
+        while (p < P && rem >= P - p) {
+            rem -= P - p;
+            p++;
+        }
+        tp[j] = p;
+        tq[j] = p + rem;
+        acc[j] = 0.0;
+    }
+    const int K = 64 / P;
+    for (int e0 = 0; e0 < E; e0 += K) {
+        {
+            const int k = lane / P, p = lane % P;
+            const int e = e0 + k;
+            if (k < K && e < E) {
+                const double* re = rv + (size_t)e * SC;
+                Jc[lane] = (re[(size_t)(1 + 2 * p) * C + c] - re[(size_t)(2 + 2 * p) * C + c]) / den[p];
+            }
+        }
+        __syncthreads();
+        const int kmax = E - e0 < K ? E - e0 : K;
+#pragma unroll
+        for (int j = 0; j < PER_LANE; j++) {
+            if (lane + 64 * j < ntri) {
+                double a = acc[j];
+                for (int k = 0; k < kmax; k++) a += (Jc[k * P + tp[j]] * w[e0 + k]) * Jc[k * P + tq[j]];
+                acc[j] = a;
+            }
+        }
+        __syncthreads();
+    }
+    const double fac = 2.0 / npoints;
+#pragma unroll
+    for (int j = 0; j < PER_LANE; j++) {
+        if (lane + 64 * j < ntri) {
+            const double a = fac * acc[j];
+            A[tp[j] * P + tq[j]] = a;
+            A[tq[j] * P + tp[j]] = a;
+        }
+    }
+    for (int i = lane; i < P * P; i += 64) Qm[i] = (i / P == i % P) ? 1.0 : 0.0;
+    __syncthreads();
+    // cyclic Jacobi: A -> diag(lambda), Q -> eigenvectors (A = Q diag(lambda) Q^T).  Every lane
+    // computes the rotation from the same LDS values; lane r updates row/column r.
+    for (int sweep = 0; sweep < 60; sweep++) {
+        double off = 0.0, dia = 0.0;
+        for (int i = 0; i < P; i++) {
+            dia += A[i * P + i] * A[i * P + i];
+            for (int j = i + 1; j < P; j++) off += A[i * P + j] * A[i * P + j];
+        }
+        if (!(off > 1e-32 * dia)) break;  // converged (or NaN: caught by the SoftAbs check)
+        for (int p = 0; p < P - 1; p++) {
+            for (int q = p + 1; q < P; q++) {
+                const double apq = A[p * P + q];
+                if (apq == 0.0) continue;
+                const double app = A[p * P + p], aqq = A[q * P + q];
+                const double theta = (aqq - app) / (2.0 * apq);
+                double tt = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                if (theta < 0.0) tt = -tt;
+                const double cs = 1.0 / sqrt(tt * tt + 1.0);
+                const double sn = tt * cs;
+                const double tau = sn / (1.0 + cs);
+                double nrp = 0.0, nrq = 0.0, qnp = 0.0, qnq = 0.0;
+                const int r = lane;
+                if (r < P) {
+                    const double qrp = Qm[r * P + p], qrq = Qm[r * P + q];
+                    qnp = qrp - sn * (qrq + tau * qrp);
+                    qnq = qrq + sn * (qrp - tau * qrq);
+                    if (r != p && r != q) {
+                        const double arp = A[r * P + p], arq = A[r * P + q];
+                        nrp = arp - sn * (arq + tau * arp);
+                        nrq = arq + sn * (arp - tau * arq);
+                    }
+                }
+                __syncthreads();
+                if (r < P) {
+                    Qm[r * P + p] = qnp;
+                    Qm[r * P + q] = qnq;
+                    if (r != p && r != q) {
+                        A[r * P + p] = nrp;
+                        A[p * P + r] = nrp;
+                        A[r * P + q] = nrq;
+                        A[q * P + r] = nrq;
+                    } else if (r == p) {
+                        A[p * P + p] = app - tt * apq;
+                        A[p * P + q] = 0.0;
+                        A[q * P + p] = 0.0;
+                    } else {
+                        A[q * P + q] = aqq + tt * apq;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+    // SoftAbs (mcmc.py:135-139): lambda~ = lambda coth(alpha lambda), 1/alpha where |alpha lambda| < 1e-8
+    if (lane < P) {
+        const double lam = A[lane * P + lane];
+        const double al = alpha * lam;
+        const double l = fabs(al) < 1e-8 ? 1.0 / alpha : lam / tanh(al);
+        lt[lane] = l;
+        inv[lane] = 1.0 / l;
+        if (!(isfinite(l) && l > 0.0)) okflag = 0;
+    }
+    __syncthreads();
+    // G = Q diag(lambda~) Q^T (out) and G^-1 = Q diag(1/lambda~) Q^T (into A)
+    for (int idx = lane; idx < ntri; idx += 64) {
+        int p = 0, rem = idx;
+        while (rem >= P - p) {
+            rem -= P - p;
+            p++;
+        }
+        const int q = p + rem;
+        double g = 0.0, gi = 0.0;
+        for (int k = 0; k < P; k++) {
+            const double qpk = Qm[p * P + k], qqk = Qm[q * P + k];
+            g += (qpk * lt[k]) * qqk;
+            gi += (qpk * inv[k]) * qqk;
+        }
+        out.G[(size_t)(p * P + q) * C + c] = g;
+        out.G[(size_t)(q * P + p) * C + c] = g;
+        A[p * P + q] = gi;
+        A[q * P + p] = gi;
+    }
+    __syncthreads();
+    // drift mu = x + eps^2/2 G^-1 grad   (mcmc.py:150)
+    if (lane < P) {
+        double sgi = 0.0;
+        for (int q = 0; q < P; q++) sgi += A[lane * P + q] * gr[q];
+        out.mu[(size_t)lane * C + c] = xv[lane] + (0.5 * eps * eps) * sgi;
+    }
+    __syncthreads();
+    // Cholesky of G^-1 (lower, in place; mcmc.py:149): column j, rows i > j in parallel
+    for (int j = 0; j < P; j++) {
+        double d = A[j * P + j];
+        for (int k = 0; k < j; k++) d -= A[j * P + k] * A[j * P + k];
+        const double ljj = sqrt(d > 0.0 ? d : 1.0);
+        double lij = 0.0;
+        const int i = lane;
+        if (i > j && i < P) {
+            double s = A[i * P + j];
+            for (int k = 0; k < j; k++) s -= A[i * P + k] * A[j * P + k];
+            lij = s / ljj;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            A[j * P + j] = ljj;
+            if (!(d > 0.0)) okflag = 0;
+        }
+        if (i > j && i < P) A[i * P + j] = lij;
+        __syncthreads();
+    }
+    for (int idx = lane; idx < P * P; idx += 64) {
+        const int i = idx / P, j = idx % P;
+        out.L[(size_t)idx * C + c] = j <= i ? A[idx] : 0.0;
+    }
+    if (lane == 0) {
+        double logdet = 0.0;  // log det G^-1
+        for (int k = 0; k < P; k++) logdet += log(inv[k]);
+        out.lp[c] = lp_st[c];
+        out.logdet[c] = logdet;
+        out.ok[c] = okflag;
+    }
+}
+
+__device__ __forceinline__ double box_muller_s(double u0, double u1) {
+    return sqrt(-2.0 * log(u0)) * cospi(2.0 * u1);
+}
+
+__global__ void smala_propose_kernel(int P, int C, int64_t begin, const double* __restrict__ x, SmalaCache cur,
+                                     double eps, uint64_t seed, uint64_t iteration, const double* __restrict__ draws,
+                                     double* __restrict__ xs) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    if (!cur.ok[c]) {  // no usable metric at x: stay (the proposal is then rejected)
+        for (int p = 0; p < P; p++) xs[(size_t)p * C + c] = x[(size_t)p * C + c];
+        return;
+    }
+    double z[RVM_SMALA_MAX_PARAMS];
+    for (int p = 0; p < P; p++) {
+        if (draws) {
+            z[p] = draws[(size_t)p * C + c];
+        } else {
+            double u0, u1;
+            uniform2(seed, (uint64_t)(begin + c), iteration, RNG_SMALA_PROPOSE | ((uint32_t)p << 8), u0, u1);
+            z[p] = box_muller_s(u0, u1);
+        }
+    }
+    // mcmc.py:151: newparams = mu + eps * chol(G^-1) . N(0,1)
+    for (int p = 0; p < P; p++) {
+        double s = 0.0;
+        for (int q = 0; q <= p; q++) s += cur.L[(size_t)(p * P + q) * C + c] * z[q];
+        xs[(size_t)p * C + c] = cur.mu[(size_t)p * C + c] + eps * s;
+    }
+}
+
+// log N(y; mu, eps^2 G^-1) = -1/2 [ (y-mu)^T G (y-mu) / eps^2 + P log eps^2 + log det G^-1 + P log 2 pi ]
+__device__ __forceinline__ double mvn_logpdf(int P, int C, int c, const double* y, const double* mu, const double* G,
+                                             double logdet, double eps) {
+    double maha = 0.0;
+    for (int p = 0; p < P; p++) {
+        const double dp = y[(size_t)p * C + c] - mu[(size_t)p * C + c];
+        double s = 0.0;
+        for (int q = 0; q < P; q++) s += G[(size_t)(p * P + q) * C + c] * (y[(size_t)q * C + c] - mu[(size_t)q * C + c]);
+        maha += dp * s;
+    }
+    return -0.5 * (maha / (eps * eps) + (double)P * log(eps * eps) + logdet + (double)P * log(2.0 * M_PI));
+}
+
+__global__ void smala_accept_kernel(int P, int C, int64_t begin, double* __restrict__ x, SmalaCache cur,
+                                    const double* __restrict__ xs, SmalaCache prop, double eps, uint64_t seed,
+                                    uint64_t iteration, const double* __restrict__ draws, int32_t* __restrict__ accepted,
+                                    int32_t* __restrict__ failures) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double u, unused;
+    if (draws) {
+        u = draws[c];
+    } else {
+        uniform2(seed, (uint64_t)(begin + c), iteration, RNG_SMALA_ACCEPT, u, unused);
+    }
+    const bool okc = cur.ok[c] != 0, okp = prop.ok[c] != 0;
+    const double lpp = prop.lp[c];
+    if (failures && !okp && isfinite(lpp)) failures[c] += 1;  // metric failure with a finite logp
+    if (!(okc && okp && isfinite(lpp))) return;
+    // mcmc.py:176-181: ratio = exp(logp* - logp + log q(x|x*) - log q(x*|x)) > uniform
+    const double q_ts_t = mvn_logpdf(P, C, c, xs, cur.mu, cur.G, cur.logdet[c], eps);
+    const double q_t_ts = mvn_logpdf(P, C, c, x, prop.mu, prop.G, prop.logdet[c], eps);
+    const double ratio = exp(lpp - cur.lp[c] + q_t_ts - q_ts_t);
+    if (!(ratio > u)) return;
+    for (int p = 0; p < P; p++) {
+        x[(size_t)p * C + c] = xs[(size_t)p * C + c];
+        cur.mu[(size_t)p * C + c] = prop.mu[(size_t)p * C + c];
+        cur.grad[(size_t)p * C + c] = prop.grad[(size_t)p * C + c];
+    }
+    for (int i = 0; i < P * P; i++) {
+        cur.L[(size_t)i * C + c] = prop.L[(size_t)i * C + c];
+        cur.G[(size_t)i * C + c] = prop.G[(size_t)i * C + c];
+    }
+    cur.lp[c] = lpp;
+    cur.logdet[c] = prop.logdet[c];
+    cur.ok[c] = 1;
+    if (accepted) accepted[c] += 1;
+}
+
+hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,
+                               const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
+                               double npoints, double alpha, double eps, const SmalaCache& out, hipStream_t st) {
+    smala_derive_kernel<<<C, 64, 0, st>>>(P, C, E, x, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_smala_propose(int P, int C, int64_t begin, const double* x, const SmalaCache& cur, double eps,
+                                uint64_t seed, uint64_t it, const double* draws, double* xs, hipStream_t st) {
+    smala_propose_kernel<<<(C + 127) / 128, 128, 0, st>>>(P, C, begin, x, cur, eps, seed, it, draws, xs);
+    return hipGetLastError();
+}
+
+hipError_t launch_smala_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
+                               const SmalaCache& prop, double eps, uint64_t seed, uint64_t it, const double* draws,
+                               int32_t* accepted, int32_t* failures, hipStream_t st) {
+    smala_accept_kernel<<<(C + 127) / 128, 128, 0, st>>>(P, C, begin, x, cur, xs, prop, eps, seed, it, draws,
+                                                         accepted, failures);
+    return hipGetLastError();
+}
+
+}  // namespace rvm

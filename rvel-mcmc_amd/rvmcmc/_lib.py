@@ -31,6 +31,13 @@ class RvmConfig(C.Structure):
     ]
 
 
+RVM_SMALA_MAX_PARAMS = 20
+
+
+class SmalaCache(C.Structure):  # include/rvmcmc.h: rvm_smala_cache (device pointers)
+    _fields_ = [(k, C.c_void_p) for k in ("lp", "grad", "mu", "L", "G", "logdet", "ok")]
+
+
 class RvmError(RuntimeError):
     pass
 
@@ -39,6 +46,12 @@ class RvmError(RuntimeError):
 _dp = C.c_void_p  # device pointers are passed as integers (torch.Tensor.data_ptr())
 SIGNATURES = {
     "rvm_abi_version": (C.c_int, []),
+    "rvm_smala_derive": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _dp, C.c_double, _dp, _dp, _dp, _dp, _dp,
+                                   C.c_double, C.c_double, C.c_double, C.POINTER(SmalaCache), _dp]),
+    "rvm_smala_propose": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, C.POINTER(SmalaCache), C.c_double,
+                                    C.c_uint64, C.c_uint64, _dp, _dp, _dp]),
+    "rvm_smala_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, C.POINTER(SmalaCache), _dp,
+                                   C.POINTER(SmalaCache), C.c_double, C.c_uint64, C.c_uint64, _dp, _dp, _dp, _dp]),
     "rvm_last_error": (C.c_char_p, []),
     "rvm_plan_create": (C.c_int, [C.POINTER(RvmConfig), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),

@@ -17,6 +17,7 @@ defined; parity is statistical.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import numpy as np
@@ -102,7 +103,12 @@ def _mvn_logpdf(x, mu, Ginv, logdetGinv, eps):
 
 
 class SmalaChains:
-    """C independent SMALA chains on the device (config 4: 256 chains)."""
+    """C independent SMALA chains on the device (config 4: 256 chains).
+
+    Per step (mcmc.py:167-187 for every chain at once): rvm_smala_propose, one likelihood launch
+    over the (2P+1)-point stencil of the proposals (rvm_fd_params + rvm_logl_batch with rv_out),
+    rvm_smala_derive (gradient, Gauss-Newton Hessian, SoftAbs metric by a per-chain Jacobi
+    eigen-solver, Cholesky, drift) and rvm_smala_accept.  No host synchronisation in step()."""
 
     def __init__(self, initial_state, obs, eps, alpha, n_chains, X0=None, seed=0, device=None, rel_step=FD_REL_STEP):
         torch = _torch()
@@ -111,49 +117,78 @@ class SmalaChains:
         self.eps = float(eps)
         self.alpha = float(alpha)
         self.P = self.state.Nvars
+        if self.P > _lib.RVM_SMALA_MAX_PARAMS:
+            raise ValueError(f"SMALA supports at most {_lib.RVM_SMALA_MAX_PARAMS} free parameters")
         self.n = int(n_chains)
-        self.rel_step = rel_step
+        self.rel_step = float(rel_step)
+        self.seed = int(seed)
         self.device = torch.device(device) if device is not None else engine.default_device()
+        self.lib = _lib.load()
         self.pmap = self.state.param_map()
-        self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(int(seed))
+        self.floor = torch.as_tensor(fd_floor_vector(self.state), device=self.device)
+        _, _, er = engine.obs_arrays(obs)
+        self.inv_sigma2 = torch.as_tensor(1.0 / (er * er), device=self.device)
+        self.n_obs = len(er)
         if X0 is None:
             X0 = np.tile(self.state.get_params()[:, None], (1, self.n))
         self.X = torch.as_tensor(np.asarray(X0, dtype=np.float64), device=self.device).contiguous()
-        self.cache = self._derive(self.X)
-        self.accepted = torch.zeros(self.n, dtype=torch.int64, device=self.device)
-        self.linalg_failures = 0
+        S = 2 * self.P + 1
+        self.stencil = torch.empty((self.P, S * self.n), dtype=torch.float64, device=self.device)
+        self.Xs = torch.empty_like(self.X)
+        self.cache = self._new_cache()
+        self.prop = self._new_cache()
+        self.accepted = torch.zeros(self.n, dtype=torch.int32, device=self.device)
+        self.failures = torch.zeros(self.n, dtype=torch.int32, device=self.device)
         self.iteration = 0
+        self._derive_into(self.X, self.cache)
 
-    def _derive(self, X):
-        lp, g, H, st = fd_logp_grad_metric(self.state, self.obs, X, self.rel_step, self.pmap, hill_factor=1.0)
-        Ginv, L, logdet, ok = softabs_inv(H, self.alpha)
-        mu = X.t() + 0.5 * self.eps ** 2 * (Ginv @ g.t()[:, :, None])[:, :, 0]   # [C][P]
-        return dict(lp=lp, g=g, Ginv=Ginv, L=L, logdet=logdet, ok=ok & (st == 0), mu=mu)
+    def _new_cache(self):
+        torch = _torch()
+        P, C, dev = self.P, self.n, self.device
+        d = dict(lp=torch.empty(C, dtype=torch.float64, device=dev),
+                 grad=torch.empty((P, C), dtype=torch.float64, device=dev),
+                 mu=torch.empty((P, C), dtype=torch.float64, device=dev),
+                 L=torch.empty((P * P, C), dtype=torch.float64, device=dev),
+                 G=torch.empty((P * P, C), dtype=torch.float64, device=dev),
+                 logdet=torch.empty(C, dtype=torch.float64, device=dev),
+                 ok=torch.zeros(C, dtype=torch.int32, device=dev))
+        d["_c"] = _lib.SmalaCache(*[d[k].data_ptr() for k in ("lp", "grad", "mu", "L", "G", "logdet", "ok")])
+        return d
+
+    def _derive_into(self, X, cache):
+        st_h = _lib.stream_handle()
+        _lib.check(self.lib.rvm_fd_params(self.P, self.n, X.data_ptr(), self.rel_step, self.floor.data_ptr(),
+                                          self.stencil.data_ptr(), st_h), "rvm_fd_params")
+        lp, st, rv = self.state.get_logp_batch(self.obs, self.stencil, hill_factor=1.0, want_rv=True, pmap=self.pmap)
+        _lib.check(self.lib.rvm_smala_derive(self.P, self.n, self.n_obs, X.data_ptr(), self.rel_step,
+                                             self.floor.data_ptr(), lp.data_ptr(), st.data_ptr(), rv.data_ptr(),
+                                             self.inv_sigma2.data_ptr(), float(self.obs.Npoints), self.alpha,
+                                             self.eps, C.byref(cache["_c"]), st_h), "rvm_smala_derive")
+
+    @property
+    def linalg_failures(self):
+        return int(self.failures.sum().item())
 
     def step(self, z=None, u=None):
-        torch = _torch()
-        c = self.cache
-        if z is None:
-            z = torch.randn((self.n, self.P), generator=self.gen, device=self.device, dtype=torch.float64)
-        if u is None:
-            u = torch.rand(self.n, generator=self.gen, device=self.device, dtype=torch.float64)
-        Xs = c["mu"] + self.eps * (c["L"] @ z[:, :, None])[:, :, 0]               # [C][P]
-        Xs = torch.where(c["ok"][:, None], Xs, self.X.t())
-        cs = self._derive(Xs.t().contiguous())
-        q_ts_t = _mvn_logpdf(Xs, c["mu"], c["Ginv"], c["logdet"], self.eps)
-        q_t_ts = _mvn_logpdf(self.X.t(), cs["mu"], cs["Ginv"], cs["logdet"], self.eps)
-        ratio = torch.exp(cs["lp"] - c["lp"] + q_t_ts - q_ts_t)
-        acc = (ratio > u) & cs["ok"] & c["ok"] & torch.isfinite(cs["lp"])
-        self.linalg_failures += int((~cs["ok"] & torch.isfinite(cs["lp"])).sum().item())
-        self.X = torch.where(acc[None, :], Xs.t(), self.X).contiguous()
-        for k in c:
-            v, vs = c[k], cs[k]
-            m = acc.view(1, -1) if k == "g" else acc.view((-1,) + (1,) * (v.dim() - 1))
-            c[k] = torch.where(m, vs, v)
-        self.accepted += acc.long()
+        """One SMALA step of every chain; z [C][P] / u [C] inject the normals / uniforms."""
+        st_h = _lib.stream_handle()
+        zp = 0
+        if z is not None:
+            self._z = z.t().contiguous()
+            zp = self._z.data_ptr()
+        up = 0
+        if u is not None:
+            self._u = u.contiguous()
+            up = self._u.data_ptr()
+        _lib.check(self.lib.rvm_smala_propose(self.P, self.n, 0, self.X.data_ptr(), C.byref(self.cache["_c"]),
+                                              self.eps, self.seed, self.iteration, zp, self.Xs.data_ptr(), st_h),
+                   "rvm_smala_propose")
+        self._derive_into(self.Xs, self.prop)
+        _lib.check(self.lib.rvm_smala_accept(self.P, self.n, 0, self.X.data_ptr(), C.byref(self.cache["_c"]),
+                                             self.Xs.data_ptr(), C.byref(self.prop["_c"]), self.eps, self.seed,
+                                             self.iteration, up, self.accepted.data_ptr(), self.failures.data_ptr(),
+                                             st_h), "rvm_smala_accept")
         self.iteration += 1
-        return acc
 
 
 class Smala:

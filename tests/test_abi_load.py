@@ -18,7 +18,8 @@ def header_functions():
 def test_header_declares_expected_surface():
     fns = header_functions()
     for f in ("rvm_plan_create", "rvm_logl_batch", "rvm_stretch_propose", "rvm_stretch_accept",
-              "rvm_mh_propose", "rvm_mh_accept", "rvm_fd_params", "rvm_last_error", "rvm_abi_version"):
+              "rvm_mh_propose", "rvm_mh_accept", "rvm_fd_params", "rvm_smala_derive", "rvm_smala_propose",
+              "rvm_smala_accept", "rvm_last_error", "rvm_abi_version"):
         assert f in fns
 
 
@@ -43,3 +44,13 @@ def test_argument_errors_do_not_touch_the_device():
     rc = lib.rvm_plan_create(C.byref(cfg), z, z, z, 1, 64, C.byref(h))
     assert rc < 0 and b"n_planets" in lib.rvm_last_error()
     assert lib.rvm_logl_batch(None, 1, 0, 1.0, 0, 0, 0, 0) < 0
+
+
+def test_struct_layouts_match_header():
+    """ctypes mirrors of rvm_config / rvm_smala_cache have the C layouts (x86-64 SysV)."""
+    import ctypes as C
+
+    # int32 n_planets | pad | f64 dt | int32 n_levels | pad | f64 npoints | int32 mult[6] | f64 hint
+    assert C.sizeof(_lib.RvmConfig) == 64
+    assert _lib.RvmConfig.level_mult.offset == 32 and _lib.RvmConfig.period_hint.offset == 56
+    assert C.sizeof(_lib.SmalaCache) == 7 * 8

@@ -168,6 +168,92 @@ def test_smala_chains_run():
     assert int(sm.accepted.sum()) > 0
 
 
+def _smala_numpy(lp, g, H, x, alpha, eps):
+    """mcmc.py:135-150 restated in numpy for one chain: SoftAbs metric, G^-1, chol, drift."""
+    lam, Q = np.linalg.eigh(-0.5 * (H + H.T))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        lt = np.where(np.abs(alpha * lam) < 1e-8, 1.0 / alpha, lam / np.tanh(alpha * lam))
+    G = Q @ np.diag(lt) @ Q.T
+    Ginv = Q @ np.diag(1.0 / lt) @ Q.T
+    L = np.linalg.cholesky(Ginv)
+    mu = x + eps ** 2 * Ginv @ g / 2.0
+    return dict(G=G, Ginv=Ginv, L=L, mu=mu, logdet=float(np.sum(np.log(1.0 / lt))))
+
+
+def test_smala_derive_matches_numpy_softabs():
+    """rvm_smala_derive (Jacobi eigen-solver, SoftAbs, Cholesky, drift on device) vs numpy on the
+    gradient/Hessian of the same stencil launch (smala.fd_logp_grad_metric, torch)."""
+    torch = _torch()
+    from rvmcmc.smala import SmalaChains, fd_logp_grad_metric
+
+    s, obs = _state_and_obs()
+    C_, dim = 24, s.Nvars
+    rng = np.random.default_rng(4)
+    scales = np.array([S2_SCALES[k] for k in s.get_rawkeys()])
+    X0 = (s.get_params()[None] + 1e-3 * scales * rng.standard_normal((C_, dim))).T.copy()
+    sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=C_, X0=X0, seed=3)
+    X = torch.as_tensor(X0, device="cuda")
+    lp, g, H, st = fd_logp_grad_metric(sm.state, obs, X, sm.rel_step, sm.pmap, hill_factor=1.0)
+    lp, g, H = lp.cpu().numpy(), g.cpu().numpy(), H.cpu().numpy()
+    c = {k: v.cpu().numpy() for k, v in sm.cache.items() if k != "_c"}
+    np.testing.assert_array_equal(c["lp"], lp)
+    np.testing.assert_array_equal(c["grad"], g)
+    assert (c["ok"] == 1).all()
+    for i in range(C_):
+        ref = _smala_numpy(lp[i], g[:, i], H[:, :, i], X0[:, i], 1e3, 0.5)
+        G = c["G"][:, i].reshape(dim, dim)
+        L = c["L"][:, i].reshape(dim, dim)
+        np.testing.assert_allclose(G, ref["G"], rtol=1e-9, atol=1e-9 * np.abs(ref["G"]).max())
+        np.testing.assert_allclose(L @ L.T, ref["Ginv"], rtol=1e-9, atol=1e-9 * np.abs(ref["Ginv"]).max())
+        np.testing.assert_allclose(np.tril(L), L)
+        np.testing.assert_allclose(c["mu"][:, i], ref["mu"], rtol=1e-10, atol=1e-14)
+        assert abs(c["logdet"][i] - ref["logdet"]) < 1e-9 * max(1.0, abs(ref["logdet"]))
+
+
+def test_smala_step_matches_numpy_with_injected_draws():
+    """One device SMALA step with injected z and u == mcmc.py:167-187 restated in numpy on the
+    device's cached derivatives (proposal bit-close, decisions identical away from ties)."""
+    torch = _torch()
+    from rvmcmc.smala import SmalaChains
+
+    s, obs = _state_and_obs()
+    C_, dim, eps = 32, s.Nvars, 0.5
+    sm = SmalaChains(s, obs, eps=eps, alpha=1e3, n_chains=C_, seed=5)
+    for _ in range(2):
+        sm.step()
+    rng = np.random.default_rng(6)
+    z = rng.standard_normal((C_, dim))
+    u = rng.random(C_)
+    x0 = sm.X.cpu().numpy().copy()
+    c0 = {k: v.cpu().numpy().copy() for k, v in sm.cache.items() if k != "_c"}
+    acc0 = sm.accepted.cpu().numpy().copy()
+    sm.step(z=torch.as_tensor(z, device="cuda"), u=torch.as_tensor(u, device="cuda"))
+    xs = sm.Xs.cpu().numpy()
+    p = {k: v.cpu().numpy() for k, v in sm.prop.items() if k != "_c"}
+    near = 0
+    for i in range(C_):
+        L0 = c0["L"][:, i].reshape(dim, dim)
+        want = c0["mu"][:, i] + eps * L0 @ z[i] if c0["ok"][i] else x0[:, i]
+        np.testing.assert_allclose(xs[:, i], want, rtol=1e-13, atol=1e-16)
+
+        def logq(y, mu, G, logdet):
+            d = y - mu
+            return -0.5 * (d @ G @ d / eps ** 2 + dim * np.log(eps ** 2) + logdet + dim * np.log(2 * np.pi))
+
+        G0 = c0["G"][:, i].reshape(dim, dim)
+        Gp = p["G"][:, i].reshape(dim, dim)
+        lr = (p["lp"][i] - c0["lp"][i] + logq(x0[:, i], p["mu"][:, i], Gp, p["logdet"][i])
+              - logq(xs[:, i], c0["mu"][:, i], G0, c0["logdet"][i]))
+        acc = bool(np.exp(lr) > u[i]) and c0["ok"][i] == 1 and p["ok"][i] == 1 and np.isfinite(p["lp"][i])
+        if abs(lr - np.log(u[i])) < 1e-9:
+            near += 1
+            continue
+        got = sm.accepted.cpu().numpy()[i] - acc0[i] == 1
+        assert got == acc, (i, lr, np.log(u[i]))
+        np.testing.assert_array_equal(sm.X.cpu().numpy()[:, i], xs[:, i] if acc else x0[:, i])
+    assert near <= 1
+
+
 def test_device_philox_matches_restatement():
     """rvm_stretch_propose with the built-in Philox draws == tests/philox_ref.py restatement."""
     torch = _torch()
