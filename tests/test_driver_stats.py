@@ -1,0 +1,48 @@
+"""Chain statistics of rvmcmc.driver (driver.py:37-43 auto_correlation, :343-382 AC times,
+:412-414 efficacy) and the integrated-time / ESS estimator bench.py reports.  CPU only."""
+import datetime
+
+import numpy as np
+
+from rvmcmc import driver
+
+
+def _ar1(rho, n, walkers, seed=0):
+    rng = np.random.default_rng(seed)
+    x = np.zeros((n, walkers))
+    e = rng.standard_normal((n, walkers)) * np.sqrt(1 - rho * rho)
+    for i in range(1, n):
+        x[i] = rho * x[i - 1] + e[i]
+    return x
+
+
+def test_auto_correlation_matches_reference_definition():
+    x = np.random.default_rng(1).standard_normal(257)
+    r = driver.auto_correlation(x)
+    y = x - x.mean()
+    full = np.array([np.dot(y[: len(y) - k], y[k:]) for k in range(len(y))])  # np.correlate, lags >= 0
+    np.testing.assert_allclose(r, full / full[0], rtol=1e-12, atol=1e-15)
+    assert r[0] == 1.0
+
+
+def test_ac_time_is_first_lag_below_half():
+    rho = 0.9
+    x = _ar1(rho, 20000, 1, seed=2)[:, 0]
+    # theory: rho^k < 0.5  ->  k = ceil(ln 0.5 / ln rho) = 7
+    assert abs(driver.ac_time(x) - np.ceil(np.log(0.5) / np.log(rho))) <= 1
+
+
+def test_integrated_time_and_ess_on_ar1():
+    rho = 0.8
+    x = _ar1(rho, 4000, 64, seed=3)
+    tau = driver.integrated_time(x)
+    assert abs(tau - (1 + rho) / (1 - rho)) < 0.5          # tau_int = (1 + rho) / (1 - rho) = 9
+    ess, taus = driver.ess(np.stack([x, _ar1(0.5, 4000, 64, seed=4)], axis=2))
+    assert abs(taus[1] - 3.0) < 0.3 and ess[1] > ess[0]
+
+
+def test_efficacy_reference_formula():
+    t0 = datetime.datetime(2017, 1, 1)
+    clock = [t0, t0 + datetime.timedelta(seconds=1), t0 + datetime.timedelta(seconds=11)]
+    # driver.py:412-414: Niter / ((clock[-1] - clock[1]) * max(AC))
+    assert driver.efficacy(100, [2.0, 5.0], clock) == 100 / (10.0 * 5.0)
