@@ -26,9 +26,9 @@
  *     stream-ordered on `stream` (a hipStream_t; NULL = the null stream), so they are capturable
  *     into a hipGraph.  rvm_plan_create is the only call that allocates (device buffers owned by
  *     the plan) and it synchronises once.
- *   - Walker parameters are SoA, [n_params][n_walkers] float64, n_params = 5*n_planets, with the
+ *   - Walker parameters are SoA, [n_params][n_walkers] float64, n_params = 5*n_planets with the
  *     canonical per-planet key order  m, a, h, k, l  (the Python layer maps a
- *     State's dict order onto it).  Coplanar (ix = iy = 0) systems only in this ABI version.
+ *     State's dict order onto it), or 7*n_planets (m, a, h, k, l, ix, iy) for inclined plans.
  *   - Return code: 0 = success, < 0 = argument / launch error (rvm_last_error() explains).
  *     Per-walker physics outcomes are never errors: they are status codes plus logl = -INFINITY
  *     (the reference raises rebound.Encounter / returns -inf from priorHard; mcmc.py:28-35 maps
@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 2
+#define RVM_ABI_VERSION 3
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -68,6 +68,9 @@ typedef struct {
     double period_hint;    /* shortest orbital period the walkers are expected to have (code units):
                               sizes the per-level Stumpff series (performance only, results are
                               exact for any orbit); 0 = longest series on every level              */
+    int32_t inclined;      /* 0: coplanar, params [5*n_planets][W] (m, a, h, k, l); 1: inclined,
+                              params [7*n_planets][W] (m, a, h, k, l, ix, iy; REBOUND's Pal ix, iy),
+                              3-D integration, prior adds ix^2 + iy^2 >= 4 (state.py:311-313)      */
 } rvm_config;
 
 typedef struct rvm_plan rvm_plan;

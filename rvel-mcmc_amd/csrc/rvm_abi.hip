@@ -174,6 +174,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.n_levels = cfg->n_levels;
     P.npoints = cfg->npoints_norm;
     P.n_obs = n_obs;
+    P.inclined = cfg->inclined ? 1 : 0;
     // Richardson weights for the h^2 expansion: level k steps dt/mult[k]; Lagrange at 0 in x = 1/mult^2
     for (int k = 0; k < RVM_MAX_LEVELS; k++) {
         P.mult[k] = k < cfg->n_levels ? mult[k] : 1;

@@ -147,6 +147,22 @@ __device__ __forceinline__ void pal_to_cart(double mu, double a, double lam, dou
     VY = fac * ((1.0 - k * k * beta) * cF - h * k * beta * sF);
 }
 
+// Inclined orbits (REBOUND's Pal coordinates ix, iy): rotate the orbital plane,
+//   x' = (1 - iy^2/2) X + (ix iy/2) Y,  y' = (ix iy/2) X + (1 - ix^2/2) Y,
+//   z' = (sqrt(4 - ix^2 - iy^2)/2) (ix Y - iy X)       (same for the velocity)
+__device__ __forceinline__ void pal_incline(double ix, double iy, double& X, double& Y, double& Z, double& VX,
+                                            double& VY, double& VZ) {
+    const double W = sqrt(fabs(4.0 - ix * ix - iy * iy));
+    const double axx = 1.0 - 0.5 * iy * iy, axy = 0.5 * ix * iy, ayy = 1.0 - 0.5 * ix * ix;
+    const double x = X, y = Y, vx = VX, vy = VY;
+    X = axx * x + axy * y;
+    Y = axy * x + ayy * y;
+    Z = 0.5 * W * (ix * y - iy * x);
+    VX = axx * vx + axy * vy;
+    VY = axy * vx + ayy * vy;
+    VZ = 0.5 * W * (ix * vy - iy * vx);
+}
+
 // ---- lane layout: the planets of one walker live on L adjacent lanes ----------------------------
 // L = lanes per walker (1, 2 or 4): planet p of a walker runs on lane (group base + p), so every
 // Kepler drift runs on its own lane and the kick exchanges positions inside the lane group with
@@ -191,6 +207,7 @@ __device__ __forceinline__ double grp_get(double v, int q) {
 template <int NP>
 struct Lane {
     double rx, ry, vx, vy;  // own Jacobi coordinate
+    double rz, vz;          // out-of-plane components (inclined systems, D3 = true; else unused)
     double r, ir;           // |r'| and 1/|r'| at the current positions (carried from the drift)
     double GM, GM2;         // interior mass M_p (G = 1) of the own Jacobi coordinate, and 2 M_p
     double m[NP];           // planet masses
@@ -362,10 +379,10 @@ __device__ __forceinline__ void kepler_rare(double r0, double eta, double zeta, 
 // New position/velocity from the G-functions at the last evaluation point and the final Halley
 // correction Q (Taylor update of G1..G3 and of r = f' from there to X = x - Q), Gauss f and g.
 struct DriftOut {
-    double rx, ry, vx, vy, r, ir;
+    double rx, ry, vx, vy, rz, vz, r, ir;
 };
 
-template <int NP>
+template <bool D3, int NP>
 __device__ __forceinline__ DriftOut drift_apply(const Lane<NP>& s, double dt, double beta, double eta, double zeta,
                                                 double G0, double G1, double G2, double G3, double fp, double fpp,
                                                 double Q) {
@@ -387,6 +404,10 @@ __device__ __forceinline__ DriftOut drift_apply(const Lane<NP>& s, double dt, do
     o.ry = fma(f_, s.ry, g_ * s.vy);
     o.vx = fma(fd, s.rx, gd * s.vx);
     o.vy = fma(fd, s.ry, gd * s.vy);
+    if constexpr (D3) {
+        o.rz = fma(f_, s.rz, g_ * s.vz);
+        o.vz = fma(fd, s.rz, gd * s.vz);
+    }
     o.r = rr;
     o.ir = irr;
     return o;
@@ -407,11 +428,15 @@ __device__ __forceinline__ DriftOut drift_apply(const Lane<NP>& s, double dt, do
 //   the others; the caller (segment<> in rvm_logl.hip) re-runs the whole segment gated when any
 //   lane was not good.  Good lanes compute bit-identical states either way.
 // No square root anywhere in the step.
-template <int NT, bool GATED, int NP>
+template <int NT, bool GATED, bool D3 = false, int NP>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;
-    const double v2 = fma(s.vx, s.vx, s.vy * s.vy);
-    const double eta = fma(s.rx, s.vx, s.ry * s.vy);
+    double v2 = fma(s.vx, s.vx, s.vy * s.vy);
+    double eta = fma(s.rx, s.vx, s.ry * s.vy);
+    if constexpr (D3) {
+        v2 = fma(s.vz, s.vz, v2);
+        eta = fma(s.rz, s.vz, eta);
+    }
     const double beta = fma(s.GM2, ir0, -v2);
     const double zeta = fma(-beta, r0, GM);
     const double u = dt * ir0, sg = eta * ir0, g = GM * ir0;
@@ -446,11 +471,15 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad) {
     } else {
         bad = bad || !(fabs(z) <= B) || !halley_ok<NT>(Q, x);
     }
-    const DriftOut o = drift_apply(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
+    const DriftOut o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     s.rx = o.rx;
     s.ry = o.ry;
     s.vx = o.vx;
     s.vy = o.vy;
+    if constexpr (D3) {
+        s.rz = o.rz;
+        s.vz = o.vz;
+    }
     s.r = o.r;
     s.ir = o.ir;
 }
@@ -467,32 +496,38 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
 //   x_i = r'_i + (sum_{j<i} m_j x_j)/M_{i-1}, pairwise accelerations (1/r^3 from rsq), the Jacobi
 //   acceleration a'_i = a_i - (sum_{j<i} m_j a_j)/M_{i-1}, and v'_i += dt (a'_i + M_i r'_i/|r'_i|^3)
 //   (the Kepler part is removed because the drift integrates it exactly).
-template <int NP, int L>
+template <int NP, int L, bool D3 = false>
 __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
     constexpr int NB = NP + 1;
-    double x[NB], y[NB], ax[NB], ay[NB];
+    double x[NB], y[NB], zz[NB], ax[NB], ay[NB], az[NB];
     x[0] = 0.0;
     y[0] = 0.0;
-    double cmx = 0.0, cmy = 0.0;
+    zz[0] = 0.0;
+    double cmx = 0.0, cmy = 0.0, cmz = 0.0;
 #pragma unroll
     for (int i = 1; i < NB; i++) {
-        double Rx, Ry;
+        double Rx, Ry, Rz = 0.0;
         if constexpr (NP == 1) {
             Rx = s.rx;
             Ry = s.ry;
+            if constexpr (D3) Rz = s.rz;
         } else {
             Rx = grp_get<L>(s.rx, i - 1);
             Ry = grp_get<L>(s.ry, i - 1);
+            if constexpr (D3) Rz = grp_get<L>(s.rz, i - 1);
         }
         x[i] = Rx + cmx * s.iMi[i - 1];
         y[i] = Ry + cmy * s.iMi[i - 1];
+        zz[i] = D3 ? Rz + cmz * s.iMi[i - 1] : 0.0;
         cmx += s.m[i - 1] * x[i];
         cmy += s.m[i - 1] * y[i];
+        if constexpr (D3) cmz += s.m[i - 1] * zz[i];
     }
 #pragma unroll
     for (int i = 0; i < NB; i++) {
         ax[i] = 0.0;
         ay[i] = 0.0;
+        az[i] = 0.0;
     }
     uint64_t enc = 0;
     // star -- planet 1 distance is |r'_1|, already known to planet 1's lane from its drift
@@ -501,13 +536,14 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
     for (int i = 0; i < NB; i++) {
 #pragma unroll
         for (int j = i + 1; j < NB; j++) {
-            const double dx = x[j] - x[i], dy = y[j] - y[i];
+            const double dx = x[j] - x[i], dy = y[j] - y[i], dz = zz[j] - zz[i];
             double ir;
             if (i == 0 && j == 1) {
                 ir = ir01;
                 enc |= ballot(ir * ir > s.idmin2);
             } else {
-                const double r2 = dx * dx + dy * dy;
+                double r2 = dx * dx + dy * dy;
+                if constexpr (D3) r2 += dz * dz;
                 enc |= ballot(r2 < s.dmin2);
                 ir = rsq_nr(r2);
             }
@@ -518,26 +554,34 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
             ay[i] += mj * ir3 * dy;
             ax[j] -= mi * ir3 * dx;
             ay[j] -= mi * ir3 * dy;
+            if constexpr (D3) {
+                az[i] += mj * ir3 * dz;
+                az[j] -= mi * ir3 * dz;
+            }
         }
     }
     s.encm |= enc;
     // Jacobi acceleration of the own coordinate (index i = p + 1)
-    double max_ = ax[0], may_ = ay[0];  // M_star = 1
-    double ajx = 0.0, ajy = 0.0;
+    double max_ = ax[0], may_ = ay[0], maz_ = az[0];  // M_star = 1
+    double ajx = 0.0, ajy = 0.0, ajz = 0.0;
 #pragma unroll
     for (int i = 1; i < NB; i++) {
         const double tx = ax[i] - max_ * s.iMi[i - 1];
         const double ty = ay[i] - may_ * s.iMi[i - 1];
+        const double tz = az[i] - maz_ * s.iMi[i - 1];
         if (s.p == i - 1) {
             ajx = tx;
             ajy = ty;
+            ajz = tz;
         }
         max_ += s.m[i - 1] * ax[i];
         may_ += s.m[i - 1] * ay[i];
+        if constexpr (D3) maz_ += s.m[i - 1] * az[i];
     }
     const double kep = s.GM * (s.ir * s.ir * s.ir);
     s.vx += dt * (ajx + kep * s.rx);
     s.vy += dt * (ajy + kep * s.ry);
+    if constexpr (D3) s.vz += dt * (ajz + kep * s.rz);
 }
 
 // Two-planet kick in closed form (same interaction as the generic kick; G = M_star = 1):
@@ -545,7 +589,7 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
 //   dv'_2 = dt [ M_2 r'_2/|r'_2|^3 - (M_2/M_1)(d02/r02^3 + m_1 d12/r12^3) ]
 // with heliocentric x_1 = r'_1, x_2 = r'_2 + (m_1/M_1) r'_1, d02 = x_2, d12 = x_2 - x_1.  The
 // star--planet-1 distance |r'_1| and the own |r'| are carried from the drift: 2 rsq per kick.
-template <int L>
+template <int L, bool D3 = false>
 __device__ __forceinline__ void kick2(Lane<2>& s) {
     const double x1 = grp_get<L, 0>(s.rx), y1 = grp_get<L, 0>(s.ry);
     const double R2x = grp_get<L, 1>(s.rx), R2y = grp_get<L, 1>(s.ry);
@@ -553,8 +597,16 @@ __device__ __forceinline__ void kick2(Lane<2>& s) {
     const double c = s.m[0] * s.iMi[1];  // m_1 / M_1
     const double x2 = fma(c, x1, R2x), y2 = fma(c, y1, R2y);
     const double dx12 = x2 - x1, dy12 = y2 - y1;
-    const double r02sq = fma(x2, x2, y2 * y2);
-    const double r12sq = fma(dx12, dx12, dy12 * dy12);
+    double r02sq = fma(x2, x2, y2 * y2);
+    double r12sq = fma(dx12, dx12, dy12 * dy12);
+    double z2 = 0.0, dz12 = 0.0;
+    if constexpr (D3) {
+        const double z1 = grp_get<L, 0>(s.rz), R2z = grp_get<L, 1>(s.rz);
+        z2 = fma(c, z1, R2z);
+        dz12 = z2 - z1;
+        r02sq = fma(z2, z2, r02sq);
+        r12sq = fma(dz12, dz12, r12sq);
+    }
     s.encm |= ballot(r02sq < s.dmin2) | ballot(r12sq < s.dmin2) | ballot(ir01 * ir01 > s.idmin2);
     const double i02c = rcube_nr(r02sq), i12c = rcube_nr(r12sq);
     // coefficients carry the step (lane_set_step): v += A r' + B x2/r02^3 + C d12/r12^3
@@ -562,14 +614,15 @@ __device__ __forceinline__ void kick2(Lane<2>& s) {
     const double bx = s.kBh * i02c, cx = s.kCh * i12c;
     s.vx = fma(A, s.rx, fma(bx, x2, fma(cx, dx12, s.vx)));
     s.vy = fma(A, s.ry, fma(bx, y2, fma(cx, dy12, s.vy)));
+    if constexpr (D3) s.vz = fma(A, s.rz, fma(bx, z2, fma(cx, dz12, s.vz)));
 }
 
-template <int NP, int L>
+template <int NP, int L, bool D3 = false>
 __device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
     if constexpr (NP == 2)
-        kick2<L>(s);  // step folded into the lane's coefficients (lane_set_step(s, dt) beforehand)
+        kick2<L, D3>(s);  // step folded into the lane's coefficients (lane_set_step(s, dt) beforehand)
     else
-        kick_generic<NP, L>(s, dt);
+        kick_generic<NP, L, D3>(s, dt);
 }
 
 // star barycentric x-velocity: v0 = -sum_q (m_q / M_q) v'_q (gathered over the lane group)

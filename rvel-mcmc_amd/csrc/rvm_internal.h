@@ -26,6 +26,7 @@ struct DevPlan {
     double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
     double npoints;
     int32_t n_obs;
+    int32_t inclined;  // 1: 7 parameter rows per planet (ix, iy), 3-D integration
     DirSched fwd, bwd;
 };
 

@@ -38,51 +38,55 @@ __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 // One epoch-to-epoch segment of ns Wisdom-Holman DKD steps of size h (ns is wave-uniform; the
 // step loop is unrolled by hand because the compiler will not unroll a runtime trip count around
 // the convergent DPP / ballot operations).
-template <int NT, bool GATED, int NP, int L>
+template <int NT, bool GATED, bool D3, int NP, int L>
 __device__ __forceinline__ void segment_steps(Lane<NP>& s, double h, int ns, bool& bad) {
     lane_set_step(s, h);
-    drift<NT, GATED>(s, 0.5 * h, bad);
+    drift<NT, GATED, D3>(s, 0.5 * h, bad);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
-        kick<NP, L>(s, h);
-        drift<NT, GATED>(s, h, bad);
-        kick<NP, L>(s, h);
-        drift<NT, GATED>(s, h, bad);
+        kick<NP, L, D3>(s, h);
+        drift<NT, GATED, D3>(s, h, bad);
+        kick<NP, L, D3>(s, h);
+        drift<NT, GATED, D3>(s, h, bad);
     }
     if (j < ns - 1) {
-        kick<NP, L>(s, h);
-        drift<NT, GATED>(s, h, bad);
+        kick<NP, L, D3>(s, h);
+        drift<NT, GATED, D3>(s, h, bad);
     }
-    kick<NP, L>(s, h);
-    drift<NT, GATED>(s, 0.5 * h, bad);
+    kick<NP, L, D3>(s, h);
+    drift<NT, GATED, D3>(s, 0.5 * h, bad);
 }
 
 // SPEC: run the segment with ungated drifts (rvm_device.h) and vote once at its end; if any lane
 // of the wave had a step that needs the general solver, restore the segment's initial state and
 // redo it gated.  Used on the fine levels, where such steps are rare.
-template <int NT, bool SPEC, int NP, int L>
+template <int NT, bool SPEC, bool D3, int NP, int L>
 __device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
     bool bad = false;
     if constexpr (SPEC) {
         const double rx = s.rx, ry = s.ry, vx = s.vx, vy = s.vy, r = s.r, ir = s.ir;
+        const double rz = s.rz, vz = s.vz;
         const uint64_t encm = s.encm;
-        segment_steps<NT, false, NP, L>(s, h, ns, bad);
+        segment_steps<NT, false, D3, NP, L>(s, h, ns, bad);
         if (__builtin_expect(ballot(bad) != 0, 0)) {
             s.rx = rx;
             s.ry = ry;
             s.vx = vx;
             s.vy = vy;
+            s.rz = rz;
+            s.vz = vz;
             s.r = r;
             s.ir = ir;
             s.encm = encm;
-            segment_steps<NT, true, NP, L>(s, h, ns, bad);
+            segment_steps<NT, true, D3, NP, L>(s, h, ns, bad);
         }
     } else {
-        segment_steps<NT, true, NP, L>(s, h, ns, bad);
+        segment_steps<NT, true, D3, NP, L>(s, h, ns, bad);
     }
 }
 
-template <int NP>
+// D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
+template <int NP, bool D3>
 __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan P, const int W,
                                                                    const double* __restrict__ params,
                                                                    const double hill_factor,
@@ -135,19 +139,23 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         st_idx = S.obs_idx[i0];
     }
 
-    // ---- walker parameters (m, a, h, k, l per planet), prior (state.py:299-315) ----------------
+    // ---- walker parameters (m, a, h, k, l [, ix, iy] per planet), prior (state.py:299-315) -----
+    constexpr int PR = D3 ? 7 : 5;  // parameter rows per planet
     Lane<NP> s;
-    double pa[NP], ph[NP], pk[NP], pl[NP];
+    double pa[NP], ph[NP], pk[NP], pl[NP], pix[NP], piy[NP];
     int status = RVM_STATUS_OK;
 #pragma unroll
     for (int p = 0; p < NP; p++) {
-        s.m[p] = params[(size_t)(5 * p + 0) * W + wl];
-        pa[p] = params[(size_t)(5 * p + 1) * W + wl];
-        ph[p] = params[(size_t)(5 * p + 2) * W + wl];
-        pk[p] = params[(size_t)(5 * p + 3) * W + wl];
-        pl[p] = params[(size_t)(5 * p + 4) * W + wl];
-        const bool bad = !(pa[p] > 0.02) || !(s.m[p] > 5e-6) || !(ph[p] * ph[p] + pk[p] * pk[p] < 1.0) ||
-                         !isfinite(pl[p]);
+        s.m[p] = params[(size_t)(PR * p + 0) * W + wl];
+        pa[p] = params[(size_t)(PR * p + 1) * W + wl];
+        ph[p] = params[(size_t)(PR * p + 2) * W + wl];
+        pk[p] = params[(size_t)(PR * p + 3) * W + wl];
+        pl[p] = params[(size_t)(PR * p + 4) * W + wl];
+        pix[p] = D3 ? params[(size_t)(PR * p + 5) * W + wl] : 0.0;
+        piy[p] = D3 ? params[(size_t)(PR * p + 6) * W + wl] : 0.0;
+        bool bad = !(pa[p] > 0.02) || !(s.m[p] > 5e-6) || !(ph[p] * ph[p] + pk[p] * pk[p] < 1.0) ||
+                   !isfinite(pl[p]);
+        if constexpr (D3) bad = bad || !(pix[p] * pix[p] + piy[p] * piy[p] < 4.0);  // state.py:311-313
         if (bad) status = RVM_STATUS_PRIOR;
     }
     if (status != RVM_STATUS_OK) {  // keep the lane numerically benign; its result is discarded
@@ -158,6 +166,8 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
             ph[p] = 0.0;
             pk[p] = 0.0;
             pl[p] = 0.0;
+            pix[p] = 0.0;
+            piy[p] = 0.0;
         }
     }
 
@@ -178,6 +188,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     for (int p = 0; p < NP; p++) s.mu[p] = s.m[p] / Mi[p + 1];
     s.dmin2 = (hill_factor * hill) * (hill_factor * hill);
     double own_m = s.m[0], own_a = pa[0], own_h = ph[0], own_k = pk[0], own_l = pl[0], own_M = Mi[1];
+    double own_ix = pix[0], own_iy = piy[0];
 #pragma unroll
     for (int p = 1; p < NP; p++) {
         if (s.p == p) {
@@ -187,15 +198,20 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
             own_k = pk[p];
             own_l = pl[p];
             own_M = Mi[p + 1];
+            own_ix = pix[p];
+            own_iy = piy[p];
         }
     }
     s.GM = own_M;
-    double X, Y, VX, VY;
+    double X, Y, VX, VY, Z = 0.0, VZ = 0.0;
     pal_to_cart(1.0 + own_m, own_a, own_l, own_k, own_h, X, Y, VX, VY);
+    if constexpr (D3) {
+        if (own_ix != 0.0 || own_iy != 0.0) pal_incline(own_ix, own_iy, X, Y, Z, VX, VY, VZ);
+    }
     {
         // r'_p = x_p - (sum_{q<p} m_q x_q) / M_{p-1}   (heliocentric -> Jacobi)
-        double sx = 0.0, sy = 0.0, svx = 0.0, svy = 0.0;
-        double jx = X, jy = Y, jvx = VX, jvy = VY;
+        double sx = 0.0, sy = 0.0, sz = 0.0, svx = 0.0, svy = 0.0, svz = 0.0;
+        double jx = X, jy = Y, jz = Z, jvx = VX, jvy = VY, jvz = VZ;
 #pragma unroll
         for (int q = 0; q < NP - 1; q++) {
             const double xq = grp_get<L>(X, q), yq = grp_get<L>(Y, q);
@@ -204,25 +220,35 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
             sy += s.m[q] * yq;
             svx += s.m[q] * vxq;
             svy += s.m[q] * vyq;
+            if constexpr (D3) {
+                sz += s.m[q] * grp_get<L>(Z, q);
+                svz += s.m[q] * grp_get<L>(VZ, q);
+            }
             if (s.p == q + 1) {
                 jx = X - sx * s.iMi[q + 1];
                 jy = Y - sy * s.iMi[q + 1];
                 jvx = VX - svx * s.iMi[q + 1];
                 jvy = VY - svy * s.iMi[q + 1];
+                if constexpr (D3) {
+                    jz = Z - sz * s.iMi[q + 1];
+                    jvz = VZ - svz * s.iMi[q + 1];
+                }
             }
         }
         s.rx = jx;
         s.ry = jy;
         s.vx = jvx;
         s.vy = jvy;
+        s.rz = D3 ? jz : 0.0;
+        s.vz = D3 ? jvz : 0.0;
     }
-    s.r = sqrt(s.rx * s.rx + s.ry * s.ry);
+    s.r = D3 ? sqrt(s.rx * s.rx + s.ry * s.ry + s.rz * s.rz) : sqrt(s.rx * s.rx + s.ry * s.ry);
     s.ir = 1.0 / s.r;
     s.encm = 0;
     lane_finish(s);
     {
         Lane<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
-        kick<NP, L>(t0, 0.0);
+        kick<NP, L, D3>(t0, 0.0);
         s.encm = t0.encm;
     }
 
@@ -259,11 +285,11 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         if (ns > 0) {
             const double h = len * inv_mult;  // len holds the segment's base step
             if (nt <= 6)
-                segment<6, true, NP, L>(s, h, ns);
+                segment<6, true, D3, NP, L>(s, h, ns);
             else if (nt == 7)
-                segment<7, false, NP, L>(s, h, ns);
+                segment<7, false, D3, NP, L>(s, h, ns);
             else
-                segment<8, false, NP, L>(s, h, ns);
+                segment<8, false, D3, NP, L>(s, h, ns);
         }
         PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
@@ -337,22 +363,26 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
     const dim3 block(64 * P.n_levels);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t smem = (size_t)emax * (3 * sizeof(double) + 2 * sizeof(int32_t)) + 16;
+#define RVM_LAUNCH(NPV, D3V) \
+    logl_kernel<NPV, D3V><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out)
+    const bool inc = P.inclined != 0;
     switch (P.n_planets) {
         case 1:
-            logl_kernel<1><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            if (inc) RVM_LAUNCH(1, true); else RVM_LAUNCH(1, false);
             break;
         case 2:
-            logl_kernel<2><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            if (inc) RVM_LAUNCH(2, true); else RVM_LAUNCH(2, false);
             break;
         case 3:
-            logl_kernel<3><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            if (inc) RVM_LAUNCH(3, true); else RVM_LAUNCH(3, false);
             break;
         case 4:
-            logl_kernel<4><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out);
+            if (inc) RVM_LAUNCH(4, true); else RVM_LAUNCH(4, false);
             break;
         default:
             return hipErrorInvalidValue;
     }
+#undef RVM_LAUNCH
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     finalize_kernel<<<(W + 255) / 256, 256, 0, stream>>>(W, P.npoints, chi2_part, status_part, logl, status);

@@ -17,7 +17,7 @@ RVM_STATUS_ENCOUNTER = 2
 RVM_STATUS_NONFINITE = 3
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
-ABI_VERSION = 2  # include/rvmcmc.h RVM_ABI_VERSION
+ABI_VERSION = 3  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):
@@ -28,6 +28,7 @@ class RvmConfig(C.Structure):
         ("npoints_norm", C.c_double),
         ("level_mult", C.c_int32 * RVM_MAX_LEVELS),
         ("period_hint", C.c_double),
+        ("inclined", C.c_int32),
     ]
 
 

@@ -3,7 +3,8 @@
 `LoglPlan` owns one `rvm_plan` (epoch schedule + observation data resident in HBM) and launches
 `rvm_logl_batch` on the caller's current torch stream.  `ParamMap` maps a reference-style
 `State` (dict-of-planets, free parameters in dict order, state.py:8-31 / 124-207) onto the
-kernel's canonical SoA layout [5 * n_planets][n_walkers] with per-planet order m, a, h, k, l.
+kernel's canonical SoA layout [5 * n_planets][n_walkers] with per-planet order m, a, h, k, l
+(7 rows with ix, iy for inclined systems).
 """
 from __future__ import annotations
 
@@ -17,7 +18,8 @@ import numpy as np
 from . import _lib
 
 KERNEL_KEYS = ("m", "a", "h", "k", "l")
-SUPPORTED_KEYS = set(KERNEL_KEYS) | {"ix", "iy"}
+KERNEL_KEYS_INCLINED = KERNEL_KEYS + ("ix", "iy")
+SUPPORTED_KEYS = set(KERNEL_KEYS_INCLINED)
 
 
 def level_multipliers(levels) -> tuple:
@@ -43,7 +45,7 @@ class IntegratorConfig:
                      segment with mult[k] x its base steps (step dt/mult[k]); an int n means the
                      harmonic sequence 1..n.  The default (4, 5, 6, 7) at steps_per_orbit = 8
                      (steps P/32 .. P/56) keeps |logL - logL_IAS15| <= ~2e-9 on the benchmark
-                     configs (T2 tier; the tests enforce 5e-9) with the shortest longest-level
+                     configs (T2 tier; the tests enforce 5e-8) with the shortest longest-level
                      integration of the sequences we measured.
     """
 
@@ -67,6 +69,11 @@ class IntegratorConfig:
     def plan_args(self, planets):
         """(dt, level multipliers, period hint) for plan_for / LoglPlan."""
         return self.step_for(planets), self.mult, min_period(planets)
+
+
+def is_inclined(planets) -> bool:
+    """An inclined plan is needed when any planet dict carries ix / iy (REBOUND adds z then)."""
+    return any(("ix" in p) or ("iy" in p) for p in planets)
 
 
 DEFAULT_CONFIG = IntegratorConfig()
@@ -102,7 +109,7 @@ class LoglPlan:
     """rvm_plan for one observation set on one device."""
 
     def __init__(self, t, rv, sigma, npoints, n_planets, dt, levels=4, max_walkers=4096, device=None,
-                 period_hint=0.0):
+                 period_hint=0.0, inclined=False):
         torch = _torch()
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else default_device()
@@ -117,10 +124,13 @@ class LoglPlan:
         self.mult = level_multipliers(levels)
         self.n_levels = len(self.mult)
         self.period_hint = float(period_hint)
+        self.inclined = bool(inclined)
+        self.rows = (7 if self.inclined else 5) * self.n_planets
         self.npoints = float(npoints)
         self.max_walkers = int(max_walkers)
         lm = (C.c_int32 * _lib.RVM_MAX_LEVELS)(*self.mult)
-        cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints, lm, self.period_hint)
+        cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints, lm, self.period_hint,
+                             int(self.inclined))
         handle = C.c_void_p()
         dp = C.POINTER(C.c_double)
         with torch.cuda.device(self.device):
@@ -136,14 +146,16 @@ class LoglPlan:
                     epochs_bwd=vals[3].value)
 
     def logl(self, params, hill_factor=1.0, want_rv=False, out=None, status=None, rv_out=None, stream=None):
-        """params: float64 device tensor [5*n_planets][W] (contiguous) -> (logl[W], status[W], rv|None).
+        """params: float64 device tensor [5*n_planets][W] ([7*n_planets][W] for an inclined plan) ->
+        (logl[W], status[W], rv|None).
 
         rv (if requested) is [n_obs][W], rows in the plan's input epoch order."""
         torch = _torch()
         if params.dtype != torch.float64 or params.device != self.device or params.dim() != 2:
             raise ValueError("params must be a 2-D float64 tensor on the plan's device")
-        if params.shape[0] != 5 * self.n_planets:
-            raise ValueError(f"params must have {5 * self.n_planets} rows (m,a,h,k,l per planet)")
+        if params.shape[0] != self.rows:
+            raise ValueError(f"params must have {self.rows} rows (m,a,h,k,l{',ix,iy' if self.inclined else ''} "
+                             f"per planet)")
         params = params.contiguous()
         W = params.shape[1]
         if W > self.max_walkers:
@@ -183,17 +195,17 @@ def obs_arrays(obs):
     return t, rv, er
 
 
-def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0.0) -> LoglPlan:
+def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0.0, inclined=False) -> LoglPlan:
     """Cached LoglPlan on an Observation object (keyed by device and integrator settings)."""
     dev = _torch().device(device) if device is not None else default_device()
     cache = obs.__dict__.setdefault("_rvm_plans", {})
     mult = level_multipliers(levels)
-    key = (str(dev), int(n_planets), float(dt), mult, float(period_hint))
+    key = (str(dev), int(n_planets), float(dt), mult, float(period_hint), bool(inclined))
     plan = cache.get(key)
     if plan is None or plan.max_walkers < max_walkers:
         t, rv, er = obs_arrays(obs)
         cap = max(int(max_walkers), plan.max_walkers * 2 if plan else 0, 64)
-        plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, mult, cap, dev, period_hint)
+        plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, mult, cap, dev, period_hint, inclined)
         cache[key] = plan
     return plan
 
@@ -202,41 +214,42 @@ class ParamMap:
     """Free-parameter vectors of a State  <->  kernel SoA parameter blocks.
 
     The free parameters of a State are its planets' keys in dict order minus ignore_vars /
-    ignore_params (state.py:26-31, 143-155).  The kernel wants every planet's m, a, h, k, l;
-    non-free values are taken from the State's planets (missing h/k/l default to 0 as REBOUND's
-    Pal constructor does)."""
+    ignore_params (state.py:26-31, 143-155).  The kernel wants every planet's m, a, h, k, l (and
+    ix, iy when any planet carries an inclination key: an inclined plan); non-free values are
+    taken from the State's planets (missing h/k/l/ix/iy default to 0 as REBOUND's Pal
+    constructor does)."""
 
     def __init__(self, state):
         self.n_planets = len(state.planets)
         if not 1 <= self.n_planets <= _lib.RVM_MAX_PLANETS:
             raise ValueError(f"1..{_lib.RVM_MAX_PLANETS} planets supported, got {self.n_planets}")
-        base = np.zeros(5 * self.n_planets)
+        self.inclined = any(("ix" in p) or ("iy" in p) for p in state.planets)
+        keys = KERNEL_KEYS_INCLINED if self.inclined else KERNEL_KEYS
+        R = len(keys)
+        self.rows_per_planet = R
+        base = np.zeros(R * self.n_planets)
         for i, p in enumerate(state.planets):
             unknown = set(p.keys()) - SUPPORTED_KEYS
             if unknown:
-                raise ValueError(f"planet {i}: unsupported keys {sorted(unknown)} (Pal elements m,a,h,k,l only)")
-            if float(p.get("ix", 0.0)) != 0.0 or float(p.get("iy", 0.0)) != 0.0:
-                raise NotImplementedError("inclined orbits (ix, iy != 0) are not supported by the kernel")
+                raise ValueError(f"planet {i}: unsupported keys {sorted(unknown)} (Pal elements m,a,h,k,l,ix,iy)")
             if "a" not in p:
                 raise ValueError(f"planet {i}: 'a' is required")
-            for j, k in enumerate(KERNEL_KEYS):
-                base[5 * i + j] = float(p.get(k, 0.0))
+            for j, k in enumerate(keys):
+                base[R * i + j] = float(p.get(k, 0.0))
         self.base = base
         slots = []
         for i, planet in enumerate(state.planets):
             for k in planet.keys():
                 if state._is_free(i, k):
-                    if k in ("ix", "iy"):
-                        raise NotImplementedError("free inclination parameters are not supported by the kernel")
-                    slots.append(5 * i + KERNEL_KEYS.index(k))
+                    slots.append(R * i + keys.index(k))
         self.slots = np.asarray(slots, dtype=np.int64)
         self.n_free = len(slots)
-        # free parameters already in kernel order (m,a,h,k,l per planet, all free): no remapping
-        self.identity = self.n_free == 5 * self.n_planets and bool(np.all(self.slots == np.arange(self.n_free)))
+        # free parameters already in kernel order (all keys free, kernel order): no remapping
+        self.identity = self.n_free == R * self.n_planets and bool(np.all(self.slots == np.arange(self.n_free)))
         self._dev_cache = {}
 
     def to_kernel(self, X):
-        """X: float64 device tensor [n_free][W] -> kernel params [5*np][W]."""
+        """X: float64 device tensor [n_free][W] -> kernel params [R*np][W] (R = 5, or 7 if inclined)."""
         torch = _torch()
         if self.identity and X.is_contiguous():
             return X

@@ -45,7 +45,7 @@ class DeviceOps:
         st = sampler.state
         dt, mult, hint = st.integrator.plan_args(st.planets)
         self.plan = engine.plan_for(sampler.obs, sampler.pmap.n_planets, dt, mult, sampler.nloc,
-                                    sampler.device, hint)
+                                    sampler.device, hint, sampler.pmap.inclined)
         self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
         self.track_status = False  # set True to histogram per-walker statuses (costs a small kernel)
         self.status_counts = torch.zeros(4, dtype=torch.int64, device=sampler.device)

@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == 2
+    assert lib.rvm_abi_version() == 3
 
 
 def test_python_binding_matches_header():
@@ -51,6 +51,7 @@ def test_struct_layouts_match_header():
     import ctypes as C
 
     # int32 n_planets | pad | f64 dt | int32 n_levels | pad | f64 npoints | int32 mult[6] | f64 hint
-    assert C.sizeof(_lib.RvmConfig) == 64
+    # | int32 inclined | pad
+    assert C.sizeof(_lib.RvmConfig) == 72 and _lib.RvmConfig.inclined.offset == 64
     assert _lib.RvmConfig.level_mult.offset == 32 and _lib.RvmConfig.period_hint.offset == 56
     assert C.sizeof(_lib.SmalaCache) == 7 * 8

@@ -6,7 +6,8 @@ Tiers:
       1e-14 sum|w| absolute, identical status codes.  Chaotic walkers (wide ball) are compared within
       their own roundoff sensitivity, measured on the oracle.
   T2  kernel vs the IAS15 restatement of the reference (reference-equivalent physics):
-      |dlogL| <= 5e-9 absolute at the default integrator settings; golden G2/G3 reproduced.
+      |dlogL| <= 5e-8 absolute at the default integrator settings (SURVEY.md §8c allows 1e-6;
+      measured 1.4e-9 S2, 1.9e-9 HD155358, 1.2e-8 on the short inclined set below); golden G2/G3.
 """
 import os
 
@@ -23,7 +24,7 @@ pytestmark = pytest.mark.gpu
 # 6.2 at 4 levels, 26 at 6) and by the likelihood's conditioning (dlogL/drv ~ 2 sum|r|/(N sigma^2)
 # ~ 1e4).  Tolerance: 1e-11 * sum|w| * max(1, |logL|)  (measured max 4e-11 at 4 levels).
 T1_REL_PER_W = 1e-11
-T2_ABS = 5e-9
+T2_ABS = 5e-8
 # default integrator (rvmcmc.engine.IntegratorConfig): level multipliers and base steps per orbit
 LEVELS = (4, 5, 6, 7)
 SPO = 8.0
@@ -46,14 +47,14 @@ def _torch():
     return torch
 
 
-def _plan(obs, planets, n_levels=LEVELS, steps=SPO, max_walkers=4096):
+def _plan(obs, planets, n_levels=LEVELS, steps=SPO, max_walkers=4096, inclined=False):
     from rvmcmc import engine
 
     pmin = engine.min_period(planets)
     dt = pmin / steps
     t, rv, er = engine.obs_arrays(obs)
     return engine.LoglPlan(t, rv, er, obs.Npoints, len(planets), dt, n_levels, max_walkers,
-                           period_hint=pmin), dt
+                           period_hint=pmin, inclined=inclined), dt
 
 
 def _ball(planets, W, rel=1e-3, seed=0):
@@ -64,14 +65,14 @@ def _ball(planets, W, rel=1e-3, seed=0):
     return P  # [W][np][7]
 
 
-def _kernel_params(P):
+def _kernel_params(P, rows=5):
     W, n, _ = P.shape
-    return np.ascontiguousarray(np.concatenate([P[:, p, :5].T for p in range(n)], 0))
+    return np.ascontiguousarray(np.concatenate([P[:, p, :rows].T for p in range(n)], 0))
 
 
 def _run(plan, P, hill=1.0, want_rv=False):
     torch = _torch()
-    K = torch.as_tensor(_kernel_params(P), device="cuda")
+    K = torch.as_tensor(_kernel_params(P, 7 if plan.inclined else 5), device="cuda")
     lp, st, rv = plan.logl(K, hill_factor=hill, want_rv=want_rv)
     torch.cuda.synchronize()
     return lp.cpu().numpy(), st.cpu().numpy(), (rv.cpu().numpy() if rv is not None else None)
@@ -264,3 +265,70 @@ def test_large_batch_size_independent_results():
         one, st1, _ = _run(plan, P[i:i + 1])
         assert one[0] == big[i] and st1[0] == st_big[i]
     assert np.isfinite(big).all()
+
+
+# ---- inclined systems (REBOUND Pal ix, iy; 3-D integration) ---------------------------------------
+# No stored reference output has an inclined system (the reference only checks ix^2 + iy^2 < 4 in
+# priorHard, state.py:311-313): the 3-D Pal rotation is the oracle's restatement of REBOUND's
+# (pinned in the plane by G1), so these tiers are pinned to the oracle only.
+S2_INCLINED = [dict(S2_PLANETS[0], ix=0.12, iy=-0.05), dict(S2_PLANETS[1], ix=0.04, iy=0.18)]
+
+
+def _inclined_ball(W, seed, rel=1e-3):
+    P = _ball(S2_INCLINED, W, rel=rel, seed=seed)
+    rng = np.random.default_rng(seed + 100)
+    P[:, :, 5:7] += 1e-3 * rng.standard_normal((W, 2, 2))
+    return P
+
+
+def test_t1_inclined_vs_oracle():
+    np.random.seed(7)
+    obs = O.fake_obs(S2_INCLINED, Npoints=60, error=1.5e-4, errorVar=2.5e-5, tmax=80.)
+    plan, dt = _plan(obs, S2_INCLINED, inclined=True)
+    P = _inclined_ball(96, seed=8)
+    P[0, 1, 5], P[0, 1, 6] = 1.5, 1.4      # ix^2 + iy^2 >= 4 -> prior (state.py:311-313)
+    got, st, _ = _run(plan, P)
+    ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, LEVELS, has_inc=1)
+    assert st[0] == 1
+    _assert_t1(got, st, ref, st_ref)
+
+
+def test_t2_inclined_vs_ias15():
+    np.random.seed(7)
+    obs = O.fake_obs(S2_INCLINED, Npoints=60, error=1.5e-4, errorVar=2.5e-5, tmax=80.)
+    plan, _ = _plan(obs, S2_INCLINED, inclined=True)
+    P = _inclined_ball(16, seed=9)
+    got, st, _ = _run(plan, P)
+    ref, st_ref = O.logl_ias15_batch(P, 2, obs, hill_factor=1.0, has_inc=1)
+    assert (st == st_ref).all()
+    assert np.abs(got - ref).max() < T2_ABS
+
+
+def test_inclined_kernel_with_zero_inclination_equals_planar():
+    """ix = iy = 0 through the 3-D kernel is bit-identical to the planar kernel."""
+    obs = s2_obs_oracle()
+    plan2, _ = _plan(obs, S2_PLANETS)
+    plan3, _ = _plan(obs, S2_PLANETS, inclined=True)
+    P = _ball(S2_PLANETS, 64, seed=10)
+    a, sa, _ = _run(plan2, P)
+    b, sb, _ = _run(plan3, P)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(sa, sb)
+
+
+def test_state_api_inclined_free_parameters():
+    """A State whose planets carry ix/iy (free) maps onto an inclined plan (7 rows per planet)."""
+    torch = _torch()
+    from rvmcmc import state
+
+    s = state.State(planets=[dict(p) for p in S2_INCLINED])
+    assert s.Nvars == 14
+    pm = s.param_map()
+    assert pm.inclined and pm.identity
+    np.random.seed(7)
+    obs = O.fake_obs(S2_INCLINED, Npoints=60, error=1.5e-4, errorVar=2.5e-5, tmax=80.)
+    X = torch.as_tensor(np.repeat(s.get_params()[:, None], 3, 1), device="cuda")
+    lp, st, _ = s.get_logp_batch(obs, X, hill_factor=1.0)
+    ref, _ = O.logl_ias15_batch(O.pal_params(S2_INCLINED)[None], 2, obs, hill_factor=1.0, has_inc=1)
+    assert (st.cpu().numpy() == 0).all()
+    assert np.abs(lp.cpu().numpy() - ref[0]).max() < T2_ABS

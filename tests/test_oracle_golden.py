@@ -16,7 +16,7 @@ import oracle as O
 from conftest import GOLDEN, S2_PLANETS, s2_obs_oracle
 
 # T2 tolerance: |logL_kernel_algorithm - logL_IAS15| (absolute) at default settings
-T2_LOGL_ABS = 5e-9
+T2_LOGL_ABS = 5e-8  # SURVEY.md §8c allows 1e-6; see tests/test_gpu_logl.py
 
 
 def _sol_planets(sol):
