@@ -51,15 +51,31 @@ __device__ __forceinline__ double fma_sk(double a, double b, double k) {
     return r;
 }
 
+// A constant materialised once into a VGPR (opaque to the compiler, so it is not re-materialised
+// with a v_mov inside the loops that use it as the second operand of fma_sk).
+__device__ __forceinline__ double vconst(double k) {
+    double r;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(r) : "s"(k));
+    return r;
+}
+
+// Loop-invariant VGPR constants of the hot path (set once per segment, vconsts_for<NT>).
+struct VConsts {
+    double k2, k3;  // top Horner coefficients of c2, c3 for the level's series length
+    double c1875;   // 15/8 of rcube_nr
+};
+
 // x^(-3/2) straight from v_rsq_f64: with y = rsq(x), e = 1 - x y^2,
 //   x^(-3/2) = y^3 (1 - e)^(-3/2) = y^3 (1 + 3e/2 + 15e^2/8 + O(e^3))      (|e| ~ 5e-8)
-__device__ __forceinline__ double rcube_nr(double x) {
+__device__ __forceinline__ double rcube_nr(double x, double c1875) {
     const double y = __builtin_amdgcn_rsq(x);
     const double y2 = y * y;
     const double y3 = y2 * y;
     const double e = fma(-x, y2, 1.0);
-    return fma(y3, e * fma_sk(e, 1.875, 1.5), y3);
+    return fma(y3, e * fma_sk(e, c1875, 1.5), y3);
 }
+
+__device__ __forceinline__ double rcube_nr(double x) { return rcube_nr(x, 1.875); }
 
 // ---- Stumpff functions (Danby) ------------------------------------------------------------------
 // c2 = sum_j (-z)^j / (2j+2)!,  c3 = sum_j (-z)^j / (2j+3)!;  c1 = 1 - z c3,  c0 = 1 - z c2.
@@ -73,6 +89,33 @@ __device__ __forceinline__ double rcube_nr(double x) {
 template <int NT>
 __device__ __forceinline__ constexpr double stumpff_bound() {
     return NT >= 8 ? 0.3 : (NT == 7 ? 0.12 : 0.04);
+}
+
+struct StumpffK {
+    static constexpr double K2[9] = {1.0 / 2.0,         -1.0 / 24.0,           1.0 / 720.0,
+                                     -1.0 / 40320.0,    1.0 / 3628800.0,       -1.0 / 479001600.0,
+                                     1.0 / 87178291200.0, -1.0 / 20922789888000.0, 1.0 / 6402373705728000.0};
+    static constexpr double K3[9] = {1.0 / 6.0,           -1.0 / 120.0,           1.0 / 5040.0,
+                                     -1.0 / 362880.0,     1.0 / 39916800.0,       -1.0 / 6227020800.0,
+                                     1.0 / 1307674368000.0, -1.0 / 355687428096000.0, 1.0 / 121645100408832000.0};
+};
+
+template <int NT>
+__device__ __forceinline__ VConsts vconsts_for() {
+    return VConsts{vconst(StumpffK::K2[NT - 1]), vconst(StumpffK::K3[NT - 1]), vconst(1.875)};
+}
+
+// with the top coefficients k2 = K2[NT-1], k3 = K3[NT-1] already in VGPRs (vconsts_for<NT>)
+template <int NT>
+__device__ __forceinline__ void stumpff23(double z, double& c2, double& c3, double k2, double k3) {
+    double a = fma_sk(z, k2, StumpffK::K2[NT - 2]), b = fma_sk(z, k3, StumpffK::K3[NT - 2]);
+#pragma unroll
+    for (int j = NT - 3; j >= 0; j--) {
+        a = fma_sk(a, z, StumpffK::K2[j]);
+        b = fma_sk(b, z, StumpffK::K3[j]);
+    }
+    c2 = a;
+    c3 = b;
 }
 
 template <int NT>
@@ -296,12 +339,12 @@ __device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, 
 template <int NT>
 __device__ __forceinline__ void halley(double x, double beta, double r0, double eta, double zeta, double GM,
                                        double dt, double& G0, double& G1, double& G2, double& G3, double& fp,
-                                       double& fpp, double& q, double& z, double& x3) {
+                                       double& fpp, double& q, double& z, double& x3, const VConsts& vk) {
     const double x2 = x * x;
     z = beta * x2;
     x3 = x2 * x;
     double c2, c3;
-    stumpff23<NT>(z, c2, c3);
+    stumpff23<NT>(z, c2, c3, vk.k2, vk.k3);
     G3 = x3 * c3;
     G2 = x2 * c2;
     G1 = fma(-beta, G3, x);  // x c1 = x (1 - z c3)
@@ -429,7 +472,7 @@ __device__ __forceinline__ DriftOut drift_apply(const Lane<NP>& s, double dt, do
 //   lane was not good.  Good lanes compute bit-identical states either way.
 // No square root anywhere in the step.
 template <int NT, bool GATED, bool D3 = false, int NP>
-__device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad) {
+__device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const VConsts& vk) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;
     double v2 = fma(s.vx, s.vx, s.vy * s.vy);
     double eta = fma(s.rx, s.vx, s.ry * s.vy);
@@ -445,7 +488,7 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad) {
     const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
     const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
     double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3);
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk);
     constexpr double B = stumpff_bound<NT>();
     // A step spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) that passes these tests has
     // converged all the same; only kepler_rare treats such steps separately (bracketed solver).
@@ -456,7 +499,7 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad) {
             if (nb != 0) {
                 if (fabs(z) <= B && !halley_ok<NT>(Q, x)) {
                     xe = x - Q;
-                    halley<NT>(xe, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3);
+                    halley<NT>(xe, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk);
                 }
                 nb = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, xe));
             }
@@ -488,7 +531,7 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad) {
 template <int NT, int NP>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt) {
     bool unused = false;
-    drift<NT, true>(s, dt, unused);
+    drift<NT, true>(s, dt, unused, vconsts_for<NT>());
 }
 
 // Interaction kick of the own Jacobi velocity by dt (and the encounter test on every pair):
@@ -590,7 +633,7 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
 // with heliocentric x_1 = r'_1, x_2 = r'_2 + (m_1/M_1) r'_1, d02 = x_2, d12 = x_2 - x_1.  The
 // star--planet-1 distance |r'_1| and the own |r'| are carried from the drift: 2 rsq per kick.
 template <int L, bool D3 = false>
-__device__ __forceinline__ void kick2(Lane<2>& s) {
+__device__ __forceinline__ void kick2(Lane<2>& s, double c1875 = 1.875) {
     const double x1 = grp_get<L, 0>(s.rx), y1 = grp_get<L, 0>(s.ry);
     const double R2x = grp_get<L, 1>(s.rx), R2y = grp_get<L, 1>(s.ry);
     const double ir01 = grp_get<L, 0>(s.ir);
@@ -608,7 +651,7 @@ __device__ __forceinline__ void kick2(Lane<2>& s) {
         r12sq = fma(dz12, dz12, r12sq);
     }
     s.encm |= ballot(r02sq < s.dmin2) | ballot(r12sq < s.dmin2) | ballot(ir01 * ir01 > s.idmin2);
-    const double i02c = rcube_nr(r02sq), i12c = rcube_nr(r12sq);
+    const double i02c = rcube_nr(r02sq, c1875), i12c = rcube_nr(r12sq, c1875);
     // coefficients carry the step (lane_set_step): v += A r' + B x2/r02^3 + C d12/r12^3
     const double A = s.kAh * (s.ir * (s.ir * s.ir));
     const double bx = s.kBh * i02c, cx = s.kCh * i12c;
@@ -618,9 +661,9 @@ __device__ __forceinline__ void kick2(Lane<2>& s) {
 }
 
 template <int NP, int L, bool D3 = false>
-__device__ __forceinline__ void kick(Lane<NP>& s, double dt) {
+__device__ __forceinline__ void kick(Lane<NP>& s, double dt, double c1875 = 1.875) {
     if constexpr (NP == 2)
-        kick2<L, D3>(s);  // step folded into the lane's coefficients (lane_set_step(s, dt) beforehand)
+        kick2<L, D3>(s, c1875);  // step folded into the lane's coefficients (lane_set_step(s, dt) beforehand)
     else
         kick_generic<NP, L, D3>(s, dt);
 }

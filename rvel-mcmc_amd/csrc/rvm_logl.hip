@@ -41,20 +41,21 @@ __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 template <int NT, bool GATED, bool D3, int NP, int L>
 __device__ __forceinline__ void segment_steps(Lane<NP>& s, double h, int ns, bool& bad) {
     lane_set_step(s, h);
-    drift<NT, GATED, D3>(s, 0.5 * h, bad);
+    const VConsts vk = vconsts_for<NT>();  // loop-invariant VGPR constants
+    drift<NT, GATED, D3>(s, 0.5 * h, bad, vk);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
-        kick<NP, L, D3>(s, h);
-        drift<NT, GATED, D3>(s, h, bad);
-        kick<NP, L, D3>(s, h);
-        drift<NT, GATED, D3>(s, h, bad);
+        kick<NP, L, D3>(s, h, vk.c1875);
+        drift<NT, GATED, D3>(s, h, bad, vk);
+        kick<NP, L, D3>(s, h, vk.c1875);
+        drift<NT, GATED, D3>(s, h, bad, vk);
     }
     if (j < ns - 1) {
-        kick<NP, L, D3>(s, h);
-        drift<NT, GATED, D3>(s, h, bad);
+        kick<NP, L, D3>(s, h, vk.c1875);
+        drift<NT, GATED, D3>(s, h, bad, vk);
     }
-    kick<NP, L, D3>(s, h);
-    drift<NT, GATED, D3>(s, 0.5 * h, bad);
+    kick<NP, L, D3>(s, h, vk.c1875);
+    drift<NT, GATED, D3>(s, 0.5 * h, bad, vk);
 }
 
 // SPEC: run the segment with ungated drifts (rvm_device.h) and vote once at its end; if any lane
