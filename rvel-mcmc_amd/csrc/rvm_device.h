@@ -61,8 +61,9 @@ __device__ __forceinline__ double vconst(double k) {
 
 // Loop-invariant VGPR constants of the hot path (set once per segment, vconsts_for<NT>).
 struct VConsts {
-    double k2, k3;  // top Horner coefficients of c2, c3 for the level's series length
-    double c1875;   // 15/8 of rcube_nr
+    double k2, k3;      // top Horner coefficients of c2, c3 for the level's series length
+    double k2_8, k3_8;  // the same for the 8-term series (second Halley steps)
+    double c1875;       // 15/8 of rcube_nr
 };
 
 // x^(-3/2) straight from v_rsq_f64: with y = rsq(x), e = 1 - x y^2,
@@ -102,7 +103,8 @@ struct StumpffK {
 
 template <int NT>
 __device__ __forceinline__ VConsts vconsts_for() {
-    return VConsts{vconst(StumpffK::K2[NT - 1]), vconst(StumpffK::K3[NT - 1]), vconst(1.875)};
+    return VConsts{vconst(StumpffK::K2[NT - 1]), vconst(StumpffK::K3[NT - 1]), vconst(StumpffK::K2[7]),
+                   vconst(StumpffK::K3[7]), vconst(1.875)};
 }
 
 // with the top coefficients k2 = K2[NT-1], k3 = K3[NT-1] already in VGPRs (vconsts_for<NT>)
@@ -339,12 +341,12 @@ __device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, 
 template <int NT>
 __device__ __forceinline__ void halley(double x, double beta, double r0, double eta, double zeta, double GM,
                                        double dt, double& G0, double& G1, double& G2, double& G3, double& fp,
-                                       double& fpp, double& q, double& z, double& x3, const VConsts& vk) {
+                                       double& fpp, double& q, double& z, double& x3, double k2v, double k3v) {
     const double x2 = x * x;
     z = beta * x2;
     x3 = x2 * x;
     double c2, c3;
-    stumpff23<NT>(z, c2, c3, vk.k2, vk.k3);
+    stumpff23<NT>(z, c2, c3, k2v, k3v);
     G3 = x3 * c3;
     G2 = x2 * c2;
     G1 = fma(-beta, G3, x);  // x c1 = x (1 - z c3)
@@ -488,27 +490,34 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
     const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
     const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
     double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk);
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2, vk.k3);
     constexpr double B = stumpff_bound<NT>();
     // A step spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) that passes these tests has
     // converged all the same; only kepler_rare treats such steps separately (bracketed solver).
     if constexpr (GATED) {
-        double xe = x;  // point where the G-functions were evaluated (X = xe - Q)
-        uint64_t nb = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, x));
-        if constexpr (NT >= 7) {  // coarse levels: a second Halley step is common (pericentre passages)
-            if (nb != 0) {
-                if (fabs(z) <= B && !halley_ok<NT>(Q, x)) {
-                    xe = x - Q;
-                    halley<NT>(xe, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk);
+        constexpr double B8 = stumpff_bound<8>();
+        const bool ok1 = fabs(z) <= B && halley_ok<NT>(Q, x);
+        if (ballot(!ok1) != 0) {
+            // a second Halley step with the 8-term series (|z| <= 0.3) for the lanes that need it:
+            // pericentre passages on the coarse levels, and walkers whose periods are much shorter
+            // than the plan's period hint on any level
+            bool ok = ok1;
+            double xe = x;
+            if (!ok1) {
+                const double X1 = x - Q;
+                if (fabs(beta * X1 * X1) <= B8) {
+                    xe = X1;
+                    halley<8>(xe, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2_8, vk.k3_8);
+                    ok = fabs(z) <= B8 && halley_ok<8>(Q, xe);
                 }
-                nb = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, xe));
             }
-        }
-        if (__builtin_expect(nb != 0, 0)) {
-            const bool zok = fabs(z) <= B;
-            if (!(zok && halley_ok<NT>(Q, xe))) {
-                const bool hard = fabs(beta) * (u * u) > 0.5;
-                kepler_rare(r0, eta, zeta, beta, GM, dt, zok ? xe - Q : x, hard, G0, G1, G2, G3, fp, fpp, Q);
+            if (__builtin_expect(ballot(!ok) != 0, 0)) {
+                if (!ok) {
+                    const bool hard = fabs(beta) * (u * u) > 0.5;
+                    const double start = xe - Q;
+                    kepler_rare(r0, eta, zeta, beta, GM, dt, isfinite(start) && xe != x ? start : x, hard, G0, G1,
+                                G2, G3, fp, fpp, Q);
+                }
             }
         }
     } else {

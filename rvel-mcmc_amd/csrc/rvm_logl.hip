@@ -27,12 +27,14 @@ namespace rvm {
 // Timing build (make profile -> scripts/probe/librvmcmc_prof.so): per wave, s_memtime at kernel
 // start, after the prologue, accumulated inside segments, accumulated in epoch handling (incl.
 // the barrier), and at the end.  Read with rvm_prof_copy (scripts/probe/prof_kernel.py).
-#define RVM_PROF_SLOTS 8
+#define RVM_PROF_SLOTS 10
 #define RVM_PROF_MAX_WAVES 4096
 __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 #define PROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define PROF_COUNT(var) (var)++
 #else
 #define PROF_T(v)
+#define PROF_COUNT(var)
 #endif
 
 // One epoch-to-epoch segment of ns Wisdom-Holman DKD steps of size h (ns is wave-uniform; the
@@ -60,9 +62,10 @@ __device__ __forceinline__ void segment_steps(Lane<NP>& s, double h, int ns, boo
 
 // SPEC: run the segment with ungated drifts (rvm_device.h) and vote once at its end; if any lane
 // of the wave had a step that needs the general solver, restore the segment's initial state and
-// redo it gated.  Used on the fine levels, where such steps are rare.
+// redo it gated.  Used on the fine levels, where such steps are rare.  Returns whether the
+// segment was redone (wave-uniform).  Either way every lane ends bit-identical to a gated run.
 template <int NT, bool SPEC, bool D3, int NP, int L>
-__device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
+__device__ __forceinline__ bool segment(Lane<NP>& s, double h, int ns, int& redo) {
     bool bad = false;
     if constexpr (SPEC) {
         const double rx = s.rx, ry = s.ry, vx = s.vx, vy = s.vy, r = s.r, ir = s.ir;
@@ -70,6 +73,7 @@ __device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
         const uint64_t encm = s.encm;
         segment_steps<NT, false, D3, NP, L>(s, h, ns, bad);
         if (__builtin_expect(ballot(bad) != 0, 0)) {
+            PROF_COUNT(redo);
             s.rx = rx;
             s.ry = ry;
             s.vx = vx;
@@ -80,10 +84,12 @@ __device__ __forceinline__ void segment(Lane<NP>& s, double h, int ns) {
             s.ir = ir;
             s.encm = encm;
             segment_steps<NT, true, D3, NP, L>(s, h, ns, bad);
+            return true;
         }
     } else {
         segment_steps<NT, true, D3, NP, L>(s, h, ns, bad);
     }
+    return false;
 }
 
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
@@ -274,6 +280,8 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
 #ifdef RVM_PROFILE
     unsigned long long t_seg = 0, t_epo = 0;
 #endif
+    int redo = 0;      // speculative segments redone gated (counted in the timing build only)
+    int spec_off = 0;  // wave-uniform: segments left to run gated after a redo
     double chi2 = 0.0;
     int n1 = E > 0 ? l_n[0] : 0;
     double len = E > 0 ? l_len[0] : 0.0;
@@ -285,12 +293,20 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         PROF_T(ta);
         if (ns > 0) {
             const double h = len * inv_mult;  // len holds the segment's base step
-            if (nt <= 6)
-                segment<6, true, D3, NP, L>(s, h, ns);
-            else if (nt == 7)
-                segment<7, false, D3, NP, L>(s, h, ns);
+            if (nt <= 6) {
+                // speculate unless a recent segment of this wave needed a redo: walkers whose
+                // orbits keep needing the general solver (short periods, high eccentricity in a
+                // wide ensemble) then run gated for a while instead of paying for redos
+                if (spec_off == 0) {
+                    if (segment<6, true, D3, NP, L>(s, h, ns, redo)) spec_off = 4;
+                } else {
+                    segment<6, false, D3, NP, L>(s, h, ns, redo);
+                    spec_off--;
+                }
+            } else if (nt == 7)
+                segment<7, false, D3, NP, L>(s, h, ns, redo);
             else
-                segment<8, false, D3, NP, L>(s, h, ns);
+                segment<8, false, D3, NP, L>(s, h, ns, redo);
         }
         PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
@@ -339,6 +355,8 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         o[5] = rt_start;
         o[6] = __builtin_amdgcn_s_memrealtime();
         o[7] = (unsigned long long)lvl | ((unsigned long long)blockIdx.y << 8) | ((unsigned long long)mult << 16);
+        o[8] = (unsigned long long)redo;
+        o[9] = (unsigned long long)E;
     }
 #endif
 }

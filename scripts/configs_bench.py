@@ -1,6 +1,7 @@
 """Throughput of every BASELINE.json config on one GPU (bench.py keeps the headline config).
 
   config 2: affine stretch, 1024 walkers, 2-planet synthetic (101 epochs)
+  config 2w: the headline workload (4096 walkers) from a wide initial ball
   config 3: affine stretch, 4096 walkers, HD155358.vels (122 epochs)
   config 4: SMALA, 256 chains, 10-dim 2-planet, FD gradient/metric (21 logL per chain-step)
   config 5: affine stretch, 3-planet synthetic, 8192 walkers per GPU (= 65536 over 8 GPUs);
@@ -32,9 +33,9 @@ THIRD = {"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}
 SCALES = {"m": 1.5e-3, "a": 0.3, "h": 0.1, "k": 0.1, "l": np.pi / 2.}
 
 
-def _affine(state, obs, W, steps=20, warmup=3):
+def _affine(state, obs, W, steps=20, warmup=3, ball=1e-3):
     sc = np.array([SCALES[k] for k in state.get_rawkeys()])
-    X0 = state.get_params()[None] + 1e-3 * sc * np.random.normal(size=(W, state.Nvars))
+    X0 = state.get_params()[None] + ball * sc * np.random.normal(size=(W, state.Nvars))
     ens = EnsembleSampler(W, state, obs, seed=1)
     ens.set_positions(X0)
     ens.compute_lnprob()
@@ -55,6 +56,16 @@ def config2():
     s = State(planets=[dict(p) for p in S2])
     obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
     return {"config": "2: affine, 1024 walkers, 2-planet synthetic", **_affine(s, obs, 1024)}
+
+
+def config2w():
+    """the same workload from a wide ball (x100 the tight one) to expose prior /
+    encounter exits and the kernel's general-solver paths (eccentric, close orbits)."""
+    np.random.seed(2017)
+    s = State(planets=[dict(p) for p in S2])
+    obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    out = _affine(s, obs, 4096, ball=1e-1)
+    return {"config": "2w: affine, 4096 walkers, 2-planet synthetic, wide ball (0.1 x scales)", **out}
 
 
 def config3():
@@ -109,9 +120,9 @@ def config1(steps=200):
 
 
 def main():
-    which = sys.argv[1:] or ["2", "3", "4", "5", "1"]
+    which = sys.argv[1:] or ["2", "2w", "3", "4", "5", "1"]
     for c in which:
-        out = {"1": config1, "2": config2, "3": config3, "4": config4, "5": config5}[c]()
+        out = {"1": config1, "2": config2, "2w": config2w, "3": config3, "4": config4, "5": config5}[c]()
         print(json.dumps(out), flush=True)
 
 

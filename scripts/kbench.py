@@ -29,7 +29,7 @@ def main():
     rng = np.random.default_rng(0)
     for W in Ws:
         P = np.repeat(O.pal_params(S2_PLANETS)[None], W, 0)
-        P[:, :, :5] *= 1 + 1e-3 * rng.standard_normal((W, 2, 5))
+        P[:, :, :5] *= 1 + float(os.environ.get("BALL", "1e-3")) * rng.standard_normal((W, 2, 5))
         K = torch.as_tensor(np.concatenate([P[:, p, :5].T for p in range(2)], 0).copy(), device="cuda")
         lp, st, _ = plan.logl(K)
         torch.cuda.synchronize()

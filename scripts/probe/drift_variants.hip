@@ -29,7 +29,7 @@ __device__ __forceinline__ void drift_v1(Lane<NP>& s, double dt) {
         x = u * fma(u, fma(u, T3, -hs), 1.0);
     }
     double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>());
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>().k2, vconsts_for<NT>().k3);
     constexpr double B = stumpff_bound<NT>();
     const double X = x - Q;
     const bool hard = fabs(beta) * (u * u) > 0.5;
@@ -61,7 +61,7 @@ __device__ __forceinline__ void drift_v2(Lane<NP>& s, double dt) {
     const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
     const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
     double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>());
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>().k2, vconsts_for<NT>().k3);
     const DriftOut o = drift_apply<false>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     s.rx = o.rx;
     s.ry = o.ry;

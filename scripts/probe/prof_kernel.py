@@ -16,7 +16,7 @@ import oracle as O  # noqa: E402
 from conftest import S2_PLANETS, s2_obs_oracle  # noqa: E402
 from rvmcmc import _lib, engine  # noqa: E402
 
-SLOTS, MAXW = 8, 4096
+SLOTS, MAXW = 10, 4096
 
 
 def main():
@@ -31,7 +31,7 @@ def main():
     plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint)
     rng = np.random.default_rng(0)
     P = np.repeat(O.pal_params(S2_PLANETS)[None], W, 0)
-    P[:, :, :5] *= 1 + 1e-3 * rng.standard_normal((W, 2, 5))
+    P[:, :, :5] *= 1 + float(os.environ.get("BALL", "1e-3")) * rng.standard_normal((W, 2, 5))
     K = torch.as_tensor(np.concatenate([P[:, p, :5].T for p in range(2)], 0).copy(), device="cuda")
     for _ in range(3):
         plan.logl(K)
@@ -58,7 +58,8 @@ def main():
                             "segments_kcyc": float(np.median(b[m, 2]) / 1e3),
                             "epochs_kcyc": float(np.median(b[m, 3]) / 1e3),
                             "tail_kcyc": float(np.median(tot - (b[m, 1] - b[m, 0]) - b[m, 2] - b[m, 3]) / 1e3),
-                            "max_total_kcyc": float(tot.max() / 1e3)}
+                            "max_total_kcyc": float(tot.max() / 1e3),
+                            "segments_redone_mean": float(b[m, 8].mean()), "segments": int(b[m, 9].max())}
     rt = (b[:, 6] - b[:, 5]) / 100.0
     out["wave_realtime_us"] = {"min": float(rt.min()), "median": float(np.median(rt)), "max": float(rt.max())}
     out["start_spread_us"] = float((b[:, 5].max() - b[:, 5].min()) / 100.0)
