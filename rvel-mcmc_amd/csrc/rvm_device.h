@@ -248,6 +248,13 @@ __device__ __forceinline__ double grp_get(double v, int q) {
     }
 }
 
+// Body pairs (a, b), a < b, of the closed-form kick for NP >= 3: all but (0, 1), whose term
+// cancels the own Kepler term on planet 1's lane and vanishes on every other lane (kickN).
+template <int NP>
+struct KickPairs {
+    static constexpr int n = NP >= 3 ? (NP + 1) * NP / 2 - 1 : 1;
+};
+
 // One lane: one planet's Jacobi coordinate plus the walker-wide constants every lane needs.
 template <int NP>
 struct Lane {
@@ -261,6 +268,8 @@ struct Lane {
     double dmin2, idmin2;   // (hill_factor * max r_Hill)^2 and its reciprocal
     double kA, kB, kC;      // closed-form 2-planet kick coefficients of the own lane (kick2)
     double kAh, kBh, kCh;   // the same times the current step (lane_set_step)
+    double kP[KickPairs<NP>::n];   // NP >= 3 (kickN): own-lane coefficient of every pair but (0,1)
+    double kPh[KickPairs<NP>::n];  // the same times the current step
     int p;                  // own planet index (lane % L, clamped to NP-1)
     uint64_t encm;          // wave mask of lanes that saw a pair closer than the exit distance
                             // (SGPRs: the kick's compares go straight into it; identical bits on
@@ -273,6 +282,10 @@ __device__ __forceinline__ void lane_set_step(Lane<NP>& s, double h) {
     s.kAh = s.kA * h;
     s.kBh = s.kB * h;
     s.kCh = s.kC * h;
+    if constexpr (NP >= 3) {
+#pragma unroll
+        for (int k = 0; k < KickPairs<NP>::n; k++) s.kPh[k] = s.kP[k] * h;
+    }
 }
 
 // Derived per-lane constants (after p, GM, m, iMi, dmin2 are set).
@@ -288,7 +301,36 @@ __device__ __forceinline__ void lane_finish(Lane<NP>& s) {
         s.kB = p1 ? -s.m[1] : -q;
         s.kC = p1 ? s.m[1] : -q * s.m[0];
     } else {
-        s.kA = s.kB = s.kC = 0.0;
+        s.kB = s.kC = 0.0;
+        s.kA = 0.0;
+#pragma unroll
+        for (int k = 0; k < KickPairs<NP>::n; k++) s.kP[k] = 0.0;
+        if constexpr (NP >= 3) {
+            // kickN: Jacobi acceleration of coordinate i = p + 1 (bodies 0..NP, m_0 = M_star = 1)
+            //   a'_i = sum_{j != i} m_j d_ij / r_ij^3 - (1/M_{i-1}) sum_{a < i <= b} m_a m_b d_ab / r_ab^3
+            // so pair (a, b) enters with c_ab = [a = i] m_b - [b = i] m_a - [a < i <= b] m_a m_b / M_{i-1},
+            // and the own Kepler term M_i r'_i / |r'_i|^3 is added back for i >= 2 (for i = 1 it
+            // cancels c_01 exactly; c_01 = 0 on every other lane).
+            const int i = s.p + 1;
+            s.kA = i == 1 ? 0.0 : s.GM;
+            double iMprev = 0.0;  // 1 / M_{i-1}, summed rather than indexed (no runtime array index)
+#pragma unroll
+            for (int q = 0; q < NP; q++) iMprev += s.p == q ? s.iMi[q] : 0.0;
+            int k = 0;
+#pragma unroll
+            for (int a = 0; a <= NP; a++) {
+#pragma unroll
+                for (int b = a + 1; b <= NP; b++) {
+                    if (a == 0 && b == 1) continue;
+                    const double ma = a == 0 ? 1.0 : s.m[a - 1], mb = s.m[b - 1];
+                    double c = 0.0;
+                    if (a == i) c += mb;
+                    if (b == i) c -= ma;
+                    if (a < i && i <= b) c -= ma * mb * iMprev;
+                    s.kP[k++] = c;
+                }
+            }
+        }
     }
     lane_set_step(s, 0.0);
 }
@@ -669,10 +711,63 @@ __device__ __forceinline__ void kick2(Lane<2>& s, double c1875 = 1.875) {
     if constexpr (D3) s.vz = fma(A, s.rz, fma(bx, z2, fma(cx, dz12, s.vz)));
 }
 
+// Closed-form kick for NP >= 3 planets (the same interaction as kick_generic): every lane of
+// the group forms the heliocentric positions and the inverse cubes of all pairs but (0, 1), and
+// applies its own coefficients (lane_finish, step folded in by lane_set_step):
+//   v'_i += h [ A_i r'_i / |r'_i|^3 + sum_ab c_ab(i) d_ab / r_ab^3 ],   d_ab = x_b - x_a.
+// The star--planet-1 exit check uses |r'_1| = |x_1| on planet 1's lane, the only lane whose
+// encounter bit is read.
+template <int NP, int L, bool D3 = false>
+__device__ __forceinline__ void kickN(Lane<NP>& s, double c1875) {
+    constexpr int NB = NP + 1;
+    double x[NB], y[NB], z[NB];
+    x[0] = y[0] = z[0] = 0.0;
+    double cmx = 0.0, cmy = 0.0, cmz = 0.0;
+#pragma unroll
+    for (int i = 1; i < NB; i++) {
+        const double Rx = grp_get<L>(s.rx, i - 1), Ry = grp_get<L>(s.ry, i - 1);
+        const double Rz = D3 ? grp_get<L>(s.rz, i - 1) : 0.0;
+        x[i] = i == 1 ? Rx : fma(cmx, s.iMi[i - 1], Rx);
+        y[i] = i == 1 ? Ry : fma(cmy, s.iMi[i - 1], Ry);
+        z[i] = i == 1 ? Rz : fma(cmz, s.iMi[i - 1], Rz);
+        if (i + 1 < NB) {
+            cmx = fma(s.m[i - 1], x[i], cmx);
+            cmy = fma(s.m[i - 1], y[i], cmy);
+            if constexpr (D3) cmz = fma(s.m[i - 1], z[i], cmz);
+        }
+    }
+    uint64_t enc = ballot(s.ir * s.ir > s.idmin2);
+    double vx = s.vx, vy = s.vy, vz = s.vz;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < NB; a++) {
+#pragma unroll
+        for (int b = a + 1; b < NB; b++) {
+            if (a == 0 && b == 1) continue;
+            const double dx = x[b] - x[a], dy = y[b] - y[a], dz = z[b] - z[a];
+            double r2 = fma(dx, dx, dy * dy);
+            if constexpr (D3) r2 = fma(dz, dz, r2);
+            enc |= ballot(r2 < s.dmin2);
+            const double cf = s.kPh[k++] * rcube_nr(r2, c1875);
+            vx = fma(cf, dx, vx);
+            vy = fma(cf, dy, vy);
+            if constexpr (D3) vz = fma(cf, dz, vz);
+        }
+    }
+    s.encm |= enc;
+    const double A = s.kAh * (s.ir * (s.ir * s.ir));
+    s.vx = fma(A, s.rx, vx);
+    s.vy = fma(A, s.ry, vy);
+    if constexpr (D3) s.vz = fma(A, s.rz, vz);
+}
+
 template <int NP, int L, bool D3 = false>
 __device__ __forceinline__ void kick(Lane<NP>& s, double dt, double c1875 = 1.875) {
+    // NP >= 2: the step is folded into the lane's coefficients (lane_set_step(s, dt) beforehand)
     if constexpr (NP == 2)
-        kick2<L, D3>(s, c1875);  // step folded into the lane's coefficients (lane_set_step(s, dt) beforehand)
+        kick2<L, D3>(s, c1875);
+    else if constexpr (NP >= 3)
+        kickN<NP, L, D3>(s, c1875);
     else
         kick_generic<NP, L, D3>(s, dt);
 }

@@ -148,17 +148,34 @@ def test_t1_levels(nl, spo):
     _assert_t1(got, st, ref, st_ref, nl)
 
 
+EXTRA_PLANETS = [{"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0},
+                 {"m": 5e-4, "a": 4.1, "h": -0.03, "k": 0.02, "l": 4.0}]
+
+
 @pytest.mark.parametrize("n_planets", [1, 3, 4])
 def test_t1_planet_counts(n_planets):
-    extra = [{"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0},
-             {"m": 5e-4, "a": 4.1, "h": -0.03, "k": 0.02, "l": 4.0}]
-    planets = (S2_PLANETS + extra)[:n_planets]
+    planets = (S2_PLANETS + EXTRA_PLANETS)[:n_planets]
     np.random.seed(11)
     obs = O.fake_obs(planets, Npoints=40, error=1.5e-4, errorVar=2.5e-5, tmax=60.)
     plan, dt = _plan(obs, planets)
     P = _ball(planets, 70, seed=n_planets)
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS)
+    _assert_t1(got, st, ref, st_ref)
+
+
+@pytest.mark.parametrize("n_planets,hill", [(3, 4.0), (4, 3.0)])
+def test_t1_planet_counts_close_encounters(n_planets, hill):
+    """3- and 4-planet closed-form kick (kickN): exit-distance statuses on a wide ball with a
+    large Hill factor must match the oracle walker for walker, logL within T1 elsewhere."""
+    planets = (S2_PLANETS + EXTRA_PLANETS)[:n_planets]
+    np.random.seed(12)
+    obs = O.fake_obs(planets, Npoints=30, error=1.5e-4, errorVar=2.5e-5, tmax=40.)
+    plan, dt = _plan(obs, planets)
+    P = _ball(planets, 128, rel=0.05, seed=30 + n_planets)
+    got, st, _ = _run(plan, P, hill=hill)
+    ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS, hill_factor=hill)
+    assert 0 < np.count_nonzero(st_ref == 2) < len(P)  # some walkers exit, not all
     _assert_t1(got, st, ref, st_ref)
 
 
@@ -332,3 +349,18 @@ def test_state_api_inclined_free_parameters():
     ref, _ = O.logl_ias15_batch(O.pal_params(S2_INCLINED)[None], 2, obs, hill_factor=1.0, has_inc=1)
     assert (st.cpu().numpy() == 0).all()
     assert np.abs(lp.cpu().numpy() - ref[0]).max() < T2_ABS
+
+
+@pytest.mark.parametrize("n_planets", [3, 4])
+def test_t1_inclined_planet_counts(n_planets):
+    """3-D closed-form kick for 3 and 4 planets against the oracle."""
+    planets = [dict(p, ix=0.03 * (i + 1), iy=-0.02 * i) for i, p in enumerate((S2_PLANETS + EXTRA_PLANETS)[:n_planets])]
+    np.random.seed(13)
+    obs = O.fake_obs(planets, Npoints=40, error=1.5e-4, errorVar=2.5e-5, tmax=50.)
+    plan, dt = _plan(obs, planets, inclined=True)
+    P = _ball(planets, 64, seed=40 + n_planets)
+    rng = np.random.default_rng(50 + n_planets)
+    P[:, :, 5:7] += 1e-3 * rng.standard_normal((64, n_planets, 2))
+    got, st, _ = _run(plan, P)
+    ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS, has_inc=1)
+    _assert_t1(got, st, ref, st_ref)
