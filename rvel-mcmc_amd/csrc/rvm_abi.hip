@@ -175,6 +175,12 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.npoints = cfg->npoints_norm;
     P.n_obs = n_obs;
     P.inclined = cfg->inclined ? 1 : 0;
+    {
+        int dev = 0, ncu = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            ncu = 0;
+        P.n_cu = ncu;
+    }
     // Richardson weights for the h^2 expansion: level k steps dt/mult[k]; Lagrange at 0 in x = 1/mult^2
     for (int k = 0; k < RVM_MAX_LEVELS; k++) {
         P.mult[k] = k < cfg->n_levels ? mult[k] : 1;

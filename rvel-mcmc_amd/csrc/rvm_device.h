@@ -682,12 +682,11 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
 //   dv'_1 = dt m_2 (d12/r12^3 - d02/r02^3)
 //   dv'_2 = dt [ M_2 r'_2/|r'_2|^3 - (M_2/M_1)(d02/r02^3 + m_1 d12/r12^3) ]
 // with heliocentric x_1 = r'_1, x_2 = r'_2 + (m_1/M_1) r'_1, d02 = x_2, d12 = x_2 - x_1.  The
-// star--planet-1 distance |r'_1| and the own |r'| are carried from the drift: 2 rsq per kick.
+// own |r'| (= star--planet-1 distance on planet 1's lane) is carried from the drift: 2 rsq per kick.
 template <int L, bool D3 = false>
 __device__ __forceinline__ void kick2(Lane<2>& s, double c1875 = 1.875) {
     const double x1 = grp_get<L, 0>(s.rx), y1 = grp_get<L, 0>(s.ry);
     const double R2x = grp_get<L, 1>(s.rx), R2y = grp_get<L, 1>(s.ry);
-    const double ir01 = grp_get<L, 0>(s.ir);
     const double c = s.m[0] * s.iMi[1];  // m_1 / M_1
     const double x2 = fma(c, x1, R2x), y2 = fma(c, y1, R2y);
     const double dx12 = x2 - x1, dy12 = y2 - y1;
@@ -701,7 +700,8 @@ __device__ __forceinline__ void kick2(Lane<2>& s, double c1875 = 1.875) {
         r02sq = fma(z2, z2, r02sq);
         r12sq = fma(dz12, dz12, r12sq);
     }
-    s.encm |= ballot(r02sq < s.dmin2) | ballot(r12sq < s.dmin2) | ballot(ir01 * ir01 > s.idmin2);
+    // star--planet-1 exit check from |r'_1| on planet 1's lane, the only encounter bit read
+    s.encm |= ballot(r02sq < s.dmin2) | ballot(r12sq < s.dmin2) | ballot(s.ir * s.ir > s.idmin2);
     const double i02c = rcube_nr(r02sq, c1875), i12c = rcube_nr(r12sq, c1875);
     // coefficients carry the step (lane_set_step): v += A r' + B x2/r02^3 + C d12/r12^3
     const double A = s.kAh * (s.ir * (s.ir * s.ir));

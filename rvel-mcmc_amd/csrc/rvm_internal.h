@@ -27,6 +27,7 @@ struct DevPlan {
     double npoints;
     int32_t n_obs;
     int32_t inclined;  // 1: 7 parameter rows per planet (ix, iy), 3-D integration
+    int32_t n_cu;      // compute units of the plan's device (launch shape, launch_logl)
     DirSched fwd, bwd;
 };
 

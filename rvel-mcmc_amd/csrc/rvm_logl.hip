@@ -27,7 +27,7 @@ namespace rvm {
 // Timing build (make profile -> scripts/probe/librvmcmc_prof.so): per wave, s_memtime at kernel
 // start, after the prologue, accumulated inside segments, accumulated in epoch handling (incl.
 // the barrier), and at the end.  Read with rvm_prof_copy (scripts/probe/prof_kernel.py).
-#define RVM_PROF_SLOTS 10
+#define RVM_PROF_SLOTS 11
 #define RVM_PROF_MAX_WAVES 4096
 __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 #define PROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -94,7 +94,7 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, double h, int ns, int& redo
 
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
 template <int NP, bool D3>
-__global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan P, const int W,
+__global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                                                                    const double* __restrict__ params,
                                                                    const double hill_factor,
                                                                    double* __restrict__ chi2_part,
@@ -106,18 +106,28 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
 #ifdef RVM_PROFILE
     const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    const int lvl = threadIdx.x >> 6;              // wave-uniform extrapolation level
+    // A block holds G = 1 or 2 walker groups (launch_logl), each one wave per level.  Group 1
+    // runs the levels in mirrored order: consecutive waves of a block land on consecutive SIMDs,
+    // so wave i of group 1 shares a SIMD with wave i of group 0 and every SIMD carries
+    // mult[i] + mult[nl-1-i] steps per base step instead of up to 2 mult[nl-1].
+    const int nl = P.n_levels;
+    const int wv = threadIdx.x >> 6;
+    const int grp = wv >= nl ? 1 : 0;
+    const int lvl = grp ? 2 * nl - 1 - wv : wv;    // wave-uniform extrapolation level
+    const int G = (blockDim.x >> 6) / nl;
     const int lane = threadIdx.x & 63;
-    const int slot = lane / L;                     // walker slot within the block
+    const int slot = lane / L;                     // walker slot within the group
     const int pl_idx = lane % L;
     const int d = blockIdx.y;
-    const int w = blockIdx.x * WPB + slot;
+    const int w0 = (blockIdx.x * G + grp) * WPB;   // first walker of the group
+    const int w = w0 + slot;
     const bool valid = w < W;
     const int wl = valid ? w : (W - 1);
-    const int nl = P.n_levels;
 
-    __shared__ double s_rv[2][RVM_MAX_LEVELS][64];
-    __shared__ int s_enc[RVM_MAX_LEVELS][64];
+    __shared__ double s_rv_all[2][2][RVM_MAX_LEVELS][64];
+    __shared__ int s_enc_all[2][RVM_MAX_LEVELS][64];
+    double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
+    int(*s_enc)[64] = s_enc_all[grp];
     // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
     extern __shared__ double s_sched[];  // [E] seg_h1 | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
 
@@ -317,7 +327,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
             for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv[e & 1][k][lane];
             const double r = rvx - l_rv[e];
             chi2 += (r * r) / l_s2[e];
-            const int wo = blockIdx.x * WPB + lane;
+            const int wo = w0 + lane;
             if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[e] * W + wo] = rvx;
         }
         n1 = n1_next;
@@ -331,7 +341,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     if (pl_idx == 0) s_enc[lvl][slot] = (int)((s.encm >> lane) & 1) | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
     if (lvl == 0 && lane < WPB) {
-        const int wo = blockIdx.x * WPB + lane;
+        const int wo = w0 + lane;
         if (wo < W) {
             int enc = 0;
             for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
@@ -344,7 +354,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
     }
 #ifdef RVM_PROFILE
     PROF_T(t_end);
-    const int gw = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + lvl;
+    const int gw = (blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + wv;
     if (lane == 0 && gw < RVM_PROF_MAX_WAVES) {
         unsigned long long* o = rvm_prof + (size_t)gw * RVM_PROF_SLOTS;
         o[0] = t_start;
@@ -357,6 +367,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void logl_kernel(const DevPlan
         o[7] = (unsigned long long)lvl | ((unsigned long long)blockIdx.y << 8) | ((unsigned long long)mult << 16);
         o[8] = (unsigned long long)redo;
         o[9] = (unsigned long long)E;
+        o[10] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
     }
 #endif
 }
@@ -378,8 +389,13 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
                        int32_t* status_part, double* logl, int32_t* status, double* rv_out, hipStream_t stream) {
     const int lpw = P.n_planets == 1 ? 1 : (P.n_planets == 2 ? 2 : 4);  // LanesPerWalker
     const int wpb = 64 / lpw;
-    const dim3 grid((W + wpb - 1) / wpb, 2);
-    const dim3 block(64 * P.n_levels);
+    const int groups = (W + wpb - 1) / wpb;
+    // one walker group per block while the blocks fit one per CU (every wave alone on its SIMD:
+    // latency-bound); beyond that two groups with mirrored level order per block, which pairs
+    // the heaviest level with the lightest on each SIMD (logl_kernel)
+    const int G = (P.n_cu > 0 && 2 * groups > P.n_cu && 2 * P.n_levels * 64 <= 512) ? 2 : 1;
+    const dim3 grid((groups + G - 1) / G, 2);
+    const dim3 block(64 * P.n_levels * G);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t smem = (size_t)emax * (3 * sizeof(double) + 2 * sizeof(int32_t)) + 16;
 #define RVM_LAUNCH(NPV, D3V) \

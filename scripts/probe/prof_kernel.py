@@ -16,11 +16,12 @@ import oracle as O  # noqa: E402
 from conftest import S2_PLANETS, s2_obs_oracle  # noqa: E402
 from rvmcmc import _lib, engine  # noqa: E402
 
-SLOTS, MAXW = 10, 4096
+SLOTS, MAXW = 11, 4096
 
 
 def main():
     W = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+    assert W <= 8192
     _lib.LIB_PATH = os.path.join(ROOT, "scripts", "probe", "librvmcmc_prof.so")
     lib = _lib.load()
     lib.rvm_prof_copy.argtypes = [C.c_void_p, C.c_size_t]
@@ -63,6 +64,20 @@ def main():
     rt = (b[:, 6] - b[:, 5]) / 100.0
     out["wave_realtime_us"] = {"min": float(rt.min()), "median": float(np.median(rt)), "max": float(rt.max())}
     out["start_spread_us"] = float((b[:, 5].max() - b[:, 5].min()) / 100.0)
+    # placement (HW_REG_HW_ID, gfx9 layout): wave_id [3:0], simd [5:4], cu [11:8], sh [12], se [15:13]
+    hw = b[:, 10]
+    simd, cu, sh, se = (hw >> 4) & 3, (hw >> 8) & 15, (hw >> 12) & 1, (hw >> 13) & 7
+    gidx = np.nonzero(used)[0]
+    wv = gidx % int(os.environ.get("WPB_WAVES", "4"))  # wave index within its block
+    out["wave_in_block_vs_simd"] = {int(k): np.bincount(simd[wv == k], minlength=4).tolist() for k in sorted(set(wv.tolist()))}
+    key = (se * 2 + sh) * 16 + cu
+    mult = (b[:, 7] >> 16) & 0xFF
+    load = {}
+    for k, s_, m_ in zip(key.tolist(), simd.tolist(), mult.tolist()):
+        load.setdefault((k, s_), []).append(m_)
+    per = [sum(v) for v in load.values()]
+    out["simd_load_mult_sum"] = {"max": int(max(per)), "hist": {str(x): per.count(x) for x in sorted(set(per))}}
+    out["cus_used"] = int(len(set(key.tolist())))
     print(json.dumps(out, indent=1))
 
 

@@ -34,7 +34,15 @@ def main():
     W = int(os.environ.get("W", "16"))
     grid = [(4, 24), (3, 24), (3, 32), (3, 40), (5, 16), (5, 20), (6, 12), (6, 16), (4, 20), (4, 16)]
     if len(sys.argv) > 1:
-        grid = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
+        # "nl,spo" (harmonic levels 1..nl) or "m1-m2-...@spo" (level multiplier sequence)
+        grid = []
+        for a in sys.argv[1:]:
+            if "@" in a:
+                seq, spo = a.split("@")
+                grid.append((tuple(int(v) for v in seq.split("-")), float(spo)))
+            else:
+                nl, spo = a.split(",")
+                grid.append((int(nl), float(spo)))
     for name, planets, obs in cases:
         pmin = min(2 * np.pi * np.sqrt(p["a"] ** 3 / (1 + p["m"])) for p in planets)
         rng = np.random.default_rng(1)
@@ -48,8 +56,10 @@ def main():
             got, st = O.logl_whx_batch(params, len(planets), obs, dt, nl, hill_factor=1.0)
             err = np.max(np.abs(got[ok] - ref[ok]))
             s1 = steps(obs, dt)
-            print(json.dumps({"case": name, "levels": nl, "spo": spo, "max_abs_dlogl": float(err),
-                              "critical_steps": s1 * nl, "total_steps": s1 * nl * (nl + 1) // 2}), flush=True)
+            mult = list(range(1, nl + 1)) if isinstance(nl, int) else list(nl)
+            print(json.dumps({"case": name, "levels": mult, "spo": spo, "max_abs_dlogl": float(err),
+                              "sum_abs_w": float(np.abs(O.richardson_weights(nl)).sum()),
+                              "critical_steps": s1 * max(mult), "total_steps": s1 * sum(mult)}), flush=True)
 
 
 if __name__ == "__main__":
