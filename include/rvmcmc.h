@@ -13,8 +13,8 @@
  *   mcmc.py:28-35     lnprob(x, e) (emcee callback)         rvm_logl_batch
  *   observations.py:6-69 Observation.{tf,tb,rvf,rvb,       rvm_plan_create (epoch schedule, obs data)
  *     errorf,errorb,Npoints}
- *   mcmc.py:57-65 Ensemble.step -> emcee 2.2.1 stretch     rvm_stretch_propose / rvm_stretch_accept
- *     move (EnsembleSampler._propose_stretch)
+ *   mcmc.py:57-65 Ensemble.step -> emcee 2.2.1 stretch     rvm_stretch_propose / rvm_stretch_accept,
+ *     move (EnsembleSampler._propose_stretch)                or fused: rvm_stretch_half_step
  *   mcmc.py:89-121 Mh.generate_proposal / Mh.step          rvm_mh_propose / rvm_mh_accept
  *   mcmc.py:144-187 Smala.generate_proposal/step           rvm_fd_params (finite-difference stencil)
  *     mcmc.py:135-139 Smala.softabs,                         + rvm_smala_derive / rvm_smala_propose /
@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 3
+#define RVM_ABI_VERSION 4
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -110,6 +110,27 @@ int rvm_stretch_propose(int32_t n_params, int32_t n_s0, int64_t s0_begin, const 
 int rvm_stretch_accept(int32_t n_params, int32_t n_s0, int64_t s0_begin, double* x, double* lnp, const double* q,
                        const double* lnp_new, const double* z, uint64_t seed, uint64_t iteration, uint32_t half,
                        const double* draws, int32_t* accepted, void* stream);
+
+/* Mapping of a State's free-parameter vector onto the kernel's parameter rows (rvmcmc.engine.
+ * ParamMap): row r (5 or 7 per planet, see Conventions) takes free parameter src[r], or the fixed
+ * value base[r] when src[r] < 0 (state.py:26-31 ignore_vars / ignore_params). */
+#define RVM_MAX_PARAM_ROWS (7 * RVM_MAX_PLANETS)
+typedef struct rvm_param_map {
+    int32_t n_rows;
+    int32_t src[RVM_MAX_PARAM_ROWS];
+    double base[RVM_MAX_PARAM_ROWS];
+} rvm_param_map;
+
+/* One whole stretch-move half-step in ONE likelihood launch: the proposal (as
+ * rvm_stretch_propose, Philox draws), the walker log-likelihood of the proposals (as
+ * rvm_logl_batch on map(q)), and the accept (as rvm_stretch_accept), bit-identical to the
+ * three-call sequence.  x: [n_params][n_s0] free parameters (in place), lnp [n_s0] (in place),
+ * c: complement [n_params][n_s1]; n_s0 <= the plan's max_walkers.  lnp_new_out / status_out
+ * (nullable): the proposals' logl and status; accepted (nullable): int32 counters += 1. */
+int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_s0,
+                          int64_t s0_begin, double* x, double* lnp, int32_t n_s1, const double* c, double a,
+                          uint64_t seed, uint64_t iteration, uint32_t half, double hill_factor,
+                          double* lnp_new_out, int32_t* status_out, int32_t* accepted, void* stream);
 
 /* Gaussian random-walk Metropolis-Hastings (mcmc.py:89-121), n_chains independent chains:
  * propose: q = x + step_size * scales[p] * N(0,1)        draws layout: [n_params][n_chains]

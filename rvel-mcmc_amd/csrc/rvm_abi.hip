@@ -15,8 +15,8 @@
 #include "rvm_internal.h"
 
 namespace rvm {
-hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, double* chi2_part,
-                       int32_t* status_part, double* logl, int32_t* status, double* rv_out, hipStream_t stream);
+hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
+                       double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
 hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
                                   uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
                                   double* z, hipStream_t st);
@@ -41,8 +41,7 @@ hipError_t launch_smala_accept(int P, int C, int64_t begin, double* x, const Sma
 struct rvm_plan {
     rvm::DevPlan dev;
     void* dmem = nullptr;        // one device allocation: schedule + workspace
-    double* chi2_part = nullptr; // [2][max_walkers]
-    int32_t* status_part = nullptr;
+    unsigned long long* slots = nullptr;  // [max_walkers] direction meeting slots (rvm_logl.hip)
     int32_t max_walkers = 0;
     int32_t steps[2] = {0, 0};
 };
@@ -122,8 +121,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
 
     // device layout: per direction [seg_n | obs_idx] int32 and [seg_len | obs_rv | obs_s2] f64, + workspace
     const size_t nf = dir[0].idx.size(), nb = dir[1].idx.size();
-    const size_t n_dbl = 3 * (nf + nb) + 2 * (size_t)max_walkers;
-    const size_t n_int = 2 * (nf + nb) + 2 * (size_t)max_walkers;
+    const size_t n_dbl = 3 * (nf + nb) + (size_t)max_walkers;  // schedule f64 | slots (u64)
+    const size_t n_int = 2 * (nf + nb);
     const size_t bytes = n_dbl * sizeof(double) + n_int * sizeof(int32_t) + 64;
     rvm_plan* plan = new rvm_plan();
     hipError_t e = hipMalloc(&plan->dmem, bytes);
@@ -159,8 +158,9 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         oi += n;
         plan->steps[dd] = (int32_t)total_steps[dd];
     }
-    plan->chi2_part = dd_base + od;
-    plan->status_part = di_base + oi;
+    plan->slots = reinterpret_cast<unsigned long long*>(dd_base + od);
+    for (int32_t i = 0; i < max_walkers; i++)  // empty between launches (the kernel restores this)
+        reinterpret_cast<unsigned long long*>(hd + od)[i] = 0x7FF4DEADBEEF0001ULL;
     plan->max_walkers = max_walkers;
     e = hipMemcpy(plan->dmem, host.data(), bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -234,10 +234,47 @@ int rvm_logl_batch(const rvm_plan* plan, int32_t n_walkers, const double* params
         return fail(-1, "rvm_logl_batch: n_walkers exceeds the plan's max_walkers");
     if (!params || !logl_out || !status_out) return fail(-1, "rvm_logl_batch: null buffer");
     if (!(hill_factor >= 0.0)) return fail(-1, "rvm_logl_batch: hill_factor must be >= 0");
-    hipError_t e = rvm::launch_logl(plan->dev, n_walkers, params, hill_factor, plan->chi2_part, plan->status_part,
-                                    logl_out, status_out, rv_out, (hipStream_t)stream);
+    rvm::StretchArgs none{};
+    hipError_t e = rvm::launch_logl(plan->dev, n_walkers, params, hill_factor, plan->slots, logl_out, status_out,
+                                    rv_out, none, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "rvm_logl_batch");
     return 0;
+}
+
+int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_s0,
+                          int64_t s0_begin, double* x, double* lnp, int32_t n_s1, const double* c, double a,
+                          uint64_t seed, uint64_t iteration, uint32_t half, double hill_factor,
+                          double* lnp_new_out, int32_t* status_out, int32_t* accepted, void* stream) {
+    if (!plan || !map) return fail(-1, "rvm_stretch_half_step: null plan or map");
+    if (n_s0 == 0) return 0;
+    if (n_s0 < 0 || n_s0 > plan->max_walkers)
+        return fail(-1, "rvm_stretch_half_step: n_s0 exceeds the plan's max_walkers");
+    if (n_params < 1 || n_s1 < 1 || !x || !lnp || !c) return fail(-1, "rvm_stretch_half_step: bad arguments");
+    if (!(a > 1.0)) return fail(-1, "rvm_stretch_half_step: stretch scale a must be > 1");
+    if (!(hill_factor >= 0.0)) return fail(-1, "rvm_stretch_half_step: hill_factor must be >= 0");
+    const int rows = (plan->dev.inclined ? 7 : 5) * plan->dev.n_planets;
+    if (map->n_rows != rows) return fail(-1, "rvm_stretch_half_step: map rows do not match the plan");
+    rvm::StretchArgs sa{};
+    sa.c = c;
+    sa.x = x;
+    sa.lnp = lnp;
+    sa.accepted = accepted;
+    sa.s0_begin = s0_begin;
+    sa.seed = seed;
+    sa.iteration = iteration;
+    sa.a = a;
+    sa.n1 = n_s1;
+    sa.dim = n_params;
+    sa.half = half;
+    for (int r = 0; r < RVM_MAX_PARAM_ROWS; r++) {
+        const int k = r < rows ? map->src[r] : -1;
+        if (k >= n_params) return fail(-1, "rvm_stretch_half_step: map source index out of range");
+        sa.src[r] = k < 0 ? -1 : k;
+        sa.base[r] = r < rows ? map->base[r] : 0.0;
+    }
+    hipError_t e = rvm::launch_logl(plan->dev, n_s0, nullptr, hill_factor, plan->slots, lnp_new_out, status_out,
+                                    nullptr, sa, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_half_step");
 }
 
 int rvm_stretch_propose(int32_t n_params, int32_t n_s0, int64_t s0_begin, const double* x, int32_t n_s1,

@@ -394,7 +394,7 @@ __device__ __forceinline__ void halley(double x, double beta, double r0, double 
     G1 = fma(-beta, G3, x);  // x c1 = x (1 - z c3)
     G0 = fma(-z, c2, 1.0);
     const double f = fma(GM, G3, fma(eta, G2, fma(r0, G1, -dt)));
-    fp = fma(GM, G2, fma(eta, G1, r0 * G0));
+    fp = fma(zeta, G2, fma(eta, G1, r0));  // r0 G0 + eta G1 + GM G2 with G0 = 1 - beta G2
     fpp = fma(zeta, G1, eta * G0);
     const double den = fma(-0.5 * f, fpp, fp * fp);
     const double num = f * fp;
@@ -484,7 +484,7 @@ __device__ __forceinline__ DriftOut drift_apply(const Lane<NP>& s, double dt, do
     const double gG2 = GM * H2;
     const double f_ = fma(-gG2, ir0, 1.0);
     const double g_ = fma(-GM, H3, dt);
-    const double fd = -(GM * H1) * (irr * ir0);
+    const double fd = -((GM * ir0) * H1) * irr;  // GM ir0: shared with the drift's guess
     const double gd = fma(-gG2, irr, 1.0);
     DriftOut o;
     o.rx = fma(f_, s.rx, g_ * s.vx);

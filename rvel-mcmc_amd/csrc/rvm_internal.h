@@ -31,6 +31,22 @@ struct DevPlan {
     DirSched fwd, bwd;
 };
 
+// Fused stretch half-step (rvm_stretch_half_step) by value as a kernel argument; c == nullptr
+// for a plain likelihood launch.
+struct StretchArgs {
+    const double* c;    // complement half [dim][n1]
+    double* x;          // this half's free parameters [dim][W] (accepted proposals written back)
+    double* lnp;        // their log-probabilities [W]
+    int32_t* accepted;  // accept counters [W] (nullable)
+    int64_t s0_begin;   // global index of walker 0 of x (Philox key)
+    uint64_t seed, iteration;
+    double a;
+    int32_t n1, dim;
+    uint32_t half;
+    int32_t src[RVM_MAX_PARAM_ROWS];  // rvm_param_map
+    double base[RVM_MAX_PARAM_ROWS];
+};
+
 // rvm_smala_cache by value as a kernel argument (same layout)
 struct SmalaCache {
     double* lp;

@@ -14,12 +14,16 @@
 //               lane, positions exchanged by DPP quad permutes for the kick); solver state in
 //               registers; the epoch schedule is wave-uniform (scalar loads); walker parameters
 //               are read once from SoA [n_params][n_walkers].
-// A second tiny kernel (finalize) combines the two directions: logl = -(chi2_b + chi2_f)/Npoints.
+// The second of a walker group's two direction blocks to finish combines them (atomic counter per
+// block column): logl = -(chi2_b + chi2_f)/Npoints.  With StretchArgs the same launch is a whole
+// emcee stretch half-step: the walkers' parameters are their proposals, formed in the prologue,
+// and the combining block runs the accept (rvm_stretch.h).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
 #include "rvm_device.h"
 #include "rvm_internal.h"
+#include "rvm_stretch.h"
 
 namespace rvm {
 
@@ -92,14 +96,35 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, double h, int ns, int& redo
     return false;
 }
 
+// kernel parameter row r of walker w: from the SoA input, or (fused stretch half-step) the row's
+// fixed value or the walker's proposal of the free parameter feeding it
+__device__ __forceinline__ double walker_param(bool stretch, const double* __restrict__ params, int W, int w,
+                                               const StretchArgs& sa, int r, double z, int j) {
+    if (!stretch) return params[(size_t)r * W + w];
+    const int k = sa.src[r];
+    if (k < 0) return sa.base[r];
+    return stretch_q(sa.c[(size_t)k * sa.n1 + j], z, sa.x[(size_t)k * W + w]);
+}
+
+__device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, int gi, int r, double v) {
+    if (stager) l_q[r * GW + gi] = v;
+    return v;
+}
+
+// Direction results meet in one 64-bit slot per walker (plan workspace, RVM_SLOT_EMPTY between
+// launches): chi2 >= 0 for an OK direction, -status otherwise.
+#define RVM_SLOT_EMPTY 0x7FF4DEADBEEF0001ULL  // a NaN pattern no direction result can take
+
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
 template <int NP, bool D3>
 __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                                                                    const double* __restrict__ params,
                                                                    const double hill_factor,
-                                                                   double* __restrict__ chi2_part,
-                                                                   int32_t* __restrict__ status_part,
-                                                                   double* __restrict__ rv_out) {
+                                                                   unsigned long long* __restrict__ slots,
+                                                                   double* __restrict__ rv_out,
+                                                                   double* __restrict__ logl_out,
+                                                                   int32_t* __restrict__ status_out,
+                                                                   const StretchArgs sa) {
     constexpr int L = LanesPerWalker<NP>::value;  // lanes per walker (one per planet)
     constexpr int WPB = 64 / L;                    // walkers per block (= per wave)
     PROF_T(t_start);
@@ -130,6 +155,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     int(*s_enc)[64] = s_enc_all[grp];
     // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
     extern __shared__ double s_sched[];  // [E] seg_h1 | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
+                                         // then, for a fused stretch half-step, [rows+3][G*WPB]
 
     const DirSched S = d ? P.bwd : P.fwd;
     // wave-uniform copies (SGPRs): the level's step divisor and Stumpff series length (rvm_device.h)
@@ -143,6 +169,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     double* l_s2 = s_sched + 2 * E;
     int* l_n = reinterpret_cast<int*>(s_sched + 3 * E);
     int* l_idx = l_n + E;
+    // fused stretch half-step: the proposal rows, z, u3 and the current lnp of every walker of the
+    // block, for the lane that finishes the walker (end of the kernel)
+    const int GW = G * WPB;
+    const int gi = grp * WPB + slot;  // walker slot within the block
+    double* l_q = s_sched + 4 * E;    // [rows][GW], then z | u3 | lnp0
     // first chunk of the schedule: loads issued now, stored to LDS after the setup below so their
     // latency hides behind the Pal conversion
     const int i0 = threadIdx.x;
@@ -157,19 +188,35 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     }
 
     // ---- walker parameters (m, a, h, k, l [, ix, iy] per planet), prior (state.py:299-315) -----
+    // Fused stretch half-step (sa.c != nullptr): the walker's parameters are its proposal
+    // q = c_j - z (c_j - x) mapped onto the kernel rows (rvm_stretch.h, rvm_param_map).
     constexpr int PR = D3 ? 7 : 5;  // parameter rows per planet
+    const bool stretch = sa.c != nullptr;
+    double zst = 0.0;
+    int jst = 0;
+    const bool stager = stretch && lvl == 0 && pl_idx == 0;  // one lane per walker stages for the end
+    if (stretch) {
+        stretch_draw(sa.seed, (uint64_t)(sa.s0_begin + wl), sa.iteration, sa.half, sa.a, sa.n1, zst, jst);
+        if (stager) {
+            constexpr int R = PR * NP;
+            l_q[R * GW + gi] = zst;
+            l_q[(R + 1) * GW + gi] = stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wl), sa.iteration, sa.half);
+            l_q[(R + 2) * GW + gi] = sa.lnp[wl];
+        }
+    }
+#define prm(r) stage_row(stager, l_q, GW, gi, (r), walker_param(stretch, params, W, wl, sa, (r), zst, jst))
     Lane<NP> s;
     double pa[NP], ph[NP], pk[NP], pl[NP], pix[NP], piy[NP];
     int status = RVM_STATUS_OK;
 #pragma unroll
     for (int p = 0; p < NP; p++) {
-        s.m[p] = params[(size_t)(PR * p + 0) * W + wl];
-        pa[p] = params[(size_t)(PR * p + 1) * W + wl];
-        ph[p] = params[(size_t)(PR * p + 2) * W + wl];
-        pk[p] = params[(size_t)(PR * p + 3) * W + wl];
-        pl[p] = params[(size_t)(PR * p + 4) * W + wl];
-        pix[p] = D3 ? params[(size_t)(PR * p + 5) * W + wl] : 0.0;
-        piy[p] = D3 ? params[(size_t)(PR * p + 6) * W + wl] : 0.0;
+        s.m[p] = prm(PR * p + 0);
+        pa[p] = prm(PR * p + 1);
+        ph[p] = prm(PR * p + 2);
+        pk[p] = prm(PR * p + 3);
+        pl[p] = prm(PR * p + 4);
+        pix[p] = D3 ? prm(PR * p + 5) : 0.0;
+        piy[p] = D3 ? prm(PR * p + 6) : 0.0;
         bool bad = !(pa[p] > 0.02) || !(s.m[p] > 5e-6) || !(ph[p] * ph[p] + pk[p] * pk[p] < 1.0) ||
                    !isfinite(pl[p]);
         if constexpr (D3) bad = bad || !(pix[p] * pix[p] + piy[p] * piy[p] < 4.0);  // state.py:311-313
@@ -338,6 +385,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         t_epo += tc - tb;
 #endif
     }
+#undef prm
     if (pl_idx == 0) s_enc[lvl][slot] = (int)((s.encm >> lane) & 1) | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
     if (lvl == 0 && lane < WPB) {
@@ -348,8 +396,36 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             int st = (enc & 2) ? RVM_STATUS_PRIOR : RVM_STATUS_OK;
             if (st == RVM_STATUS_OK && (enc & 1)) st = RVM_STATUS_ENCOUNTER;
             if (st == RVM_STATUS_OK && !isfinite(chi2)) st = RVM_STATUS_NONFINITE;
-            chi2_part[(size_t)d * W + wo] = chi2;
-            status_part[(size_t)d * W + wo] = st;
+            // ---- the two directions of a walker meet: the second to arrive finishes it ----------
+            // (one agent-scope exchange carries the other direction's result: no fence, no barrier)
+            const double mine = st == RVM_STATUS_OK ? chi2 : -(double)st;
+            const unsigned long long old = __hip_atomic_exchange(
+                slots + wo, (unsigned long long)__double_as_longlong(mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old != RVM_SLOT_EMPTY) {
+                __hip_atomic_store(slots + wo, RVM_SLOT_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const double other = __longlong_as_double((long long)old);
+                const int st_o = other < 0.0 ? (int)(-other) : RVM_STATUS_OK;
+                const int sf = d == 0 ? st : st_o, sb = d == 0 ? st_o : st;
+                const double cf = d == 0 ? chi2 : other, cb = d == 0 ? other : chi2;
+                int stw = sf != RVM_STATUS_OK ? sf : sb;  // both directions see the same PRIOR verdict
+                const double lp0 = -((cb + cf) / P.npoints);  // state.py:98, 109
+                if (stw == RVM_STATUS_OK && !isfinite(lp0)) stw = RVM_STATUS_NONFINITE;
+                const double lp = stw == RVM_STATUS_OK ? lp0 : -INFINITY;
+                if (logl_out) logl_out[wo] = lp;
+                if (status_out) status_out[wo] = stw;
+                if (stretch) {  // emcee accept with the proposal staged in the prologue
+                    constexpr int R = PR * NP;
+                    const int gl = grp * WPB + lane;
+                    const double z = l_q[R * GW + gl], u3 = l_q[(R + 1) * GW + gl];
+                    if (stretch_accepts(sa.dim, z, lp, l_q[(R + 2) * GW + gl], u3)) {
+#pragma unroll
+                        for (int r = 0; r < R; r++)
+                            if (sa.src[r] >= 0) sa.x[(size_t)sa.src[r] * W + wo] = l_q[r * GW + gl];
+                        sa.lnp[wo] = lp;
+                        if (sa.accepted) sa.accepted[wo] += 1;
+                    }
+                }
+            }
         }
     }
 #ifdef RVM_PROFILE
@@ -372,21 +448,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #endif
 }
 
-__global__ void finalize_kernel(const int W, const double npoints, const double* __restrict__ chi2_part,
-                                const int32_t* __restrict__ status_part, double* __restrict__ logl,
-                                int32_t* __restrict__ status) {
-    const int w = blockIdx.x * blockDim.x + threadIdx.x;
-    if (w >= W) return;
-    const int sf = status_part[w], sb = status_part[W + w];
-    int st = sf != RVM_STATUS_OK ? sf : sb;
-    double lp = -((chi2_part[W + w] + chi2_part[w]) / npoints);  // state.py:98, 109
-    if (st == RVM_STATUS_OK && !isfinite(lp)) st = RVM_STATUS_NONFINITE;
-    logl[w] = st == RVM_STATUS_OK ? lp : -INFINITY;
-    status[w] = st;
-}
-
-hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, double* chi2_part,
-                       int32_t* status_part, double* logl, int32_t* status, double* rv_out, hipStream_t stream) {
+hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
+                       double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
     const int lpw = P.n_planets == 1 ? 1 : (P.n_planets == 2 ? 2 : 4);  // LanesPerWalker
     const int wpb = 64 / lpw;
     const int groups = (W + wpb - 1) / wpb;
@@ -397,9 +460,10 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
     const dim3 grid((groups + G - 1) / G, 2);
     const dim3 block(64 * P.n_levels * G);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
-    const size_t smem = (size_t)emax * (3 * sizeof(double) + 2 * sizeof(int32_t)) + 16;
+    const size_t rows = (size_t)(P.inclined ? 7 : 5) * P.n_planets;
+    const size_t smem = (size_t)emax * 4 * sizeof(double) + (sa.c ? (rows + 3) * G * wpb * sizeof(double) : 0);
 #define RVM_LAUNCH(NPV, D3V) \
-    logl_kernel<NPV, D3V><<<grid, block, smem, stream>>>(P, W, params, hill_factor, chi2_part, status_part, rv_out)
+    logl_kernel<NPV, D3V><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, logl, status, sa)
     const bool inc = P.inclined != 0;
     switch (P.n_planets) {
         case 1:
@@ -418,9 +482,6 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
             return hipErrorInvalidValue;
     }
 #undef RVM_LAUNCH
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return err;
-    finalize_kernel<<<(W + 255) / 256, 256, 0, stream>>>(W, P.npoints, chi2_part, status_part, logl, status);
     return hipGetLastError();
 }
 

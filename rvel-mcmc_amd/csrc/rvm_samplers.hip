@@ -12,6 +12,7 @@
 
 #include "rvm_device.h"
 #include "rvm_internal.h"
+#include "rvm_stretch.h"
 
 // No FMA contraction in the sampler arithmetic: proposals and accept tests are then bit-identical
 // to a plain IEEE restatement (numpy) fed the same random numbers.
@@ -19,33 +20,19 @@
 
 namespace rvm {
 
-enum : uint32_t {
-    RNG_STRETCH_PROPOSE = 1,
-    RNG_STRETCH_ACCEPT = 2,
-    RNG_MH_PROPOSE = 3,
-    RNG_MH_ACCEPT = 4,
-};
-
 __global__ void stretch_propose_kernel(int P, int n0, int64_t s0_begin, const double* __restrict__ x, int n1,
                                        const double* __restrict__ c, double a, uint64_t seed, uint64_t iteration,
                                        uint32_t half, const double* __restrict__ draws, double* __restrict__ q,
                                        double* __restrict__ zout) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n0) return;
-    double u1, u2;
-    if (draws) {
-        u1 = draws[i];
-        u2 = draws[n0 + i];
-    } else {
-        uniform2(seed, (uint64_t)(s0_begin + i), iteration, RNG_STRETCH_PROPOSE | (half << 8), u1, u2);
-    }
-    const double z = ((a - 1.0) * u1 + 1.0) * ((a - 1.0) * u1 + 1.0) / a;
-    int j = (int)floor(u2 * (double)n1);
-    j = j < 0 ? 0 : (j >= n1 ? n1 - 1 : j);
-    for (int p = 0; p < P; p++) {
-        const double cj = c[(size_t)p * n1 + j];
-        q[(size_t)p * n0 + i] = cj - z * (cj - x[(size_t)p * n0 + i]);
-    }
+    double z;
+    int j;
+    if (draws)
+        stretch_zj(draws[i], draws[n0 + i], a, n1, z, j);
+    else
+        stretch_draw(seed, (uint64_t)(s0_begin + i), iteration, half, a, n1, z, j);
+    for (int p = 0; p < P; p++) q[(size_t)p * n0 + i] = stretch_q(c[(size_t)p * n1 + j], z, x[(size_t)p * n0 + i]);
     zout[i] = z;
 }
 
@@ -56,15 +43,8 @@ __global__ void stretch_accept_kernel(int P, int n0, int64_t s0_begin, double* _
                                       const double* __restrict__ draws, int32_t* __restrict__ accepted) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n0) return;
-    double u3, unused;
-    if (draws) {
-        u3 = draws[i];
-    } else {
-        uniform2(seed, (uint64_t)(s0_begin + i), iteration, RNG_STRETCH_ACCEPT | (half << 8), u3, unused);
-    }
-    // emcee 2.2.1: lnpdiff = (dim - 1) * log(zz) + newlnprob - lnprob0 ; accept = lnpdiff > log(rand)
-    const double lnpdiff = (double)(P - 1) * log(z[i]) + lnp_new[i] - lnp[i];
-    if (lnpdiff > log(u3)) {
+    const double u3 = draws ? draws[i] : stretch_u3(seed, (uint64_t)(s0_begin + i), iteration, half);
+    if (stretch_accepts(P, z[i], lnp_new[i], lnp[i], u3)) {
         for (int p = 0; p < P; p++) x[(size_t)p * n0 + i] = q[(size_t)p * n0 + i];
         lnp[i] = lnp_new[i];
         if (accepted) accepted[i] += 1;

@@ -175,6 +175,28 @@ class LoglPlan:
         _lib.check(rc, "rvm_logl_batch")
         return out, status, (rv_out if want_rv else None)
 
+    def stretch_half_step(self, pmap, X0, lnp0, c, s0_begin, a, seed, iteration, half, hill_factor=1.0,
+                          lnp_new=None, status=None, accepted=None, stream=None):
+        """Fused emcee stretch half-step (rvm_stretch_half_step): propose against the complement
+        c [dim][n1], walker logL of the proposals, accept -- one launch.  X0 [dim][n0] and lnp0
+        [n0] are updated in place; lnp_new / status (optional) receive the proposals' logl."""
+        torch = _torch()
+        for t in (X0, lnp0, c):
+            if t.dtype != torch.float64 or t.device != self.device or not t.is_contiguous():
+                raise ValueError("X0, lnp0, c must be contiguous float64 tensors on the plan's device")
+        dim, n0 = X0.shape
+        if c.shape[0] != dim or lnp0.shape != (n0,):
+            raise ValueError("shape mismatch between X0, lnp0 and c")
+        if n0 > self.max_walkers:
+            raise ValueError(f"{n0} walkers exceed the plan's max_walkers={self.max_walkers}")
+        with torch.cuda.device(self.device):
+            rc = self.lib.rvm_stretch_half_step(
+                self._h, C.byref(pmap.c_map()), dim, n0, int(s0_begin), X0.data_ptr(), lnp0.data_ptr(), c.shape[1],
+                c.data_ptr(), float(a), int(seed), int(iteration), int(half), float(hill_factor),
+                lnp_new.data_ptr() if lnp_new is not None else 0, status.data_ptr() if status is not None else 0,
+                accepted.data_ptr() if accepted is not None else 0, _lib.stream_handle(stream))
+        _lib.check(rc, "rvm_stretch_half_step")
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self.lib.rvm_plan_destroy(self._h)
@@ -263,6 +285,19 @@ class ParamMap:
         if self.n_free:
             K.index_copy_(0, slots, X)
         return K
+
+    def c_map(self):
+        """rvm_param_map for the fused stretch half-step (row -> free index, or fixed value)."""
+        if getattr(self, "_c_map", None) is None:
+            m = _lib.ParamMapC()
+            m.n_rows = len(self.base)
+            for r in range(_lib.RVM_MAX_PARAM_ROWS):
+                m.src[r] = -1
+                m.base[r] = float(self.base[r]) if r < len(self.base) else 0.0
+            for k, r in enumerate(self.slots.tolist()):
+                m.src[r] = k
+            self._c_map = m
+        return self._c_map
 
     def vector_to_kernel_np(self, x):
         k = self.base.copy()

@@ -71,6 +71,22 @@ class DeviceOps:
             self.status_counts.index_add_(0, st.long(), torch.ones_like(st, dtype=torch.int64))
         return lp, st
 
+    def fused_half_step(self, X0, lnp0, c, half, lnp_new, status, accepted):
+        """propose + logl + accept in one likelihood launch (rvm_stretch_half_step), bit-identical
+        to the three-launch sequence with Philox draws."""
+        torch = _torch()
+        s = self.s
+        if self.timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        self.plan.stretch_half_step(s.pmap, X0, lnp0, c.contiguous(), s.global_begin(half), s.a, s.seed, s.iteration,
+                                    half, s.hill_factor, lnp_new=lnp_new, status=status, accepted=accepted)
+        if self.timing is not None:
+            e1.record()
+            self.timing.append((e0, e1, X0.shape[1]))
+        if self.track_status:
+            self.status_counts.index_add_(0, status.long(), torch.ones_like(status, dtype=torch.int64))
+
     def accept(self, X0, lnp0, q, lnp_new, z, half, accepted, draws=None):
         s = self.s
         _lib.check(self.lib.rvm_stretch_accept(s.dim, s.nloc, s.global_begin(half), X0.data_ptr(), lnp0.data_ptr(),
@@ -121,6 +137,9 @@ class EnsembleSampler:
         self._gather = torch.empty(self.world * dim * n, **f64) if self.world > 1 else None
         self.naccepted = torch.zeros(2 * n, dtype=torch.int32, device=self.device)
         self.nevals = 0
+        # one launch per half-step (rvm_stretch_half_step) unless draws are injected or the ops
+        # (e.g. the CPU restatements of the distributed tests) provide only the three-step path
+        self.fused = hasattr(self.ops, "fused_half_step")
 
     @property
     def timing(self):
@@ -158,6 +177,11 @@ class EnsembleSampler:
         """Update this rank's slice X0 [dim][nloc] (in place) against the complement half."""
         c = self._complement(Xc)
         n = self.nloc
+        if self.fused and draws_propose is None and draws_accept is None:
+            self.ops.fused_half_step(X0, lnp0, c, half, self._lnp_new, self._status,
+                                     self.naccepted[half * n:(half + 1) * n])
+            self.nevals += n
+            return
         self.ops.propose(X0, c, half, self._q, self._z, draws_propose)
         self.lnprob(self._q, out=self._lnp_new, status=self._status)
         self.ops.accept(X0, lnp0, self._q, self._lnp_new, self._z, half, self.naccepted[half * n:(half + 1) * n],

@@ -11,18 +11,26 @@ import sys
 from collections import defaultdict
 
 d, W = sys.argv[1], int(sys.argv[2])
+skip = int(sys.argv[3]) if len(sys.argv) > 3 else 0      # leading logl dispatches to drop per pass
+what = sys.argv[4] if len(sys.argv) > 4 else "likelihood launch"
 vals = defaultdict(list)
 for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-    for row in csv.DictReader(open(f)):
-        if "logl_kernel" not in row.get("Kernel_Name", ""):
-            continue
-        vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+    rows = [r for r in csv.DictReader(open(f)) if "logl_kernel" in r.get("Kernel_Name", "")]
+    ids = sorted({int(r["Dispatch_Id"]) for r in rows})[skip:]
+    keep = set(ids)
+    # sum the per-dimension rows of each (dispatch, counter), then collect per counter
+    acc = defaultdict(float)
+    for r in rows:
+        if int(r["Dispatch_Id"]) in keep:
+            acc[(int(r["Dispatch_Id"]), r["Counter_Name"])] += float(r["Counter_Value"])
+    for (_, name), v in acc.items():
+        vals[name].append(v)
 # each dispatch appears once per counter (values already summed over XCDs/SEs by rocprofv3 when
 # the counter is a _sum; otherwise one row per dimension instance -> accumulate per dispatch)
 per = {}
 for k, v in vals.items():
     per[k] = v
-out = {"walkers_per_launch": W, "kernel": "rvm::logl_kernel<2>"}
+out = {"walkers_per_launch": W, "kernel": "rvm::logl_kernel<2>", "launch": what}
 def mean(k):
     v = per.get(k)
     return sum(v) / len(v) if v else None

@@ -19,7 +19,7 @@ def test_header_declares_expected_surface():
     fns = header_functions()
     for f in ("rvm_plan_create", "rvm_logl_batch", "rvm_stretch_propose", "rvm_stretch_accept",
               "rvm_mh_propose", "rvm_mh_accept", "rvm_fd_params", "rvm_smala_derive", "rvm_smala_propose",
-              "rvm_smala_accept", "rvm_last_error", "rvm_abi_version"):
+              "rvm_smala_accept", "rvm_stretch_half_step", "rvm_last_error", "rvm_abi_version"):
         assert f in fns
 
 
@@ -27,7 +27,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == 3
+    assert lib.rvm_abi_version() == 4
 
 
 def test_python_binding_matches_header():
@@ -44,6 +44,8 @@ def test_argument_errors_do_not_touch_the_device():
     rc = lib.rvm_plan_create(C.byref(cfg), z, z, z, 1, 64, C.byref(h))
     assert rc < 0 and b"n_planets" in lib.rvm_last_error()
     assert lib.rvm_logl_batch(None, 1, 0, 1.0, 0, 0, 0, 0) < 0
+    m = _lib.ParamMapC()
+    assert lib.rvm_stretch_half_step(None, C.byref(m), 10, 1, 0, 0, 0, 1, 0, 2.0, 0, 0, 0, 1.0, 0, 0, 0, 0) < 0
 
 
 def test_struct_layouts_match_header():
@@ -55,3 +57,33 @@ def test_struct_layouts_match_header():
     assert C.sizeof(_lib.RvmConfig) == 72 and _lib.RvmConfig.inclined.offset == 64
     assert _lib.RvmConfig.level_mult.offset == 32 and _lib.RvmConfig.period_hint.offset == 56
     assert C.sizeof(_lib.SmalaCache) == 7 * 8
+
+
+def test_struct_layouts_match_compiled_header(tmp_path):
+    """The same layouts as gcc sees them when compiling include/rvmcmc.h."""
+    import ctypes as C
+    import shutil
+    import subprocess
+
+    import pytest
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    src = tmp_path / "layout.c"
+    src.write_text("""
+#include <stddef.h>
+#include <stdio.h>
+#include "rvmcmc.h"
+int main(void) {
+    printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(rvm_config), offsetof(rvm_config, level_mult),
+           offsetof(rvm_config, inclined), sizeof(rvm_smala_cache), sizeof(rvm_param_map),
+           offsetof(rvm_param_map, src), offsetof(rvm_param_map, base));
+    return 0;
+}
+""")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert got == [C.sizeof(_lib.RvmConfig), _lib.RvmConfig.level_mult.offset, _lib.RvmConfig.inclined.offset,
+                   C.sizeof(_lib.SmalaCache), C.sizeof(_lib.ParamMapC), _lib.ParamMapC.src.offset,
+                   _lib.ParamMapC.base.offset]
