@@ -30,6 +30,13 @@ enum : uint32_t {
     RNG_SMALA_ACCEPT = 6,
 };
 
+// butterfly sum over the wave: every lane ends with the same bits (each step adds the same pair)
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
 // One wave per chain: the P x P matrices live in LDS, lanes own matrix rows / entries, and the
 // sequential parts (Jacobi rotations, Cholesky columns) run lock-step across the wave.
 __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, const double* __restrict__ x,
@@ -44,7 +51,10 @@ __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, c
     constexpr int PER_LANE = (NTRI + 63) / 64;     // accumulators per lane
     __shared__ double A[PM * PM], Qm[PM * PM];
     __shared__ double den[PM], gr[PM], lt[PM], inv[PM], xv[PM];
-    __shared__ double Jc[64];
+    __shared__ double ra[PM], rb[PM], dn[PM];
+    __shared__ int rp[PM];
+    constexpr int JCH = 64;                        // epochs per J chunk
+    __shared__ double Jc[JCH * PM], wc[JCH];
     __shared__ int okflag;
     const int c = blockIdx.x;
     const int lane = threadIdx.x;
@@ -84,23 +94,24 @@ __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, c
         tq[j] = p + rem;
         acc[j] = 0.0;
     }
-    const int K = 64 / P;
-    for (int e0 = 0; e0 < E; e0 += K) {
-        {
-            const int k = lane / P, p = lane % P;
-            const int e = e0 + k;
-            if (k < K && e < E) {
-                const double* re = rv + (size_t)e * SC;
-                Jc[lane] = (re[(size_t)(1 + 2 * p) * C + c] - re[(size_t)(2 + 2 * p) * C + c]) / den[p];
-            }
+    // J in chunks of JCH epochs: every lane issues its loads of the chunk at once (the chunk's
+    // latency is paid once, not once per epoch), then the triangle accumulates from LDS
+    for (int e0 = 0; e0 < E; e0 += JCH) {
+        const int kmax = E - e0 < JCH ? E - e0 : JCH;
+        const int n = kmax * P;
+#pragma unroll 4
+        for (int idx = lane; idx < n; idx += 64) {
+            const int k = idx / P, p = idx - (idx / P) * P;
+            const double* re = rv + (size_t)(e0 + k) * SC;
+            Jc[idx] = (re[(size_t)(1 + 2 * p) * C + c] - re[(size_t)(2 + 2 * p) * C + c]) / den[p];
         }
+        if (lane < kmax) wc[lane] = w[e0 + lane];
         __syncthreads();
-        const int kmax = E - e0 < K ? E - e0 : K;
 #pragma unroll
         for (int j = 0; j < PER_LANE; j++) {
             if (lane + 64 * j < ntri) {
                 double a = acc[j];
-                for (int k = 0; k < kmax; k++) a += (Jc[k * P + tp[j]] * w[e0 + k]) * Jc[k * P + tq[j]];
+                for (int k = 0; k < kmax; k++) a += (Jc[k * P + tp[j]] * wc[k]) * Jc[k * P + tq[j]];
                 acc[j] = a;
             }
         }
@@ -117,53 +128,89 @@ __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, c
     }
     for (int i = lane; i < P * P; i += 64) Qm[i] = (i / P == i % P) ? 1.0 : 0.0;
     __syncthreads();
-    // cyclic Jacobi: A -> diag(lambda), Q -> eigenvectors (A = Q diag(lambda) Q^T).  Every lane
-    // computes the rotation from the same LDS values; lane r updates row/column r.
-    for (int sweep = 0; sweep < 60; sweep++) {
-        double off = 0.0, dia = 0.0;
-        for (int i = 0; i < P; i++) {
-            dia += A[i * P + i] * A[i * P + i];
-            for (int j = i + 1; j < P; j++) off += A[i * P + j] * A[i * P + j];
-        }
-        if (!(off > 1e-32 * dia)) break;  // converged (or NaN: caught by the SoftAbs check)
-        for (int p = 0; p < P - 1; p++) {
-            for (int q = p + 1; q < P; q++) {
-                const double apq = A[p * P + q];
-                if (apq == 0.0) continue;
-                const double app = A[p * P + p], aqq = A[q * P + q];
-                const double theta = (aqq - app) / (2.0 * apq);
-                double tt = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-                if (theta < 0.0) tt = -tt;
-                const double cs = 1.0 / sqrt(tt * tt + 1.0);
-                const double sn = tt * cs;
-                const double tau = sn / (1.0 + cs);
-                double nrp = 0.0, nrq = 0.0, qnp = 0.0, qnq = 0.0;
-                const int r = lane;
-                if (r < P) {
-                    const double qrp = Qm[r * P + p], qrq = Qm[r * P + q];
-                    qnp = qrp - sn * (qrq + tau * qrp);
-                    qnq = qrq + sn * (qrp - tau * qrq);
-                    if (r != p && r != q) {
-                        const double arp = A[r * P + p], arq = A[r * P + q];
-                        nrp = arp - sn * (arq + tau * arp);
-                        nrq = arq + sn * (arp - tau * arq);
+    // Jacobi eigen-solver, parallel (round-robin) ordering: A -> diag(lambda), Q -> eigenvectors
+    // (A = Q diag(lambda) Q^T).  A sweep is N2-1 rounds (N2 = P rounded up to even); each round
+    // applies N2/2 disjoint rotations at once (pair (p, q) zeroes A_pq as in the classic cyclic
+    // method), so a sweep costs N2-1 barrier rounds instead of P(P-1)/2 sequential rotations.
+    // Lanes own matrix entries: A' = J^T A J and Q' = Q J entry by entry, column i of J being
+    // ra[i] e_i + rb[i] e_rp[i].
+    {
+        constexpr int EPL = (PM * PM + 63) / 64;  // matrix entries per lane
+        const int N2 = (P + 1) & ~1;
+        const int PP = P * P;
+        for (int sweep = 0; sweep < 60; sweep++) {
+            double off = 0.0, dia = 0.0;
+            for (int idx = lane; idx < PP; idx += 64) {
+                const int i = idx / P, j = idx - (idx / P) * P;
+                const double v = A[idx];
+                if (i == j) dia += v * v;
+                else if (i < j) off += v * v;
+            }
+            off = wave_sum(off);
+            dia = wave_sum(dia);
+            if (!(off > 1e-32 * dia)) break;  // converged (or NaN: caught by the SoftAbs check)
+            for (int r = 0; r < N2 - 1; r++) {
+                if (lane < N2 / 2) {
+                    int a, b;
+                    if (lane == 0) {
+                        a = r;
+                        b = N2 - 1;
+                    } else {
+                        a = (r + lane) % (N2 - 1);
+                        b = (r - lane + N2 - 1) % (N2 - 1);
+                    }
+                    const int p = a < b ? a : b, q = a < b ? b : a;
+                    if (q < P) {
+                        const double apq = A[p * P + q], app = A[p * P + p], aqq = A[q * P + q];
+                        double cs = 1.0, sn = 0.0, tt = 0.0;
+                        if (apq != 0.0) {
+                            const double theta = (aqq - app) / (2.0 * apq);
+                            tt = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+                            if (theta < 0.0) tt = -tt;
+                            cs = 1.0 / sqrt(tt * tt + 1.0);
+                            sn = tt * cs;
+                        }
+                        ra[p] = cs;
+                        rb[p] = -sn;
+                        rp[p] = q;
+                        ra[q] = cs;
+                        rb[q] = sn;
+                        rp[q] = p;
+                        dn[p] = app - tt * apq;
+                        dn[q] = aqq + tt * apq;
+                    } else if (p < P) {  // paired with the padding index: untouched this round
+                        ra[p] = 1.0;
+                        rb[p] = 0.0;
+                        rp[p] = p;
+                        dn[p] = A[p * P + p];
                     }
                 }
                 __syncthreads();
-                if (r < P) {
-                    Qm[r * P + p] = qnp;
-                    Qm[r * P + q] = qnq;
-                    if (r != p && r != q) {
-                        A[r * P + p] = nrp;
-                        A[p * P + r] = nrp;
-                        A[r * P + q] = nrq;
-                        A[q * P + r] = nrq;
-                    } else if (r == p) {
-                        A[p * P + p] = app - tt * apq;
-                        A[p * P + q] = 0.0;
-                        A[q * P + p] = 0.0;
-                    } else {
-                        A[q * P + q] = aqq + tt * apq;
+                double na[EPL], nq[EPL];
+#pragma unroll
+                for (int k = 0; k < EPL; k++) {
+                    const int idx = lane + 64 * k;
+                    if (idx < PP) {
+                        const int i = idx / P, j = idx - (idx / P) * P;
+                        const int ip = rp[i], jp = rp[j];
+                        const double ai = ra[i], bi = rb[i], aj = ra[j], bj = rb[j];
+                        if (i == j)
+                            na[k] = dn[i];
+                        else if (ip == j)
+                            na[k] = 0.0;  // the pair this round zeroes
+                        else
+                            na[k] = ((ai * aj) * A[i * P + j] + (ai * bj) * A[i * P + jp]) +
+                                    ((bi * aj) * A[ip * P + j] + (bi * bj) * A[ip * P + jp]);
+                        nq[k] = aj * Qm[i * P + j] + bj * Qm[i * P + jp];
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < EPL; k++) {
+                    const int idx = lane + 64 * k;
+                    if (idx < PP) {
+                        A[idx] = na[k];
+                        Qm[idx] = nq[k];
                     }
                 }
                 __syncthreads();
@@ -244,52 +291,54 @@ __device__ __forceinline__ double box_muller_s(double u0, double u1) {
     return sqrt(-2.0 * log(u0)) * cospi(2.0 * u1);
 }
 
-__global__ void smala_propose_kernel(int P, int C, int64_t begin, const double* __restrict__ x, SmalaCache cur,
-                                     double eps, uint64_t seed, uint64_t iteration, const double* __restrict__ draws,
-                                     double* __restrict__ xs) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// One wave per chain: lane p draws z_p, then x*_p = mu_p + eps sum_{q<=p} L_pq z_q (mcmc.py:151).
+__global__ __launch_bounds__(64) void smala_propose_kernel(int P, int C, int64_t begin, const double* __restrict__ x,
+                                                           SmalaCache cur, double eps, uint64_t seed,
+                                                           uint64_t iteration, const double* __restrict__ draws,
+                                                           double* __restrict__ xs) {
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    __shared__ double zs[RVM_SMALA_MAX_PARAMS];
     if (!cur.ok[c]) {  // no usable metric at x: stay (the proposal is then rejected)
-        for (int p = 0; p < P; p++) xs[(size_t)p * C + c] = x[(size_t)p * C + c];
+        if (lane < P) xs[(size_t)lane * C + c] = x[(size_t)lane * C + c];
         return;
     }
-    double z[RVM_SMALA_MAX_PARAMS];
-    for (int p = 0; p < P; p++) {
+    if (lane < P) {
+        double z;
         if (draws) {
-            z[p] = draws[(size_t)p * C + c];
+            z = draws[(size_t)lane * C + c];
         } else {
             double u0, u1;
-            uniform2(seed, (uint64_t)(begin + c), iteration, RNG_SMALA_PROPOSE | ((uint32_t)p << 8), u0, u1);
-            z[p] = box_muller_s(u0, u1);
+            uniform2(seed, (uint64_t)(begin + c), iteration, RNG_SMALA_PROPOSE | ((uint32_t)lane << 8), u0, u1);
+            z = box_muller_s(u0, u1);
         }
+        zs[lane] = z;
     }
-    // mcmc.py:151: newparams = mu + eps * chol(G^-1) . N(0,1)
-    for (int p = 0; p < P; p++) {
+    __syncthreads();
+    if (lane < P) {
         double s = 0.0;
-        for (int q = 0; q <= p; q++) s += cur.L[(size_t)(p * P + q) * C + c] * z[q];
-        xs[(size_t)p * C + c] = cur.mu[(size_t)p * C + c] + eps * s;
+        for (int q = 0; q <= lane; q++) s += cur.L[(size_t)(lane * P + q) * C + c] * zs[q];
+        xs[(size_t)lane * C + c] = cur.mu[(size_t)lane * C + c] + eps * s;
     }
 }
 
 // log N(y; mu, eps^2 G^-1) = -1/2 [ (y-mu)^T G (y-mu) / eps^2 + P log eps^2 + log det G^-1 + P log 2 pi ]
-__device__ __forceinline__ double mvn_logpdf(int P, int C, int c, const double* y, const double* mu, const double* G,
-                                             double logdet, double eps) {
-    double maha = 0.0;
-    for (int p = 0; p < P; p++) {
-        const double dp = y[(size_t)p * C + c] - mu[(size_t)p * C + c];
-        double s = 0.0;
-        for (int q = 0; q < P; q++) s += G[(size_t)(p * P + q) * C + c] * (y[(size_t)q * C + c] - mu[(size_t)q * C + c]);
-        maha += dp * s;
-    }
+// given maha = (y-mu)^T G (y-mu)
+__device__ __forceinline__ double mvn_logpdf(int P, double maha, double logdet, double eps) {
     return -0.5 * (maha / (eps * eps) + (double)P * log(eps * eps) + logdet + (double)P * log(2.0 * M_PI));
 }
 
-__global__ void smala_accept_kernel(int P, int C, int64_t begin, double* __restrict__ x, SmalaCache cur,
-                                    const double* __restrict__ xs, SmalaCache prop, double eps, uint64_t seed,
-                                    uint64_t iteration, const double* __restrict__ draws, int32_t* __restrict__ accepted,
-                                    int32_t* __restrict__ failures) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+// One wave per chain: both Mahalanobis forms with the matrix entries spread over the lanes, then
+// the accept (mcmc.py:167-187) and, on accept, the proposal's cached derivatives copied in parallel.
+__global__ __launch_bounds__(64) void smala_accept_kernel(int P, int C, int64_t begin, double* __restrict__ x,
+                                                          SmalaCache cur, const double* __restrict__ xs,
+                                                          SmalaCache prop, double eps, uint64_t seed,
+                                                          uint64_t iteration, const double* __restrict__ draws,
+                                                          int32_t* __restrict__ accepted,
+                                                          int32_t* __restrict__ failures) {
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    __shared__ double d1[RVM_SMALA_MAX_PARAMS], d2[RVM_SMALA_MAX_PARAMS];
     double u, unused;
     if (draws) {
         u = draws[c];
@@ -298,26 +347,42 @@ __global__ void smala_accept_kernel(int P, int C, int64_t begin, double* __restr
     }
     const bool okc = cur.ok[c] != 0, okp = prop.ok[c] != 0;
     const double lpp = prop.lp[c];
-    if (failures && !okp && isfinite(lpp)) failures[c] += 1;  // metric failure with a finite logp
+    if (lane == 0 && failures && !okp && isfinite(lpp)) failures[c] += 1;  // metric failure, finite logp
     if (!(okc && okp && isfinite(lpp))) return;
+    if (lane < P) {
+        d1[lane] = xs[(size_t)lane * C + c] - cur.mu[(size_t)lane * C + c];  // x* under q(.|x)
+        d2[lane] = x[(size_t)lane * C + c] - prop.mu[(size_t)lane * C + c];  // x under q(.|x*)
+    }
+    __syncthreads();
+    double m1 = 0.0, m2 = 0.0;
+    for (int idx = lane; idx < P * P; idx += 64) {
+        const int p = idx / P, q = idx - (idx / P) * P;
+        m1 += d1[p] * (cur.G[(size_t)idx * C + c] * d1[q]);
+        m2 += d2[p] * (prop.G[(size_t)idx * C + c] * d2[q]);
+    }
+    m1 = wave_sum(m1);
+    m2 = wave_sum(m2);
     // mcmc.py:176-181: ratio = exp(logp* - logp + log q(x|x*) - log q(x*|x)) > uniform
-    const double q_ts_t = mvn_logpdf(P, C, c, xs, cur.mu, cur.G, cur.logdet[c], eps);
-    const double q_t_ts = mvn_logpdf(P, C, c, x, prop.mu, prop.G, prop.logdet[c], eps);
+    const double q_ts_t = mvn_logpdf(P, m1, cur.logdet[c], eps);
+    const double q_t_ts = mvn_logpdf(P, m2, prop.logdet[c], eps);
     const double ratio = exp(lpp - cur.lp[c] + q_t_ts - q_ts_t);
     if (!(ratio > u)) return;
-    for (int p = 0; p < P; p++) {
-        x[(size_t)p * C + c] = xs[(size_t)p * C + c];
-        cur.mu[(size_t)p * C + c] = prop.mu[(size_t)p * C + c];
-        cur.grad[(size_t)p * C + c] = prop.grad[(size_t)p * C + c];
+    __syncthreads();  // every lane has read cur.* before it is overwritten
+    if (lane < P) {
+        x[(size_t)lane * C + c] = xs[(size_t)lane * C + c];
+        cur.mu[(size_t)lane * C + c] = prop.mu[(size_t)lane * C + c];
+        cur.grad[(size_t)lane * C + c] = prop.grad[(size_t)lane * C + c];
     }
-    for (int i = 0; i < P * P; i++) {
+    for (int i = lane; i < P * P; i += 64) {
         cur.L[(size_t)i * C + c] = prop.L[(size_t)i * C + c];
         cur.G[(size_t)i * C + c] = prop.G[(size_t)i * C + c];
     }
-    cur.lp[c] = lpp;
-    cur.logdet[c] = prop.logdet[c];
-    cur.ok[c] = 1;
-    if (accepted) accepted[c] += 1;
+    if (lane == 0) {
+        cur.lp[c] = lpp;
+        cur.logdet[c] = prop.logdet[c];
+        cur.ok[c] = 1;
+        if (accepted) accepted[c] += 1;
+    }
 }
 
 hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,
@@ -329,15 +394,14 @@ hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel,
 
 hipError_t launch_smala_propose(int P, int C, int64_t begin, const double* x, const SmalaCache& cur, double eps,
                                 uint64_t seed, uint64_t it, const double* draws, double* xs, hipStream_t st) {
-    smala_propose_kernel<<<(C + 127) / 128, 128, 0, st>>>(P, C, begin, x, cur, eps, seed, it, draws, xs);
+    smala_propose_kernel<<<C, 64, 0, st>>>(P, C, begin, x, cur, eps, seed, it, draws, xs);
     return hipGetLastError();
 }
 
 hipError_t launch_smala_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
                                const SmalaCache& prop, double eps, uint64_t seed, uint64_t it, const double* draws,
                                int32_t* accepted, int32_t* failures, hipStream_t st) {
-    smala_accept_kernel<<<(C + 127) / 128, 128, 0, st>>>(P, C, begin, x, cur, xs, prop, eps, seed, it, draws,
-                                                         accepted, failures);
+    smala_accept_kernel<<<C, 64, 0, st>>>(P, C, begin, x, cur, xs, prop, eps, seed, it, draws, accepted, failures);
     return hipGetLastError();
 }
 
