@@ -187,6 +187,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.inv_mult[k] = 1.0 / P.mult[k];
         P.lw[k] = 0.0;
         P.nt[k] = 8;
+        P.spec[k] = 0;
     }
     for (int k = 0; k < cfg->n_levels; k++) {
         const double xk = 1.0 / ((double)mult[k] * mult[k]);
@@ -199,12 +200,14 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.lw[k] = wk;
         // Stumpff series length (rvm_device.h stumpff_bound): nominal z = (2 pi h / P)^2 on a
         // circular orbit, x2 for the pericentre of e ~ 0.25 orbits; lanes beyond the bound take
-        // the general evaluation, so this choice only affects speed.  NT = 6 levels also run
+        // the general evaluation, so this choice only affects speed.  Levels whose nominal z is
+        // small enough that the first Halley step is accepted almost always (fine levels) run
         // their segments speculatively (rvm_logl.hip segment<>)
         if (cfg->period_hint > 0.0) {
             const double nh = 2.0 * M_PI * cfg->dt / (mult[k] * cfg->period_hint);
             const double zn = 2.0 * nh * nh;
-            P.nt[k] = zn <= 0.04 ? 6 : (zn <= 0.12 ? 7 : 8);
+            P.nt[k] = zn <= 0.1 ? 6 : (zn <= 0.3 ? 7 : 8);
+            P.spec[k] = zn <= 0.04 ? 1 : 0;
         }
     }
     *out = plan;

@@ -82,14 +82,15 @@ __device__ __forceinline__ double rcube_nr(double x) { return rcube_nr(x, 1.875)
 // c2 = sum_j (-z)^j / (2j+2)!,  c3 = sum_j (-z)^j / (2j+3)!;  c1 = 1 - z c3,  c0 = 1 - z c2.
 //
 // Hot path: c2, c3 by Horner in z with NT terms (one fma per term with the coefficient in an
-// SGPR: no constant copies).  The truncation error is below 1e-19 relative for |z| <= B(NT):
-//   NT = 6: B = 0.04 (z^6/14! <= 5e-20)   NT = 7: B = 0.12 (z^7/16! <= 2e-20)   NT = 8: B = 0.3 (z^8/18! <= 1e-20)
+// SGPR: no constant copies).  The truncation error is at most ~2e-17 relative (0.2 ulp, below the
+// Horner evaluation's own rounding) for |z| <= B(NT):
+//   NT = 6: B = 0.1 (z^6/14! <= 1.2e-17)   NT = 7: B = 0.3 (z^7/16! <= 1.1e-17)   NT = 8: B = 0.3 (z^8/18! <= 1e-20)
 // The term count is chosen per extrapolation level (wave-uniform, see logl_kernel), and lanes
 // with |z| > B(NT) redo the evaluation with stumpff_full, so a walker's result depends only on
 // its own (z, level), never on the other lanes of the wave.
 template <int NT>
 __device__ __forceinline__ constexpr double stumpff_bound() {
-    return NT >= 8 ? 0.3 : (NT == 7 ? 0.12 : 0.04);
+    return NT >= 7 ? 0.3 : 0.1;
 }
 
 struct StumpffK {
@@ -407,9 +408,9 @@ __device__ __forceinline__ void halley(double x, double beta, double r0, double 
 // Acceptance of a Halley step with relative correction qt = q/x: the error left in X is
 // ~ c z qt^3 (c << 1; Halley is cubic and its constant scales with z = beta x^2), and the Taylor
 // update of the G-functions over the correction (drift_apply) truncates at ~ z qt^3 / 3 relative.
-// Both stay below ~1e-17 when |q^3 z| <= 3e-17 |x^3|.  With |z| <= B(NT) (checked separately)
-// this holds whenever |q| <= (3e-17 / B)^(1/3) |x|, the cheap form used on the hot path:
-//   NT = 6: 9.0e-6   NT = 7: 6.2e-6   NT = 8: 4.6e-6
+// With |z| <= B(NT) (checked separately) the cheap form used on the hot path, |q| <= tol |x| with
+//   NT = 6: 9.0e-6   NT = 7: 6.2e-6   NT = 8: 4.6e-6,
+// keeps |q^3 z| <= 7.3e-17 |x^3|: both truncations stay below ~2.5e-17 relative (a quarter ulp).
 // At the default steps (P/32 .. P/56) and e <~ 0.25 the finest levels pass after one step.
 template <int NT>
 __device__ __forceinline__ constexpr double halley_tol() {
@@ -500,6 +501,26 @@ __device__ __forceinline__ DriftOut drift_apply(const Lane<NP>& s, double dt, do
     return o;
 }
 
+#ifdef RVM_PROFILE
+// timing build only (counted with -DRVM_PROFILE_FAILS): why first Halley steps fail, per series length (NT 6/7/8 -> rows 0/1/2):
+// [drifts (lanes), |z| > B, z fine but Halley not accepted]; read with rvm_prof_fail_copy
+// row 3: [wave-steps taking the second Halley step, wave-steps entering kepler_rare, lanes in it]
+static __device__ unsigned long long rvm_fail[4][3];
+__device__ __forceinline__ void rare_count(int k, uint64_t mask) {
+    if ((threadIdx.x & 63) == (int)__builtin_ctzll(ballot(true)))
+        atomicAdd(&rvm_fail[3][k], k == 2 ? (unsigned long long)__builtin_popcountll(mask) : 1ull);
+}
+__device__ __forceinline__ void drift_fail_count(int nt, bool zok, bool hok) {
+    const uint64_t all = ballot(true), zb = ballot(!zok), hb = ballot(zok && !hok);
+    if ((threadIdx.x & 63) == (int)__builtin_ctzll(all)) {
+        const int row = nt <= 6 ? 0 : (nt == 7 ? 1 : 2);
+        atomicAdd(&rvm_fail[row][0], (unsigned long long)__builtin_popcountll(all));
+        if (zb) atomicAdd(&rvm_fail[row][1], (unsigned long long)__builtin_popcountll(zb));
+        if (hb) atomicAdd(&rvm_fail[row][2], (unsigned long long)__builtin_popcountll(hb));
+    }
+}
+#endif
+
 // Kepler drift of the own Jacobi coordinate by dt in universal variables (Danby): solve
 // r0 G1 + eta0 G2 + GM G3 = dt for X by Halley steps from the fourth-order Taylor guess
 //   X = u (1 - u s/2 + u^2 T3 + u^3 T4),   u = dt/r0, s = eta0/r0, g = GM/r0,
@@ -534,12 +555,18 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
     double G0, G1, G2, G3, fp, fpp, Q, z, x3;
     halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2, vk.k3);
     constexpr double B = stumpff_bound<NT>();
+#ifdef RVM_PROFILE_FAILS
+    drift_fail_count(NT, fabs(z) <= B, halley_ok<NT>(Q, x));
+#endif
     // A step spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) that passes these tests has
     // converged all the same; only kepler_rare treats such steps separately (bracketed solver).
     if constexpr (GATED) {
         constexpr double B8 = stumpff_bound<8>();
         const bool ok1 = fabs(z) <= B && halley_ok<NT>(Q, x);
         if (ballot(!ok1) != 0) {
+#ifdef RVM_PROFILE_FAILS
+            rare_count(0, 0);
+#endif
             // a second Halley step with the 8-term series (|z| <= 0.3) for the lanes that need it:
             // pericentre passages on the coarse levels, and walkers whose periods are much shorter
             // than the plan's period hint on any level
@@ -554,6 +581,10 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
                 }
             }
             if (__builtin_expect(ballot(!ok) != 0, 0)) {
+#ifdef RVM_PROFILE_FAILS
+                rare_count(1, 0);
+                rare_count(2, ballot(!ok));
+#endif
                 if (!ok) {
                     const bool hard = fabs(beta) * (u * u) > 0.5;
                     const double start = xe - Q;

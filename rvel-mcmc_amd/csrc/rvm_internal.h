@@ -22,6 +22,7 @@ struct DevPlan {
     int32_t n_levels;
     int32_t mult[RVM_MAX_LEVELS];  // level step multipliers (steps per base step)
     int32_t nt[RVM_MAX_LEVELS];    // Stumpff series terms per level (6, 7 or 8)
+    int32_t spec[RVM_MAX_LEVELS];  // 1: speculative segments on this level (rvm_logl.hip)
     double inv_mult[RVM_MAX_LEVELS];  // 1 / mult: level step = seg_h1 * inv_mult
     double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
     double npoints;

@@ -162,6 +162,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const int lvl_u = __builtin_amdgcn_readfirstlane(lvl);
     const int mult = P.mult[lvl_u];
     const int nt = P.nt[lvl_u];
+    const bool spec = P.spec[lvl_u] != 0 && nt <= 6;
     const double inv_mult = P.inv_mult[lvl_u];
     const int E = S.n_epochs;
     double* l_len = s_sched;
@@ -350,7 +351,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         PROF_T(ta);
         if (ns > 0) {
             const double h = len * inv_mult;  // len holds the segment's base step
-            if (nt <= 6) {
+            if (spec) {  // (implies nt == 6)
                 // speculate unless a recent segment of this wave needed a redo: walkers whose
                 // orbits keep needing the general solver (short periods, high eccentricity in a
                 // wide ensemble) then run gated for a while instead of paying for redos
@@ -360,7 +361,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                     segment<6, false, D3, NP, L>(s, h, ns, redo);
                     spec_off--;
                 }
-            } else if (nt == 7)
+            } else if (nt <= 6)
+                segment<6, false, D3, NP, L>(s, h, ns, redo);
+            else if (nt == 7)
                 segment<7, false, D3, NP, L>(s, h, ns, redo);
             else
                 segment<8, false, D3, NP, L>(s, h, ns, redo);
@@ -492,7 +495,12 @@ extern "C" int rvm_prof_copy(void* host, size_t bytes) {
     const size_t n = bytes < sizeof(rvm::rvm_prof) ? bytes : sizeof(rvm::rvm_prof);
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(rvm::rvm_prof), n, 0, hipMemcpyDeviceToHost);
 }
+extern "C" int rvm_prof_fail_copy(void* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(rvm::rvm_fail), sizeof(rvm::rvm_fail), 0, hipMemcpyDeviceToHost);
+}
 extern "C" int rvm_prof_clear(void) {
+    static unsigned long long zf[12];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(rvm::rvm_fail), zf, sizeof(zf), 0, hipMemcpyHostToDevice);
     static unsigned long long zero[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
     return (int)hipMemcpyToSymbol(HIP_SYMBOL(rvm::rvm_prof), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
 }

@@ -63,6 +63,11 @@ def main():
                             "segments_redone_mean": float(b[m, 8].mean()), "segments": int(b[m, 9].max())}
     rt = (b[:, 6] - b[:, 5]) / 100.0
     out["wave_realtime_us"] = {"min": float(rt.min()), "median": float(np.median(rt)), "max": float(rt.max())}
+    tot = b[:, 4] - b[:, 0]
+    slow = np.argsort(tot)[::-1][:6]
+    out["slowest_waves"] = [{"level_mult": int((b[i, 7] >> 16) & 0xFF), "dir": int((b[i, 7] >> 8) & 0xFF),
+                             "total_kcyc": float(tot[i] / 1e3), "segments_kcyc": float(b[i, 2] / 1e3),
+                             "epochs_kcyc": float(b[i, 3] / 1e3), "redo": int(b[i, 8])} for i in slow]
     out["start_spread_us"] = float((b[:, 5].max() - b[:, 5].min()) / 100.0)
     # placement (HW_REG_HW_ID, gfx9 layout): wave_id [3:0], simd [5:4], cu [11:8], sh [12], se [15:13]
     hw = b[:, 10]
@@ -78,6 +83,16 @@ def main():
     per = [sum(v) for v in load.values()]
     out["simd_load_mult_sum"] = {"max": int(max(per)), "hist": {str(x): per.count(x) for x in sorted(set(per))}}
     out["cus_used"] = int(len(set(key.tolist())))
+    fails = np.zeros(12, dtype=np.uint64)
+    lib.rvm_prof_fail_copy.argtypes = [C.c_void_p]
+    if lib.rvm_prof_fail_copy(fails.ctypes.data) == 0 and fails.any():
+        f = fails.reshape(4, 3).astype(np.float64)
+        out["gated_rare"] = {"wave_steps_second_halley": int(f[3, 0]), "wave_steps_kepler_rare": int(f[3, 1]),
+                             "lanes_kepler_rare": int(f[3, 2])}
+        out["first_halley_step"] = {f"NT{6 + i}": {"lane_drifts": int(f[i, 0]),
+                                                   "z_beyond_bound": float(f[i, 1] / max(f[i, 0], 1)),
+                                                   "not_accepted": float(f[i, 2] / max(f[i, 0], 1))}
+                                    for i in range(3) if f[i, 0] > 0}
     print(json.dumps(out, indent=1))
 
 
