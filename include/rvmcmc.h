@@ -16,6 +16,8 @@
  *   mcmc.py:57-65 Ensemble.step -> emcee 2.2.1 stretch     rvm_stretch_propose / rvm_stretch_accept,
  *     move (EnsembleSampler._propose_stretch)                or fused: rvm_stretch_half_step
  *   mcmc.py:89-121 Mh.generate_proposal / Mh.step          rvm_mh_propose / rvm_mh_accept
+ *   state.py:218-294 get_chi2_d_dd / get_logp_d_dd         rvm_logl_derivs (exact gradient + Hessian,
+ *     (REBOUND 1st/2nd-order variational equations)         hyper-dual forward mode)
  *   mcmc.py:144-187 Smala.generate_proposal/step           rvm_fd_params (finite-difference stencil)
  *     mcmc.py:135-139 Smala.softabs,                         + rvm_smala_derive / rvm_smala_propose /
  *     mcmc.py:158-162 Smala.transitionProbability              rvm_smala_accept
@@ -37,13 +39,14 @@
 #ifndef RVMCMC_H
 #define RVMCMC_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 4
+#define RVM_ABI_VERSION 5
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -186,6 +189,25 @@ int rvm_smala_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, c
 int rvm_smala_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const rvm_smala_cache* cur,
                      const double* x_prop, const rvm_smala_cache* prop, double eps, uint64_t seed,
                      uint64_t iteration, const double* draws, int32_t* accepted, int32_t* failures, void* stream);
+
+/* ---- exact derivatives (state.py:218-294) ----------------------------------------------------
+ * logp, its gradient and its Hessian for n_chains parameter vectors (params: kernel rows
+ * [5|7 * n_planets][n_chains], as rvm_logl_batch), differentiated along n_dirs kernel rows
+ * dir_rows[0..n_dirs) (host array; the free parameters of the State, in its order):
+ *   logl_out [n_chains]            -chi2/npoints_norm (or -INF with status != 0)
+ *   grad_out [n_dirs][n_chains]    d logp / d p_i
+ *   hess_out [n_dirs*n_dirs][n_chains]  d2 logp / d p_i d p_j, row-major per chain (symmetric)
+ *   status_out [n_chains]          as rvm_logl_batch; gradient and Hessian are NaN unless 0
+ * The reference integrates REBOUND's order-1 and order-2 variational equations (one variation per
+ * parameter, one per pair); here every parameter pair (i >= j) is one hyper-dual integration of the
+ * plan's own discrete integrator (same steps, levels and Richardson weights as rvm_logl_batch),
+ * so the results are the exact derivatives of that likelihood.  workspace: device buffer of
+ * rvm_logl_derivs_workspace_bytes(n_chains, n_dirs) bytes (no allocation inside).  No limit from
+ * the plan's max_walkers. */
+size_t rvm_logl_derivs_workspace_bytes(int32_t n_chains, int32_t n_dirs);
+int rvm_logl_derivs(const rvm_plan* plan, int32_t n_chains, const double* params, int32_t n_dirs,
+                    const int32_t* dir_rows, double hill_factor, double* logl_out, double* grad_out, double* hess_out,
+                    int32_t* status_out, void* workspace, void* stream);
 
 const char* rvm_last_error(void);
 int rvm_abi_version(void);

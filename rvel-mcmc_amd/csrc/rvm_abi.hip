@@ -36,6 +36,9 @@ hipError_t launch_smala_propose(int P, int C, int64_t begin, const double* x, co
 hipError_t launch_smala_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
                                const SmalaCache& prop, double eps, uint64_t seed, uint64_t it, const double* draws,
                                int32_t* accepted, int32_t* failures, hipStream_t st);
+hipError_t launch_derivs(const DevPlan& P, int C, const double* params, int n_dirs, const int32_t* dir_rows,
+                         double hill_factor, double* ws, int32_t* wst, double* logl, double* grad, double* hess,
+                         int32_t* status, hipStream_t stream);
 }  // namespace rvm
 
 struct rvm_plan {
@@ -330,6 +333,36 @@ int rvm_fd_params(int32_t n_params, int32_t n_chains, const double* x, double re
         return fail(-1, "rvm_fd_params: bad arguments");
     hipError_t e = rvm::launch_fd_params(n_params, n_chains, x, rel_step, floor_, out, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_fd_params");
+}
+
+size_t rvm_logl_derivs_workspace_bytes(int32_t n_chains, int32_t n_dirs) {
+    if (n_chains < 0 || n_dirs < 0) return 0;
+    const size_t items = (size_t)n_chains * (size_t)(n_dirs * (n_dirs + 1) / 2);
+    return items * 2 * (4 * sizeof(double) + sizeof(int32_t));
+}
+
+int rvm_logl_derivs(const rvm_plan* plan, int32_t n_chains, const double* params, int32_t n_dirs,
+                    const int32_t* dir_rows, double hill_factor, double* logl_out, double* grad_out, double* hess_out,
+                    int32_t* status_out, void* workspace, void* stream) {
+    if (!plan) return fail(-1, "rvm_logl_derivs: null plan");
+    if (n_chains == 0) return 0;
+    const int rows = (plan->dev.inclined ? 7 : 5) * plan->dev.n_planets;
+    if (n_chains < 0 || n_dirs < 1 || n_dirs > rows || !dir_rows || !params || !grad_out || !hess_out || !workspace)
+        return fail(-1, "rvm_logl_derivs: bad arguments");
+    if ((size_t)n_chains * (size_t)(n_dirs * (n_dirs + 1) / 2) > (size_t)(1 << 30))
+        return fail(-1, "rvm_logl_derivs: too many chains x parameter pairs");
+    if (!(hill_factor >= 0.0)) return fail(-1, "rvm_logl_derivs: hill_factor must be >= 0");
+    for (int k = 0; k < n_dirs; k++) {
+        if (dir_rows[k] < 0 || dir_rows[k] >= rows) return fail(-1, "rvm_logl_derivs: dir_rows entry out of range");
+        for (int q = 0; q < k; q++)
+            if (dir_rows[q] == dir_rows[k]) return fail(-1, "rvm_logl_derivs: dir_rows entries must be distinct");
+    }
+    const size_t items = (size_t)n_chains * (size_t)(n_dirs * (n_dirs + 1) / 2);
+    double* ws = reinterpret_cast<double*>(workspace);
+    int32_t* wst = reinterpret_cast<int32_t*>(ws + 2 * 4 * items);
+    hipError_t e = rvm::launch_derivs(plan->dev, n_chains, params, n_dirs, dir_rows, hill_factor, ws, wst, logl_out,
+                                      grad_out, hess_out, status_out, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_logl_derivs");
 }
 
 static bool smala_cache_ok(const rvm_smala_cache* c) {

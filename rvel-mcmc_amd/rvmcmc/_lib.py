@@ -17,7 +17,7 @@ RVM_STATUS_ENCOUNTER = 2
 RVM_STATUS_NONFINITE = 3
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
-ABI_VERSION = 4  # include/rvmcmc.h RVM_ABI_VERSION
+ABI_VERSION = 5  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):
@@ -81,6 +81,9 @@ SIGNATURES = {
     "rvm_mh_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, _dp, _dp, _dp, C.c_uint64, C.c_uint64, _dp, _dp,
                                 _dp]),
     "rvm_fd_params": (C.c_int, [C.c_int32, C.c_int32, _dp, C.c_double, _dp, _dp, _dp]),
+    "rvm_logl_derivs_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
+    "rvm_logl_derivs": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_int32, C.POINTER(C.c_int32), C.c_double, _dp, _dp,
+                                  _dp, _dp, _dp, _dp]),
 }
 
 _lib = None

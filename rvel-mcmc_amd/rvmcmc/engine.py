@@ -175,6 +175,34 @@ class LoglPlan:
         _lib.check(rc, "rvm_logl_batch")
         return out, status, (rv_out if want_rv else None)
 
+    def derivs(self, params, dir_rows, hill_factor=1.0, stream=None):
+        """Exact logp, gradient and Hessian (rvm_logl_derivs; state.py:218-294 get_chi2_d_dd /
+        get_logp_d_dd): params [rows][C] float64 device tensor, dir_rows = kernel rows of the
+        free parameters (ParamMap.slots).  Returns (logl[C], grad[P][C], hess[P][P][C], status[C]);
+        gradient and Hessian are NaN where status != 0."""
+        torch = _torch()
+        if params.dtype != torch.float64 or params.device != self.device or params.dim() != 2:
+            raise ValueError("params must be a 2-D float64 tensor on the plan's device")
+        if params.shape[0] != self.rows:
+            raise ValueError(f"params must have {self.rows} rows")
+        params = params.contiguous()
+        C_ = params.shape[1]
+        rows = np.ascontiguousarray(np.asarray(dir_rows, dtype=np.int32))
+        P = len(rows)
+        f64 = dict(dtype=torch.float64, device=self.device)
+        lp = torch.empty(C_, **f64)
+        grad = torch.empty((P, C_), **f64)
+        hess = torch.empty((P, P, C_), **f64)
+        st = torch.empty(C_, dtype=torch.int32, device=self.device)
+        nb = int(self.lib.rvm_logl_derivs_workspace_bytes(C_, P))
+        ws = torch.empty(max(nb, 8), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.lib.rvm_logl_derivs(self._h, C_, params.data_ptr(), P, rows.ctypes.data_as(C.POINTER(C.c_int32)),
+                                          float(hill_factor), lp.data_ptr(), grad.data_ptr(), hess.data_ptr(),
+                                          st.data_ptr(), ws.data_ptr(), _lib.stream_handle(stream))
+        _lib.check(rc, "rvm_logl_derivs")
+        return lp, grad, hess, st
+
     def stretch_half_step(self, pmap, X0, lnp0, c, s0_begin, a, seed, iteration, half, hill_factor=1.0,
                           lnp_new=None, status=None, accepted=None, stream=None):
         """Fused emcee stretch half-step (rvm_stretch_half_step): propose against the complement

@@ -9,9 +9,10 @@ changed is underneath: REBOUND + IAS15 are replaced by the librvmcmc HIP kernel
 
 Deliberate differences:
   * priorHard does not print; it logs at DEBUG level.
-  * get_logp_d_dd returns finite-difference derivatives (central differences for the gradient,
-    Gauss-Newton from the per-epoch RV Jacobian for the Hessian) instead of REBOUND's
-    2nd-order variational equations (state.py:229-294).
+  * get_logp_d_dd / get_chi2_d_dd return the exact derivatives of the kernel's own discrete
+    integrator (rvm_logl_derivs, hyper-dual forward mode) where the reference integrates REBOUND's
+    order-1/order-2 variational equations alongside IAS15 (state.py:218-294); method="fd" gives
+    the SMALA fast path's central-difference gradient + Gauss-Newton Hessian instead.
   * Python 3 dict order defines the parameter order (insertion order); the reference ran on
     Python 2 dicts.
 """
@@ -212,17 +213,48 @@ class State(object):
         hf = self.hillRadiusFactor if hill_factor is None else hill_factor
         return plan.logl(K, hill_factor=hf, want_rv=want_rv)
 
-    # -- derivatives for SMALA (finite differences; state.py:253-294 replaced) ------------------
-    def get_logp_d_dd(self, obs, rel_step=1e-6):
-        if self.logp is None or self.logp_d is None:
-            from .smala import fd_logp_grad_metric
-            import torch
+    # -- derivatives (state.py:218-294) -------------------------------------------------------------
+    def get_logp_d_dd_batch(self, obs, X, hill_factor=None, pmap=None):
+        """Exact logp, gradient and Hessian for a batch of free-parameter vectors X [Nvars][C]
+        (float64 device tensor): rvm_logl_derivs, the hyper-dual counterpart of the reference's
+        order-1/order-2 variational particles.  Returns (logp[C], grad[P][C], hess[P][P][C], status[C])."""
+        pmap = pmap or self.param_map()
+        plan = self._plan(obs, device=X.device)
+        hf = self.hillRadiusFactor if hill_factor is None else hill_factor
+        return plan.derivs(pmap.to_kernel(X), pmap.slots, hill_factor=hf)
 
-            x = torch.as_tensor(self.get_params(), dtype=torch.float64, device=engine.default_device())[:, None]
-            lp, g, H, st = fd_logp_grad_metric(self, obs, x, rel_step=rel_step)
-            if int(st[0].item()) == 2:
-                raise Encounter("Two particles had a close encounter (d<exit_min_distance).")
-            self.logp = float(lp[0].item())
-            self.logp_d = g[:, 0].cpu().numpy()
-            self.logp_dd = H[:, :, 0].cpu().numpy()
+    def get_chi2_d_dd(self, obs):  # state.py:253-288
+        """(chi2, dchi2, d2chi2) ÷ obs.Npoints at the current parameters; raises Encounter."""
+        import torch
+
+        x = torch.as_tensor(self.get_params(), dtype=torch.float64, device=engine.default_device())[:, None]
+        lp, g, H, st = self.get_logp_d_dd_batch(obs, x)
+        st = int(st[0].item())
+        if st == 2:
+            raise Encounter("Two particles had a close encounter (d<exit_min_distance).")
+        return -float(lp[0].item()), -g[:, 0].cpu().numpy(), -H[:, :, 0].cpu().numpy()
+
+    def get_logp_d_dd(self, obs, method="exact", rel_step=1e-6):  # state.py:290-294
+        """logp, its gradient and its Hessian (cached like the reference until set_params/shift_params).
+
+        method="exact" (default, the reference's semantics): exact derivatives of the likelihood
+        (rvm_logl_derivs).  method="fd": the SMALA fast path's central differences with the
+        Gauss-Newton Hessian (rvmcmc.smala.fd_logp_grad_metric)."""
+        if self.logp is None or self.logp_d is None:
+            if method == "fd":
+                from .smala import fd_logp_grad_metric
+                import torch
+
+                x = torch.as_tensor(self.get_params(), dtype=torch.float64, device=engine.default_device())[:, None]
+                lp, g, H, st = fd_logp_grad_metric(self, obs, x, rel_step=rel_step)
+                if int(st[0].item()) == 2:
+                    raise Encounter("Two particles had a close encounter (d<exit_min_distance).")
+                self.logp = float(lp[0].item())
+                self.logp_d = g[:, 0].cpu().numpy()
+                self.logp_dd = H[:, :, 0].cpu().numpy()
+            elif method == "exact":
+                chi, chi_d, chi_dd = self.get_chi2_d_dd(obs)
+                self.logp, self.logp_d, self.logp_dd = -chi, -chi_d, -chi_dd
+            else:
+                raise ValueError("method must be 'exact' or 'fd'")
         return self.logp, self.logp_d, self.logp_dd

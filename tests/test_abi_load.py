@@ -19,7 +19,8 @@ def test_header_declares_expected_surface():
     fns = header_functions()
     for f in ("rvm_plan_create", "rvm_logl_batch", "rvm_stretch_propose", "rvm_stretch_accept",
               "rvm_mh_propose", "rvm_mh_accept", "rvm_fd_params", "rvm_smala_derive", "rvm_smala_propose",
-              "rvm_smala_accept", "rvm_stretch_half_step", "rvm_last_error", "rvm_abi_version"):
+              "rvm_smala_accept", "rvm_stretch_half_step", "rvm_logl_derivs", "rvm_logl_derivs_workspace_bytes",
+              "rvm_last_error", "rvm_abi_version"):
         assert f in fns
 
 
@@ -27,7 +28,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == 4
+    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_python_binding_matches_header():
@@ -46,6 +47,10 @@ def test_argument_errors_do_not_touch_the_device():
     assert lib.rvm_logl_batch(None, 1, 0, 1.0, 0, 0, 0, 0) < 0
     m = _lib.ParamMapC()
     assert lib.rvm_stretch_half_step(None, C.byref(m), 10, 1, 0, 0, 0, 1, 0, 2.0, 0, 0, 0, 1.0, 0, 0, 0, 0) < 0
+    rows = (C.c_int32 * 2)(0, 1)
+    assert lib.rvm_logl_derivs(None, 1, 0, 2, rows, 1.0, 0, 0, 0, 0, 0, 0) < 0
+    # workspace: per (chain, pair i >= j) and direction, 4 f64 partial sums and an int32 status
+    assert lib.rvm_logl_derivs_workspace_bytes(256, 10) == 256 * 55 * 2 * (4 * 8 + 4)
 
 
 def test_struct_layouts_match_header():
