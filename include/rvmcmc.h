@@ -19,8 +19,9 @@
  *   state.py:218-294 get_chi2_d_dd / get_logp_d_dd         rvm_logl_derivs (exact gradient + Hessian,
  *     (REBOUND 1st/2nd-order variational equations)         hyper-dual forward mode)
  *   mcmc.py:144-187 Smala.generate_proposal/step           rvm_fd_params (finite-difference stencil)
- *     mcmc.py:135-139 Smala.softabs,                         + rvm_smala_derive / rvm_smala_propose /
- *     mcmc.py:158-162 Smala.transitionProbability              rvm_smala_accept
+ *     mcmc.py:135-139 Smala.softabs,                         + rvm_smala_derive, or rvm_logl_derivs +
+ *     mcmc.py:158-162 Smala.transitionProbability              rvm_smala_metric; rvm_smala_propose /
+ *                                                              rvm_smala_accept
  *
  * Conventions
  *   - All array pointers passed to launch functions are DEVICE pointers (hipMalloc / torch CUDA
@@ -177,6 +178,12 @@ int rvm_smala_derive(int32_t n_params, int32_t n_chains, int32_t n_obs, const do
                      const double* floor_, const double* lp_stencil, const int32_t* status_stencil,
                      const double* rv_stencil, const double* inv_sigma2, double npoints_norm, double alpha,
                      double eps, const rvm_smala_cache* out, void* stream);
+/* The same cache from exact derivatives (rvm_logl_derivs outputs: lp [C], status [C], grad [P][C],
+ * hess [P*P][C]): the reference's Hessian (state.py:253-294) instead of the Gauss-Newton one.
+ * Chains with status != 0 or non-finite derivatives get ok = 0.  mcmc.py:135-150. */
+int rvm_smala_metric(int32_t n_params, int32_t n_chains, const double* x, const double* lp, const int32_t* status,
+                     const double* grad, const double* hess, double alpha, double eps, const rvm_smala_cache* out,
+                     void* stream);
 /* x_prop = mu + eps chol(G^-1) z (x where the cache is not ok); z ~ N(0,1) from Philox keyed by
  * (seed, chain_begin + c, iteration, 5 | p << 8) or from draws [P][C].  mcmc.py:144-153. */
 int rvm_smala_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, const double* x,

@@ -31,6 +31,9 @@ hipError_t launch_fd_params(int P, int n, const double* x, double rel, const dou
 hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,
                                const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
                                double npoints, double alpha, double eps, const SmalaCache& out, hipStream_t st);
+hipError_t launch_smala_metric(int P, int C, const double* x, const double* lp, const int32_t* status,
+                               const double* grad, const double* hess, double alpha, double eps, const SmalaCache& out,
+                               hipStream_t st);
 hipError_t launch_smala_propose(int P, int C, int64_t begin, const double* x, const SmalaCache& cur, double eps,
                                 uint64_t seed, uint64_t it, const double* draws, double* xs, hipStream_t st);
 hipError_t launch_smala_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
@@ -386,6 +389,18 @@ int rvm_smala_derive(int32_t n_params, int32_t n_chains, int32_t n_obs, const do
                                             status_stencil, rv_stencil, inv_sigma2, npoints_norm, alpha, eps,
                                             smala_cache(out), (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_derive");
+}
+
+int rvm_smala_metric(int32_t n_params, int32_t n_chains, const double* x, const double* lp, const int32_t* status,
+                     const double* grad, const double* hess, double alpha, double eps, const rvm_smala_cache* out,
+                     void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || !x || !lp || !status || !grad || !hess ||
+        !smala_cache_ok(out) || !(alpha > 0.0))
+        return fail(-1, "rvm_smala_metric: bad arguments");
+    hipError_t e = rvm::launch_smala_metric(n_params, n_chains, x, lp, status, grad, hess, alpha, eps, smala_cache(out),
+                                            (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_metric");
 }
 
 int rvm_smala_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, const double* x,

@@ -37,95 +37,15 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// One wave per chain: the P x P matrices live in LDS, lanes own matrix rows / entries, and the
-// sequential parts (Jacobi rotations, Cholesky columns) run lock-step across the wave.
-__global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, const double* __restrict__ x,
-                                                          double rel, const double* __restrict__ fl,
-                                                          const double* __restrict__ lp_st,
-                                                          const int32_t* __restrict__ st_st,
-                                                          const double* __restrict__ rv,
-                                                          const double* __restrict__ w, double npoints,
-                                                          double alpha, double eps, SmalaCache out) {
+// From A = -H (P x P in LDS), the gradient gr and the point xv: SoftAbs metric of A by the
+// cyclic Jacobi eigen-solver, G, G^-1, the drift, the Cholesky factor of G^-1 and log det G^-1
+// into the chain's cache (mcmc.py:135-150).  One wave per chain; the arrays are the caller's LDS.
+__device__ __forceinline__ void smala_metric_stage(int P, int C, int c, int lane, double* A, double* Qm, double* gr,
+                                                   double* xv, double* lt, double* inv, double* ra, double* rb,
+                                                   double* dn, int* rp, int& okflag, double lp_c, double alpha,
+                                                   double eps, const SmalaCache& out) {
     constexpr int PM = RVM_SMALA_MAX_PARAMS;
-    constexpr int NTRI = PM * (PM + 1) / 2;        // upper-triangle entries
-    constexpr int PER_LANE = (NTRI + 63) / 64;     // accumulators per lane
-    __shared__ double A[PM * PM], Qm[PM * PM];
-    __shared__ double den[PM], gr[PM], lt[PM], inv[PM], xv[PM];
-    __shared__ double ra[PM], rb[PM], dn[PM];
-    __shared__ int rp[PM];
-    constexpr int JCH = 64;                        // epochs per J chunk
-    __shared__ double Jc[JCH * PM], wc[JCH];
-    __shared__ int okflag;
-    const int c = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int S = 2 * P + 1;
-    const size_t SC = (size_t)S * C;
     const int ntri = P * (P + 1) / 2;
-    if (lane == 0) okflag = 1;
-    __syncthreads();
-    for (int s = lane; s < S; s += 64)
-        if (st_st[(size_t)s * C + c] != 0) okflag = 0;
-    // realised steps exactly as rvm_fd_params formed the stencil; gradient
-    if (lane < P) {
-        const double xp = x[(size_t)lane * C + c];
-        const double ax = fabs(xp) > fl[lane] ? fabs(xp) : fl[lane];
-        const double e = rel * ax;
-        const double d = (xp + e) - (xp - e);
-        const double g = (lp_st[(size_t)(1 + 2 * lane) * C + c] - lp_st[(size_t)(2 + 2 * lane) * C + c]) / d;
-        den[lane] = d;
-        gr[lane] = g;
-        xv[lane] = xp;
-        out.grad[(size_t)lane * C + c] = g;
-    }
-    __syncthreads();
-    // -H = (2/N) sum_e J_e^T (1/sigma_e^2) J_e, J_e[p] = (rv_e(x+e_p) - rv_e(x-e_p)) / den_p:
-    // K = 64/P epochs of J per chunk in LDS, each lane accumulates its upper-triangle entries
-    int tp[PER_LANE], tq[PER_LANE];
-    double acc[PER_LANE];
-#pragma unroll
-    for (int j = 0; j < PER_LANE; j++) {
-        const int idx = lane + 64 * j;
-        int p = 0, rem = idx;
-        while (p < P && rem >= P - p) {
-            rem -= P - p;
-            p++;
-        }
-        tp[j] = p;
-        tq[j] = p + rem;
-        acc[j] = 0.0;
-    }
-    // J in chunks of JCH epochs: every lane issues its loads of the chunk at once (the chunk's
-    // latency is paid once, not once per epoch), then the triangle accumulates from LDS
-    for (int e0 = 0; e0 < E; e0 += JCH) {
-        const int kmax = E - e0 < JCH ? E - e0 : JCH;
-        const int n = kmax * P;
-#pragma unroll 4
-        for (int idx = lane; idx < n; idx += 64) {
-            const int k = idx / P, p = idx - (idx / P) * P;
-            const double* re = rv + (size_t)(e0 + k) * SC;
-            Jc[idx] = (re[(size_t)(1 + 2 * p) * C + c] - re[(size_t)(2 + 2 * p) * C + c]) / den[p];
-        }
-        if (lane < kmax) wc[lane] = w[e0 + lane];
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < PER_LANE; j++) {
-            if (lane + 64 * j < ntri) {
-                double a = acc[j];
-                for (int k = 0; k < kmax; k++) a += (Jc[k * P + tp[j]] * wc[k]) * Jc[k * P + tq[j]];
-                acc[j] = a;
-            }
-        }
-        __syncthreads();
-    }
-    const double fac = 2.0 / npoints;
-#pragma unroll
-    for (int j = 0; j < PER_LANE; j++) {
-        if (lane + 64 * j < ntri) {
-            const double a = fac * acc[j];
-            A[tp[j] * P + tq[j]] = a;
-            A[tq[j] * P + tp[j]] = a;
-        }
-    }
     for (int i = lane; i < P * P; i += 64) Qm[i] = (i / P == i % P) ? 1.0 : 0.0;
     __syncthreads();
     // Jacobi eigen-solver, parallel (round-robin) ordering: A -> diag(lambda), Q -> eigenvectors
@@ -281,10 +201,144 @@ __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, c
     if (lane == 0) {
         double logdet = 0.0;  // log det G^-1
         for (int k = 0; k < P; k++) logdet += log(inv[k]);
-        out.lp[c] = lp_st[c];
+        out.lp[c] = lp_c;
         out.logdet[c] = logdet;
         out.ok[c] = okflag;
     }
+}
+
+// One wave per chain: the P x P matrices live in LDS, lanes own matrix rows / entries, and the
+// sequential parts (Jacobi rotations, Cholesky columns) run lock-step across the wave.
+__global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, const double* __restrict__ x,
+                                                          double rel, const double* __restrict__ fl,
+                                                          const double* __restrict__ lp_st,
+                                                          const int32_t* __restrict__ st_st,
+                                                          const double* __restrict__ rv,
+                                                          const double* __restrict__ w, double npoints,
+                                                          double alpha, double eps, SmalaCache out) {
+    constexpr int PM = RVM_SMALA_MAX_PARAMS;
+    constexpr int NTRI = PM * (PM + 1) / 2;        // upper-triangle entries
+    constexpr int PER_LANE = (NTRI + 63) / 64;     // accumulators per lane
+    __shared__ double A[PM * PM], Qm[PM * PM];
+    __shared__ double den[PM], gr[PM], lt[PM], inv[PM], xv[PM];
+    __shared__ double ra[PM], rb[PM], dn[PM];
+    __shared__ int rp[PM];
+    constexpr int JCH = 64;                        // epochs per J chunk
+    __shared__ double Jc[JCH * PM], wc[JCH];
+    __shared__ int okflag;
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int S = 2 * P + 1;
+    const size_t SC = (size_t)S * C;
+    const int ntri = P * (P + 1) / 2;
+    if (lane == 0) okflag = 1;
+    __syncthreads();
+    for (int s = lane; s < S; s += 64)
+        if (st_st[(size_t)s * C + c] != 0) okflag = 0;
+    // realised steps exactly as rvm_fd_params formed the stencil; gradient
+    if (lane < P) {
+        const double xp = x[(size_t)lane * C + c];
+        const double ax = fabs(xp) > fl[lane] ? fabs(xp) : fl[lane];
+        const double e = rel * ax;
+        const double d = (xp + e) - (xp - e);
+        const double g = (lp_st[(size_t)(1 + 2 * lane) * C + c] - lp_st[(size_t)(2 + 2 * lane) * C + c]) / d;
+        den[lane] = d;
+        gr[lane] = g;
+        xv[lane] = xp;
+        out.grad[(size_t)lane * C + c] = g;
+    }
+    __syncthreads();
+    // -H = (2/N) sum_e J_e^T (1/sigma_e^2) J_e, J_e[p] = (rv_e(x+e_p) - rv_e(x-e_p)) / den_p:
+    // K = 64/P epochs of J per chunk in LDS, each lane accumulates its upper-triangle entries
+    int tp[PER_LANE], tq[PER_LANE];
+    double acc[PER_LANE];
+#pragma unroll
+    for (int j = 0; j < PER_LANE; j++) {
+        const int idx = lane + 64 * j;
+        int p = 0, rem = idx;
+        while (p < P && rem >= P - p) {
+            rem -= P - p;
+            p++;
+        }
+        tp[j] = p;
+        tq[j] = p + rem;
+        acc[j] = 0.0;
+    }
+    // J in chunks of JCH epochs: every lane issues its loads of the chunk at once (the chunk's
+    // latency is paid once, not once per epoch), then the triangle accumulates from LDS
+    for (int e0 = 0; e0 < E; e0 += JCH) {
+        const int kmax = E - e0 < JCH ? E - e0 : JCH;
+        const int n = kmax * P;
+#pragma unroll 4
+        for (int idx = lane; idx < n; idx += 64) {
+            const int k = idx / P, p = idx - (idx / P) * P;
+            const double* re = rv + (size_t)(e0 + k) * SC;
+            Jc[idx] = (re[(size_t)(1 + 2 * p) * C + c] - re[(size_t)(2 + 2 * p) * C + c]) / den[p];
+        }
+        if (lane < kmax) wc[lane] = w[e0 + lane];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < PER_LANE; j++) {
+            if (lane + 64 * j < ntri) {
+                double a = acc[j];
+                for (int k = 0; k < kmax; k++) a += (Jc[k * P + tp[j]] * wc[k]) * Jc[k * P + tq[j]];
+                acc[j] = a;
+            }
+        }
+        __syncthreads();
+    }
+    const double fac = 2.0 / npoints;
+#pragma unroll
+    for (int j = 0; j < PER_LANE; j++) {
+        if (lane + 64 * j < ntri) {
+            const double a = fac * acc[j];
+            A[tp[j] * P + tq[j]] = a;
+            A[tq[j] * P + tp[j]] = a;
+        }
+    }
+    smala_metric_stage(P, C, c, lane, A, Qm, gr, xv, lt, inv, ra, rb, dn, rp, okflag, lp_st[c], alpha, eps, out);
+}
+
+// rvm_smala_metric: the same metric pipeline from exact derivatives (rvm_logl_derivs)
+__global__ __launch_bounds__(64) void smala_metric_kernel(int P, int C, const double* __restrict__ x,
+                                                          const double* __restrict__ lp,
+                                                          const int32_t* __restrict__ status,
+                                                          const double* __restrict__ grad,
+                                                          const double* __restrict__ hess, double alpha, double eps,
+                                                          SmalaCache out) {
+    constexpr int PM = RVM_SMALA_MAX_PARAMS;
+    __shared__ double A[PM * PM], Qm[PM * PM];
+    __shared__ double gr[PM], lt[PM], inv[PM], xv[PM];
+    __shared__ double ra[PM], rb[PM], dn[PM];
+    __shared__ int rp[PM];
+    __shared__ int okflag;
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (lane == 0) okflag = status[c] == RVM_STATUS_OK && isfinite(lp[c]) ? 1 : 0;
+    __syncthreads();
+    if (lane < P) {
+        const double g = grad[(size_t)lane * C + c];
+        gr[lane] = g;
+        xv[lane] = x[(size_t)lane * C + c];
+        out.grad[(size_t)lane * C + c] = g;
+        if (!isfinite(g)) okflag = 0;
+    }
+    for (int i = lane; i < P * P; i += 64) {
+        const int r = i / P, q = i - (i / P) * P;
+        // symmetric by construction (rvm_logl_derivs writes both triangles from one pair)
+        const double h = hess[(size_t)i * C + c];
+        A[r * P + q] = -h;
+        if (!isfinite(h)) okflag = 0;
+    }
+    __syncthreads();
+    if (!okflag) {  // keep the eigen-solver on finite numbers; the cache is marked not ok
+        for (int i = lane; i < P * P; i += 64) A[i] = (i / P == i % P) ? 1.0 : 0.0;
+        if (lane < P) gr[lane] = 0.0;
+    }
+    __syncthreads();
+    const int ok0 = okflag;
+    smala_metric_stage(P, C, c, lane, A, Qm, gr, xv, lt, inv, ra, rb, dn, rp, okflag, lp[c], alpha, eps, out);
+    if (lane == 0 && !ok0) out.ok[c] = 0;
 }
 
 __device__ __forceinline__ double box_muller_s(double u0, double u1) {
@@ -383,6 +437,13 @@ __global__ __launch_bounds__(64) void smala_accept_kernel(int P, int C, int64_t 
         cur.ok[c] = 1;
         if (accepted) accepted[c] += 1;
     }
+}
+
+hipError_t launch_smala_metric(int P, int C, const double* x, const double* lp, const int32_t* status,
+                               const double* grad, const double* hess, double alpha, double eps, const SmalaCache& out,
+                               hipStream_t st) {
+    smala_metric_kernel<<<C, 64, 0, st>>>(P, C, x, lp, status, grad, hess, alpha, eps, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,

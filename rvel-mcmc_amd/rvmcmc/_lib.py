@@ -58,6 +58,8 @@ SIGNATURES = {
     "rvm_abi_version": (C.c_int, []),
     "rvm_smala_derive": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _dp, C.c_double, _dp, _dp, _dp, _dp, _dp,
                                    C.c_double, C.c_double, C.c_double, C.POINTER(SmalaCache), _dp]),
+    "rvm_smala_metric": (C.c_int, [C.c_int32, C.c_int32, _dp, _dp, _dp, _dp, _dp, C.c_double, C.c_double,
+                                   C.POINTER(SmalaCache), _dp]),
     "rvm_smala_propose": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, C.POINTER(SmalaCache), C.c_double,
                                     C.c_uint64, C.c_uint64, _dp, _dp, _dp]),
     "rvm_smala_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, C.POINTER(SmalaCache), _dp,

@@ -108,9 +108,14 @@ class SmalaChains:
     Per step (mcmc.py:167-187 for every chain at once): rvm_smala_propose, one likelihood launch
     over the (2P+1)-point stencil of the proposals (rvm_fd_params + rvm_logl_batch with rv_out),
     rvm_smala_derive (gradient, Gauss-Newton Hessian, SoftAbs metric by a per-chain Jacobi
-    eigen-solver, Cholesky, drift) and rvm_smala_accept.  No host synchronisation in step()."""
+    eigen-solver, Cholesky, drift) and rvm_smala_accept.  No host synchronisation in step().
 
-    def __init__(self, initial_state, obs, eps, alpha, n_chains, X0=None, seed=0, device=None, rel_step=FD_REL_STEP):
+    hessian="exact": the reference's metric -- exact gradient and Hessian of logp from
+    rvm_logl_derivs (state.py:253-294) and rvm_smala_metric -- instead of the FD stencil and the
+    Gauss-Newton Hessian (BASELINE config 4 names the FD variant)."""
+
+    def __init__(self, initial_state, obs, eps, alpha, n_chains, X0=None, seed=0, device=None, rel_step=FD_REL_STEP,
+                 hessian="gauss-newton"):
         torch = _torch()
         self.state = initial_state.deepcopy()
         self.obs = obs
@@ -120,6 +125,9 @@ class SmalaChains:
         if self.P > _lib.RVM_SMALA_MAX_PARAMS:
             raise ValueError(f"SMALA supports at most {_lib.RVM_SMALA_MAX_PARAMS} free parameters")
         self.n = int(n_chains)
+        if hessian not in ("gauss-newton", "exact"):
+            raise ValueError("hessian must be 'gauss-newton' or 'exact'")
+        self.hessian = hessian
         self.rel_step = float(rel_step)
         self.seed = int(seed)
         self.device = torch.device(device) if device is not None else engine.default_device()
@@ -157,6 +165,13 @@ class SmalaChains:
 
     def _derive_into(self, X, cache):
         st_h = _lib.stream_handle()
+        if self.hessian == "exact":
+            lp, g, H, st = self.state.get_logp_d_dd_batch(self.obs, X, hill_factor=1.0, pmap=self.pmap)
+            _lib.check(self.lib.rvm_smala_metric(self.P, self.n, X.data_ptr(), lp.data_ptr(), st.data_ptr(),
+                                                 g.data_ptr(), H.data_ptr(), self.alpha, self.eps,
+                                                 C.byref(cache["_c"]), st_h), "rvm_smala_metric")
+            self._keep = (lp, g, H, st)  # alive until the stream has consumed them
+            return
         _lib.check(self.lib.rvm_fd_params(self.P, self.n, X.data_ptr(), self.rel_step, self.floor.data_ptr(),
                                           self.stencil.data_ptr(), st_h), "rvm_fd_params")
         lp, st, rv = self.state.get_logp_batch(self.obs, self.stencil, hill_factor=1.0, want_rv=True, pmap=self.pmap)

@@ -96,6 +96,25 @@ def config4(chains=256, steps=10):
             "ms_per_step": 1e3 * dt / steps, "acceptance": float(sm.accepted.double().mean().item() / sm.iteration)}
 
 
+def config4x(chains=256, steps=5):
+    """config 4 with the reference's metric: exact gradient + Hessian (rvm_logl_derivs, one
+    hyper-dual integration per chain and parameter pair: P(P+1)/2 = 55 per chain-step)."""
+    np.random.seed(2017)
+    s = State(planets=[dict(p) for p in S2])
+    obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=chains, seed=0, hessian="exact")
+    sm.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sm.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"config": "4x: SMALA, 256 chains, 10-dim, exact gradient + Hessian (hyper-dual, 55 pair integrations)",
+            "chain_steps_per_s": chains * steps / dt, "ms_per_step": 1e3 * dt / steps,
+            "acceptance": float(sm.accepted.double().mean().item() / sm.iteration)}
+
+
 def config5(W=8192):
     np.random.seed(2017)
     s = State(planets=[dict(p) for p in S2] + [dict(THIRD)])
@@ -120,9 +139,9 @@ def config1(steps=200):
 
 
 def main():
-    which = sys.argv[1:] or ["2", "2w", "3", "4", "5", "1"]
+    which = sys.argv[1:] or ["2", "2w", "3", "4", "4x", "5", "1"]
     for c in which:
-        out = {"1": config1, "2": config2, "2w": config2w, "3": config3, "4": config4, "5": config5}[c]()
+        out = {"1": config1, "2": config2, "2w": config2w, "3": config3, "4": config4, "4x": config4x, "5": config5}[c]()
         print(json.dumps(out), flush=True)
 
 

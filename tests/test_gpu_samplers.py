@@ -255,6 +255,49 @@ def test_smala_derive_matches_numpy_softabs():
         assert abs(c["logdet"][i] - ref["logdet"]) < 1e-9 * max(1.0, abs(ref["logdet"]))
 
 
+def test_smala_exact_metric_matches_numpy_softabs():
+    """SmalaChains(hessian="exact"): rvm_logl_derivs + rvm_smala_metric (the reference's exact
+    Hessian, state.py:253-294) vs numpy SoftAbs on the same exact derivatives; then a few steps."""
+    torch = _torch()
+    from rvmcmc.smala import SmalaChains
+
+    s, obs = _state_and_obs()
+    C_, dim = 12, s.Nvars
+    rng = np.random.default_rng(8)
+    scales = np.array([S2_SCALES[k] for k in s.get_rawkeys()])
+    X0 = (s.get_params()[None] + 1e-3 * scales * rng.standard_normal((C_, dim))).T.copy()
+    sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=C_, X0=X0, seed=3, hessian="exact")
+    lp, g, H, st = sm.state.get_logp_d_dd_batch(obs, torch.as_tensor(X0, device="cuda"), hill_factor=1.0)
+    lp, g, H = lp.cpu().numpy(), g.cpu().numpy(), H.cpu().numpy()
+    c = {k: v.cpu().numpy() for k, v in sm.cache.items() if k != "_c"}
+    np.testing.assert_array_equal(c["lp"], lp)
+    np.testing.assert_array_equal(c["grad"], g)
+    assert (c["ok"] == 1).all()
+    for i in range(C_):
+        ref = _smala_numpy(lp[i], g[:, i], H[:, :, i], X0[:, i], 1e3, 0.5)
+        G = c["G"][:, i].reshape(dim, dim)
+        L = c["L"][:, i].reshape(dim, dim)
+        np.testing.assert_allclose(G, ref["G"], rtol=1e-9, atol=1e-9 * np.abs(ref["G"]).max())
+        np.testing.assert_allclose(L @ L.T, ref["Ginv"], rtol=1e-9, atol=1e-9 * np.abs(ref["Ginv"]).max())
+        np.testing.assert_allclose(c["mu"][:, i], ref["mu"], rtol=1e-10, atol=1e-14)
+        assert abs(c["logdet"][i] - ref["logdet"]) < 1e-9 * max(1.0, abs(ref["logdet"]))
+    for _ in range(3):
+        sm.step()
+    assert np.isfinite(sm.cache["lp"].cpu().numpy()).all() and int(sm.accepted.sum()) > 0
+
+
+def test_reference_api_smala_step_with_exact_derivatives():
+    """mcmc.Smala (mcmc.py:126-187, host control flow) on State.get_logp_d_dd's exact derivatives."""
+    from rvmcmc.smala import Smala
+
+    s, obs = _state_and_obs()
+    np.random.seed(3)
+    sm = Smala(s, obs, eps=0.3, alp=1e3)
+    acc = sum(bool(sm.step()) for _ in range(4))
+    lp, g, H = sm.state.get_logp_d_dd(obs)
+    assert np.isfinite(lp) and np.isfinite(g).all() and np.allclose(H, H.T) and acc >= 1
+
+
 def test_smala_step_matches_numpy_with_injected_draws():
     """One device SMALA step with injected z and u == mcmc.py:167-187 restated in numpy on the
     device's cached derivatives (proposal bit-close, decisions identical away from ties)."""
