@@ -5,7 +5,8 @@
 * Ensemble                    mcmc.py:40-75   (emcee 2.2.1 stretch move; here the whole ensemble
                                                lives on the GPU, see ensemble.EnsembleSampler)
 * Mh                          mcmc.py:80-121  (single chain, host RNG as the reference)
-* Smala                       mcmc.py:126-187 (SoftAbs SMALA; derivatives by finite differences)
+* Smala                       mcmc.py:126-187 (SoftAbs SMALA on State.get_logp_d_dd: exact
+                                               derivatives, rvm_logl_derivs)
 * MhChains                    batched independent MH chains on the device (new; the batched
                               counterpart of Mh, one logL launch per step for all chains)
 """
