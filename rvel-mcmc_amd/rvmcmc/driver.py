@@ -1,8 +1,10 @@
 """Run orchestration and chain diagnostics (mirror of the non-plotting parts of /root/reference/driver.py).
 
-Kept: McmcBundle (driver.py:20-33), auto_correlation (:37-43), run_mh / run_emcee / run_smala
-(:57-147), create_obs / read_obs / save_obs (:207-222), efficacy (:412-414), calc_kstatistic
-(:423-425), the per-parameter "AC time" of plot_ACTimes / inLinePlotEmceeAcTimes (:343-410).
+Kept: McmcBundle (driver.py:20-33), auto_correlation (:37-43), writing_to_log (:45-53),
+run_mh / run_emcee / run_smala (:57-147), pre_eps_smala (:149-169), create_obs / read_obs /
+save_obs (:207-222), the non-plotting part of return_trimmed_results (:265-333, trimmed_results),
+efficacy (:412-414), calc_kstatistic (:423-425), load_data / save_data / save_aux_* (:429-448), the
+per-parameter "AC time" of plot_ACTimes / inLinePlotEmceeAcTimes (:343-410).
 Plotting (matplotlib, corner) is out of scope.  Bugs listed as "do not reproduce" in SURVEY.md
 App. C are fixed: save_obs writes the error column, chains are preallocated instead of
 np.append-grown, and run_emcee's acceptance rate counts walkers, not coordinates.
@@ -144,6 +146,87 @@ def save_obs(obs, true_state, label):  # driver.py:215-222 (writes err, not rv, 
     fn = 'obs_{ha}.vels'.format(ha=h.hexdigest())
     np.savetxt(fn, np.c_[col1, col2, col3])
     return fn
+
+
+def writing_to_log(obj, name, logging):  # driver.py:45-53 (the reference's file name is a NameError)
+    """Append every element of obj, space separated, as one line of the file log<name>."""
+    if not logging:
+        return
+    with open("log{r}".format(r=name), "a") as f:
+        f.write(" ".join("{v}".format(v=v) for _, v in np.ndenumerate(np.asarray(obj, dtype=object))) + " \n")
+
+
+def pre_eps_smala(true_state, obs, eps, alpha, Niter, rng=None, max_rounds=50):  # driver.py:149-169
+    """Tune SMALA's eps until a trial run of Niter accepted steps has an acceptance rate in
+    [0.52, 0.68]: outside it, eps moves down (rate too low) or up (too high) by
+    |N(0.065, 0.025)| * 8 |rate - 0.6| (positive draws only), as the reference's recursion does;
+    iterative here, with a bound on the rounds."""
+    rng = rng if rng is not None else np.random
+    for _ in range(max_rounds):
+        smala = mcmc.Smala(true_state, obs, eps, alpha)
+        print("Trying out eps = {e}".format(e=eps))
+        tries = 0
+        for i in range(Niter):
+            tries += smala.step_force()
+        rate = float(Niter) / tries
+        print("Acc. Rate was {a}".format(a=rate))
+        if 0.52 <= rate <= 0.68:
+            return eps
+        mod = 0.0
+        while mod <= 0.0:
+            mod = rng.normal(loc=0.065, scale=0.025) * 8. * abs(rate - 0.6)
+        eps = eps - mod if rate < 0.52 else eps + mod
+    return eps
+
+
+def trimmed_results(bundle, burn_in_fraction, take_every_n=1):
+    """The non-plotting part of return_trimmed_results (driver.py:265-333): the chain after the
+    burn-in fraction (per walker block for an emcee bundle, whose chain stacks Niter/Nwalkers
+    iterations of each walker), thinned to every n-th index, as (states, chainlogp, average state)."""
+    Niter, chain, chainlogp = bundle.mcmc_Niter, bundle.mcmc_chain, bundle.mcmc_chainlogp
+    base = bundle.mcmc.state
+    if bundle.mcmc_is_emcee:
+        per = Niter // bundle.mcmc_Nwalkers
+        idx = [c for w in range(bundle.mcmc_Nwalkers) for c in range(int(w * per + per * burn_in_fraction), (w + 1) * per)]
+    else:
+        idx = list(range(int(Niter * burn_in_fraction), Niter))
+    idx = [c for c in idx if c % take_every_n == 0]
+    states = []
+    for c in idx:
+        s = base.deepcopy()
+        s.set_params(chain[c])
+        states.append(s)
+    avg = base.deepcopy()
+    avg.set_params(np.mean(np.asarray(chain)[idx], axis=0))
+    return states, np.asarray(chainlogp)[idx], avg
+
+
+def load_data(name, h):  # driver.py:429-430
+    return np.load('{n}_{h}.npy'.format(n=name, h=h.hexdigest()))
+
+
+def save_data(dat, name, h):  # driver.py:432-433
+    np.save('{n}_{h}'.format(n=name, h=h.hexdigest()), dat)
+
+
+def _save_aux(h, true_state, line):
+    with open('aux_{h}'.format(h=h.hexdigest()), "w") as f:
+        f.write('initial = ' + str(true_state.planets))
+        f.write("\n" + line)
+
+
+def save_aux_smala(h, true_state, label, Niter, eps, alpha):  # driver.py:435-438
+    _save_aux(h, true_state, "label, Niter, Eps, Alpha = '{l}', {n}, {e}, {a}".format(l=label, n=Niter, e=eps, a=alpha))
+
+
+def save_aux_emcee(h, true_state, label, Niter, Nwalkers, scal):  # driver.py:440-443
+    _save_aux(h, true_state, "label, Niter, Nwalkers, Scale = '{l}', {n}, {s}, {t}".format(l=label, n=Niter, s=Nwalkers,
+                                                                                           t=scal))
+
+
+def save_aux_mh(h, true_state, label, Niter, scal, step):  # driver.py:445-448
+    _save_aux(h, true_state, "label, Niter, Scale, Stepsize = '{l}', {n}, {s}, {t}".format(l=label, n=Niter, s=scal,
+                                                                                           t=step))
 
 
 def efficacy(Niter, AC, clocktimes):  # driver.py:412-414

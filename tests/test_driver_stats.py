@@ -46,3 +46,44 @@ def test_efficacy_reference_formula():
     clock = [t0, t0 + datetime.timedelta(seconds=1), t0 + datetime.timedelta(seconds=11)]
     # driver.py:412-414: Niter / ((clock[-1] - clock[1]) * max(AC))
     assert driver.efficacy(100, [2.0, 5.0], clock) == 100 / (10.0 * 5.0)
+
+
+def test_log_data_and_aux_files(tmp_path, monkeypatch):
+    """writing_to_log / save_data / load_data / save_aux_* (driver.py:45-53, 429-448): same file
+    names and line formats as the reference."""
+    from rvmcmc.state import State
+
+    monkeypatch.chdir(tmp_path)
+    s = State(planets=[{"m": 1.2e-3, "a": 0.88, "h": 0.2, "k": 0.0, "l": 0.3}])
+    h = driver._hash(s, "run")
+    driver.writing_to_log([1.5, 2.0], "_t", True)
+    driver.writing_to_log("START", "_t", True)
+    driver.writing_to_log([9.0], "_t", False)
+    assert open(tmp_path / "log_t").read().splitlines() == ["1.5 2.0 ", "START "]
+    driver.save_data(np.arange(4.0), "chain", h)
+    np.testing.assert_array_equal(driver.load_data("chain", h), np.arange(4.0))
+    driver.save_aux_mh(h, s, "run", 100, {"a": 0.3}, 0.01)
+    txt = open(tmp_path / f"aux_{h.hexdigest()}").read().splitlines()
+    assert txt[0].startswith("initial = [{'m': 0.0012") and txt[1] == "label, Niter, Scale, Stepsize = 'run', 100, {'a': 0.3}, 0.01"
+
+
+def test_trimmed_results_burn_in_and_thinning():
+    """return_trimmed_results (driver.py:265-333) without the plot: per-walker burn-in for emcee
+    bundles (chain = Niter/Nwalkers iterations of walker 0, then walker 1, ...)."""
+    from rvmcmc.state import State
+
+    s = State(planets=[{"m": 1.2e-3, "a": 0.88, "h": 0.2, "k": 0.0, "l": 0.3}])
+
+    class _M:
+        state = s
+
+    Niter, Nw = 40, 4
+    chain = np.tile(s.get_params(), (Niter, 1)) + np.arange(Niter)[:, None] * 1e-6
+    b = driver.McmcBundle(_M(), chain, -np.arange(Niter, dtype=float), [], None, Niter, s, is_emcee=True, Nwalkers=Nw)
+    states, lp, avg = driver.trimmed_results(b, 0.5, take_every_n=1)
+    idx = [c for w in range(Nw) for c in range(w * 10 + 5, (w + 1) * 10)]
+    np.testing.assert_array_equal(lp, -np.array(idx, dtype=float))
+    np.testing.assert_allclose(avg.get_params(), chain[idx].mean(0))
+    b2 = driver.McmcBundle(_M(), chain, -np.arange(Niter, dtype=float), [], None, Niter, s)
+    states, lp, _ = driver.trimmed_results(b2, 0.25, take_every_n=2)
+    assert list(-lp) == list(range(10, 40, 2)) and len(states) == 15
