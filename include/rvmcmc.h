@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 5
+#define RVM_ABI_VERSION 6
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -129,11 +129,14 @@ typedef struct rvm_param_map {
  * rvm_stretch_propose, Philox draws), the walker log-likelihood of the proposals (as
  * rvm_logl_batch on map(q)), and the accept (as rvm_stretch_accept), bit-identical to the
  * three-call sequence.  x: [n_params][n_s0] free parameters (in place), lnp [n_s0] (in place),
- * c: complement [n_params][n_s1]; n_s0 <= the plan's max_walkers.  lnp_new_out / status_out
- * (nullable): the proposals' logl and status; accepted (nullable): int32 counters += 1. */
+ * c_aos: the complement WALKER-MAJOR, [n_s1][n_params] (each c_j one contiguous row: one cache line
+ * per gathered walker instead of n_params), n_s0 <= the plan's max_walkers.  x_aos (nullable): a
+ * walker-major mirror [n_s0][n_params] of x that accepted proposals are written to as well (the
+ * next half-step's c_aos).  lnp_new_out / status_out (nullable): the proposals' logl and status;
+ * accepted (nullable): int32 counters += 1. */
 int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_s0,
-                          int64_t s0_begin, double* x, double* lnp, int32_t n_s1, const double* c, double a,
-                          uint64_t seed, uint64_t iteration, uint32_t half, double hill_factor,
+                          int64_t s0_begin, double* x, double* x_aos, double* lnp, int32_t n_s1, const double* c_aos,
+                          double a, uint64_t seed, uint64_t iteration, uint32_t half, double hill_factor,
                           double* lnp_new_out, int32_t* status_out, int32_t* accepted, void* stream);
 
 /* Gaussian random-walk Metropolis-Hastings (mcmc.py:89-121), n_chains independent chains:

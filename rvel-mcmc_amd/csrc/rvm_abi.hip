@@ -251,8 +251,8 @@ int rvm_logl_batch(const rvm_plan* plan, int32_t n_walkers, const double* params
 }
 
 int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_s0,
-                          int64_t s0_begin, double* x, double* lnp, int32_t n_s1, const double* c, double a,
-                          uint64_t seed, uint64_t iteration, uint32_t half, double hill_factor,
+                          int64_t s0_begin, double* x, double* x_aos, double* lnp, int32_t n_s1, const double* c,
+                          double a, uint64_t seed, uint64_t iteration, uint32_t half, double hill_factor,
                           double* lnp_new_out, int32_t* status_out, int32_t* accepted, void* stream) {
     if (!plan || !map) return fail(-1, "rvm_stretch_half_step: null plan or map");
     if (n_s0 == 0) return 0;
@@ -266,6 +266,7 @@ int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_
     rvm::StretchArgs sa{};
     sa.c = c;
     sa.x = x;
+    sa.x_aos = x_aos;
     sa.lnp = lnp;
     sa.accepted = accepted;
     sa.s0_begin = s0_begin;

@@ -35,8 +35,9 @@ struct DevPlan {
 // Fused stretch half-step (rvm_stretch_half_step) by value as a kernel argument; c == nullptr
 // for a plain likelihood launch.
 struct StretchArgs {
-    const double* c;    // complement half [dim][n1]
+    const double* c;    // complement half, walker-major [n1][dim] (one contiguous row per c_j)
     double* x;          // this half's free parameters [dim][W] (accepted proposals written back)
+    double* x_aos;      // walker-major mirror of x [W][dim] kept in step on accept (nullable)
     double* lnp;        // their log-probabilities [W]
     int32_t* accepted;  // accept counters [W] (nullable)
     int64_t s0_begin;   // global index of walker 0 of x (Philox key)

@@ -103,7 +103,7 @@ __device__ __forceinline__ double walker_param(bool stretch, const double* __res
     if (!stretch) return params[(size_t)r * W + w];
     const int k = sa.src[r];
     if (k < 0) return sa.base[r];
-    return stretch_q(sa.c[(size_t)k * sa.n1 + j], z, sa.x[(size_t)k * W + w]);
+    return stretch_q(sa.c[(size_t)j * sa.dim + k], z, sa.x[(size_t)k * W + w]);
 }
 
 __device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, int gi, int r, double v) {
@@ -422,8 +422,13 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                     const double z = l_q[R * GW + gl], u3 = l_q[(R + 1) * GW + gl];
                     if (stretch_accepts(sa.dim, z, lp, l_q[(R + 2) * GW + gl], u3)) {
 #pragma unroll
-                        for (int r = 0; r < R; r++)
-                            if (sa.src[r] >= 0) sa.x[(size_t)sa.src[r] * W + wo] = l_q[r * GW + gl];
+                        for (int r = 0; r < R; r++) {
+                            if (sa.src[r] >= 0) {
+                                const double v = l_q[r * GW + gl];
+                                sa.x[(size_t)sa.src[r] * W + wo] = v;
+                                if (sa.x_aos) sa.x_aos[(size_t)wo * sa.dim + sa.src[r]] = v;
+                            }
+                        }
                         sa.lnp[wo] = lp;
                         if (sa.accepted) sa.accepted[wo] += 1;
                     }

@@ -203,24 +203,28 @@ class LoglPlan:
         _lib.check(rc, "rvm_logl_derivs")
         return lp, grad, hess, st
 
-    def stretch_half_step(self, pmap, X0, lnp0, c, s0_begin, a, seed, iteration, half, hill_factor=1.0,
-                          lnp_new=None, status=None, accepted=None, stream=None):
+    def stretch_half_step(self, pmap, X0, lnp0, c_aos, s0_begin, a, seed, iteration, half, hill_factor=1.0,
+                          lnp_new=None, status=None, accepted=None, X0_aos=None, stream=None):
         """Fused emcee stretch half-step (rvm_stretch_half_step): propose against the complement
-        c [dim][n1], walker logL of the proposals, accept -- one launch.  X0 [dim][n0] and lnp0
-        [n0] are updated in place; lnp_new / status (optional) receive the proposals' logl."""
+        c_aos [n1][dim] (walker-major), walker logL of the proposals, accept -- one launch.  X0
+        [dim][n0] and lnp0 [n0] are updated in place, and X0_aos [n0][dim] (optional, the
+        walker-major mirror of X0) too; lnp_new / status (optional) receive the proposals' logl."""
         torch = _torch()
-        for t in (X0, lnp0, c):
+        for t in (X0, lnp0, c_aos) + ((X0_aos,) if X0_aos is not None else ()):
             if t.dtype != torch.float64 or t.device != self.device or not t.is_contiguous():
-                raise ValueError("X0, lnp0, c must be contiguous float64 tensors on the plan's device")
+                raise ValueError("X0, lnp0, c_aos, X0_aos must be contiguous float64 tensors on the plan's device")
         dim, n0 = X0.shape
-        if c.shape[0] != dim or lnp0.shape != (n0,):
-            raise ValueError("shape mismatch between X0, lnp0 and c")
+        if c_aos.dim() != 2 or c_aos.shape[1] != dim or lnp0.shape != (n0,):
+            raise ValueError("shape mismatch between X0 [dim][n0], lnp0 [n0] and c_aos [n1][dim]")
+        if X0_aos is not None and X0_aos.shape != (n0, dim):
+            raise ValueError("X0_aos must be [n0][dim]")
         if n0 > self.max_walkers:
             raise ValueError(f"{n0} walkers exceed the plan's max_walkers={self.max_walkers}")
         with torch.cuda.device(self.device):
             rc = self.lib.rvm_stretch_half_step(
-                self._h, C.byref(pmap.c_map()), dim, n0, int(s0_begin), X0.data_ptr(), lnp0.data_ptr(), c.shape[1],
-                c.data_ptr(), float(a), int(seed), int(iteration), int(half), float(hill_factor),
+                self._h, C.byref(pmap.c_map()), dim, n0, int(s0_begin), X0.data_ptr(),
+                X0_aos.data_ptr() if X0_aos is not None else 0, lnp0.data_ptr(), c_aos.shape[0], c_aos.data_ptr(),
+                float(a), int(seed), int(iteration), int(half), float(hill_factor),
                 lnp_new.data_ptr() if lnp_new is not None else 0, status.data_ptr() if status is not None else 0,
                 accepted.data_ptr() if accepted is not None else 0, _lib.stream_handle(stream))
         _lib.check(rc, "rvm_stretch_half_step")

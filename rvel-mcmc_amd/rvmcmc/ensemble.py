@@ -18,7 +18,10 @@ index), so a run is reproducible and identical for any number of ranks.
 
 Multi-GPU (one process per GPU, torch.distributed over RCCL/xGMI): each rank owns a contiguous
 slice of each half; before each half-step the complement half's positions are all-gathered
-(dim x W/2 float64 -- the only collective on the data path).
+(dim x W/2 float64 -- the only collective on the data path).  The fused half-step reads the
+complement walker-major ([W/2][dim], one contiguous row per gathered c_j); each half keeps a
+walker-major mirror next to its [dim][n] positions, updated by the same launch on accept, so the
+gather needs no re-layout.
 """
 from __future__ import annotations
 
@@ -71,16 +74,18 @@ class DeviceOps:
             self.status_counts.index_add_(0, st.long(), torch.ones_like(st, dtype=torch.int64))
         return lp, st
 
-    def fused_half_step(self, X0, lnp0, c, half, lnp_new, status, accepted):
+    def fused_half_step(self, X0, X0_aos, lnp0, c_aos, half, lnp_new, status, accepted):
         """propose + logl + accept in one likelihood launch (rvm_stretch_half_step), bit-identical
-        to the three-launch sequence with Philox draws."""
+        to the three-launch sequence with Philox draws.  c_aos: the complement walker-major
+        [n1][dim]; X0_aos: this half's walker-major mirror (updated on accept with X0)."""
         torch = _torch()
         s = self.s
         if self.timing is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        self.plan.stretch_half_step(s.pmap, X0, lnp0, c.contiguous(), s.global_begin(half), s.a, s.seed, s.iteration,
-                                    half, s.hill_factor, lnp_new=lnp_new, status=status, accepted=accepted)
+        self.plan.stretch_half_step(s.pmap, X0, lnp0, c_aos, s.global_begin(half), s.a, s.seed, s.iteration,
+                                    half, s.hill_factor, lnp_new=lnp_new, status=status, accepted=accepted,
+                                    X0_aos=X0_aos)
         if self.timing is not None:
             e1.record()
             self.timing.append((e0, e1, X0.shape[1]))
@@ -135,6 +140,8 @@ class EnsembleSampler:
         self._status = torch.empty(n, dtype=torch.int32, device=self.device)
         self._c_full = torch.empty((dim, self.halfk), **f64)
         self._gather = torch.empty(self.world * dim * n, **f64) if self.world > 1 else None
+        self._gather_aos = torch.empty((self.halfk, dim), **f64) if self.world > 1 else None
+        self._aos_stale = True  # pos_aos (walker-major mirrors for the fused path) out of date
         self.naccepted = torch.zeros(2 * n, dtype=torch.int32, device=self.device)
         self.nevals = 0
         # one launch per half-step (rvm_stretch_half_step) unless draws are injected or the ops
@@ -173,15 +180,36 @@ class EnsembleSampler:
         self._c_full.copy_(g.permute(1, 0, 2).reshape(self.dim, self.halfk))
         return self._c_full
 
+    def _complement_aos(self, other):
+        """Full complement half walker-major [W/2][dim] in global order: this rank's mirror, or
+        the all-gather of every rank's (rank r holds walkers [r nloc, (r+1) nloc) of the half, so
+        the gathered blocks are already in global order: no re-layout copy)."""
+        torch = _torch()
+        if self.world == 1:
+            return self.pos_aos[other]
+        torch.distributed.all_gather_into_tensor(self._gather_aos, self.pos_aos[other], group=self.group)
+        return self._gather_aos
+
+    def _refresh_aos(self):
+        self.pos_aos = [p.t().contiguous() for p in self.pos]
+        self._aos_stale = False
+
     def half_step(self, X0, lnp0, Xc, half, draws_propose=None, draws_accept=None):
-        """Update this rank's slice X0 [dim][nloc] (in place) against the complement half."""
-        c = self._complement(Xc)
+        """Update this rank's slice X0 = pos[half] [dim][nloc] (in place) against the complement
+        half Xc = pos[1 - half]."""
         n = self.nloc
         if self.fused and draws_propose is None and draws_accept is None:
-            self.ops.fused_half_step(X0, lnp0, c, half, self._lnp_new, self._status,
+            if X0 is not self.pos[half] or Xc is not self.pos[1 - half]:
+                raise ValueError("the fused half-step updates the sampler's own halves (pos[half], pos[1 - half])")
+            if self._aos_stale:
+                self._refresh_aos()
+            c = self._complement_aos(1 - half)
+            self.ops.fused_half_step(X0, self.pos_aos[half], lnp0, c, half, self._lnp_new, self._status,
                                      self.naccepted[half * n:(half + 1) * n])
             self.nevals += n
             return
+        c = self._complement(Xc)
+        self._aos_stale = True
         self.ops.propose(X0, c, half, self._q, self._z, draws_propose)
         self.lnprob(self._q, out=self._lnp_new, status=self._status)
         self.ops.accept(X0, lnp0, self._q, self._lnp_new, self._z, half, self.naccepted[half * n:(half + 1) * n],
@@ -197,6 +225,8 @@ class EnsembleSampler:
             raise ValueError(f"positions must be [{self.k}][{self.dim}]")
         s0, s1 = self.local_slices()
         self.pos = [Xg[s0].t().contiguous(), Xg[s1].t().contiguous()]
+        self.pos_aos = [Xg[s0].contiguous(), Xg[s1].contiguous()]
+        self._aos_stale = False
         self.lnp = [None, None]
 
     def compute_lnprob(self):

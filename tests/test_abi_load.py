@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_python_binding_matches_header():
@@ -46,7 +46,7 @@ def test_argument_errors_do_not_touch_the_device():
     assert rc < 0 and b"n_planets" in lib.rvm_last_error()
     assert lib.rvm_logl_batch(None, 1, 0, 1.0, 0, 0, 0, 0) < 0
     m = _lib.ParamMapC()
-    assert lib.rvm_stretch_half_step(None, C.byref(m), 10, 1, 0, 0, 0, 1, 0, 2.0, 0, 0, 0, 1.0, 0, 0, 0, 0) < 0
+    assert lib.rvm_stretch_half_step(None, C.byref(m), 10, 1, 0, 0, 0, 0, 1, 0, 2.0, 0, 0, 0, 1.0, 0, 0, 0, 0) < 0
     rows = (C.c_int32 * 2)(0, 1)
     assert lib.rvm_logl_derivs(None, 1, 0, 2, rows, 1.0, 0, 0, 0, 0, 0, 0) < 0
     # workspace: per (chain, pair i >= j) and direction, 4 f64 partial sums and an int32 status

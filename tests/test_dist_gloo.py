@@ -67,18 +67,36 @@ class NumpyOps:
         accepted += acc_t.to(torch.int32)
 
 
+class FusedNumpyOps(NumpyOps):
+    """NumpyOps plus the fused half-step's contract (rvm_stretch_half_step): the complement arrives
+    walker-major [W/2][dim] (gathered from the ranks' walker-major mirrors, no re-layout) and the
+    half's mirror X0_aos is kept in step with X0."""
+
+    def fused_half_step(self, X0, X0_aos, lnp0, c_aos, half, lnp_new, status, accepted):
+        s = self.s
+        assert c_aos.shape == (s.halfk, s.dim) and X0_aos.shape == (s.nloc, s.dim)
+        np.testing.assert_array_equal(X0_aos.numpy(), X0.t().numpy())  # mirror in step before
+        q = torch.empty_like(X0)
+        z = torch.empty(s.nloc, dtype=torch.float64)
+        self.propose(X0, c_aos.t().contiguous(), half, q, z)
+        self.logl(q, out=lnp_new, status=status)
+        self.accept(X0, lnp0, q, lnp_new, z, half, accepted)
+        X0_aos.copy_(X0.t())
+
+
 def _initial_positions(state):
     rng = np.random.default_rng(3)
     scales = np.array([S2_SCALES[k] for k in state.get_rawkeys()])
     return state.get_params()[None] + 1e-3 * scales * rng.standard_normal((W, state.Nvars))
 
 
-def _run_sampler():
+def _run_sampler(fused=False):
     from rvmcmc.ensemble import EnsembleSampler
     from rvmcmc.state import State
 
     state = State(planets=[dict(p) for p in S2_PLANETS])
-    ens = EnsembleSampler(W, state, obs=None, seed=SEED, device="cpu", ops=NumpyOps)
+    ens = EnsembleSampler(W, state, obs=None, seed=SEED, device="cpu", ops=FusedNumpyOps if fused else NumpyOps)
+    assert ens.fused == fused
     ens.set_positions(_initial_positions(state))
     ens.compute_lnprob()
     for _ in range(ITERS):
@@ -86,12 +104,12 @@ def _run_sampler():
     return ens.gather_positions(), ens.gather_lnprob(), ens.naccepted.clone()
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, fused=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pos, lnp, acc = _run_sampler()
+        pos, lnp, acc = _run_sampler(fused)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), pos=pos, lnp=lnp, acc=acc.numpy())
     finally:
         dist.destroy_process_group()
@@ -105,10 +123,16 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_sharded_ensemble_bit_identical_to_single_process(tmp_path, world):
+@pytest.mark.parametrize("world,fused", [(2, False), (4, False), (2, True), (4, True)])
+def test_sharded_ensemble_bit_identical_to_single_process(tmp_path, world, fused):
+    """Three-launch path (SoA complement, all-gather + re-layout) and fused path (walker-major
+    complement gathered from the mirrors): every world size gives the single-process run."""
     pos1, lnp1, acc1 = _run_sampler()
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    if fused:
+        pf, lf, af = _run_sampler(fused=True)
+        np.testing.assert_array_equal(pf, pos1)
+        np.testing.assert_array_equal(lf, lnp1)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), fused), nprocs=world, join=True)
     accs = []
     for r in range(world):
         d = np.load(tmp_path / f"rank{r}.npz")
