@@ -38,8 +38,10 @@ __device__ __forceinline__ void pair_of(int p, int& i, int& j) {
     j = rem;
 }
 
-template <int NP, bool D3>
-__global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void derivs_kernel(const DevPlan P, const DerivArgs A,
+// MAXT: threads per block the kernel is compiled for (64 per Richardson level): 256 for plans of up
+// to 4 levels (one wave per SIMD: the whole 512-VGPR budget, no spills), 384 for 5-6 levels
+template <int NP, bool D3, int MAXT>
+__global__ __launch_bounds__(MAXT) void derivs_kernel(const DevPlan P, const DerivArgs A,
                                                                     const double* __restrict__ params,
                                                                     const double hill_factor,
                                                                     double* __restrict__ ws,
@@ -164,9 +166,10 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void derivs_kernel(const DevPl
         s.vz = jvz;
     }
     s.encm = 0;
+    lane_finish_hd(s);
     {
         LaneHD<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
-        kick_hd<NP, L, D3>(t0, 0.0);
+        kick_hd_any<NP, L, D3>(t0, 0.0);
         s.encm = t0.encm;
     }
 
@@ -179,7 +182,7 @@ __global__ __launch_bounds__(64 * RVM_MAX_LEVELS) void derivs_kernel(const DevPl
             const double h = S.seg_h1[e] * inv_mult;
             drift_hd<D3>(s, 0.5 * h);
             for (int j = 0; j < ns; j++) {
-                kick_hd<NP, L, D3>(s, h);
+                kick_hd_any<NP, L, D3>(s, h);
                 drift_hd<D3>(s, j == ns - 1 ? 0.5 * h : h);
             }
         }
@@ -256,7 +259,13 @@ hipError_t launch_derivs(const DevPlan& P, int C, const double* params, int n_di
     const int n_items = C * A.n_pairs;
     const dim3 grid((n_items + wpb - 1) / wpb, 2);
     const dim3 block(64 * P.n_levels);
-#define RVM_LAUNCH(NPV, D3V) derivs_kernel<NPV, D3V><<<grid, block, 0, stream>>>(P, A, params, hill_factor, ws, wst)
+#define RVM_LAUNCH(NPV, D3V)                                                                     \
+    do {                                                                                         \
+        if (P.n_levels <= 4)                                                                     \
+            derivs_kernel<NPV, D3V, 256><<<grid, block, 0, stream>>>(P, A, params, hill_factor, ws, wst); \
+        else                                                                                     \
+            derivs_kernel<NPV, D3V, 64 * RVM_MAX_LEVELS><<<grid, block, 0, stream>>>(P, A, params, hill_factor, ws, wst); \
+    } while (0)
     const bool inc = P.inclined != 0;
     switch (P.n_planets) {
         case 1:

@@ -41,16 +41,18 @@ __device__ __forceinline__ HD operator*(HD x, HD y) {
 __device__ __forceinline__ HD hd_chain(double f, double f1, double f2, HD x) {
     return HD{f, f1 * x.a, f1 * x.b, fma(f1, x.ab, (f2 * x.a) * x.b)};
 }
+// reciprocals and square roots from v_rcp_f64 / v_rsq_f64 with one cubic refinement (rvm_device.h
+// rcp_nr / rsq_nr: faithfully rounded, no IEEE division sequence)
 __device__ __forceinline__ HD hd_inv(HD x) {
-    const double f = 1.0 / x.v;
+    const double f = rcp_nr(x.v);
     return hd_chain(f, -f * f, 2.0 * f * f * f, x);
 }
 __device__ __forceinline__ HD operator/(HD x, HD y) { return x * hd_inv(y); }
 __device__ __forceinline__ HD operator/(HD x, double s) { return (1.0 / s) * x; }
 __device__ __forceinline__ HD operator/(double s, HD x) { return s * hd_inv(x); }
 __device__ __forceinline__ HD hd_sqrt(HD x) {
-    const double f = sqrt(x.v);
-    return hd_chain(f, 0.5 / f, -0.25 / (f * x.v), x);
+    const double y = rsq_nr(x.v), f = x.v * y;  // y = 1/sqrt(x)
+    return hd_chain(f, 0.5 * y, (-0.25 * y) * (y * y), x);
 }
 __device__ __forceinline__ HD hd_sin(HD x) {
     double s, c;
@@ -125,24 +127,38 @@ __device__ __forceinline__ void gfun_hd(HD X, HD beta, HD& G0, HD& G1, HD& G2, H
     G3 = X2 * X * c3;
 }
 
-// Primal universal-Kepler solve (converged Halley from a third-order guess with the full Stumpff
-// evaluation, bracketed fallback for hard steps), per lane.
+// Primal universal-Kepler root for the hyper-dual drift, per lane: Halley steps from the
+// fourth-order Taylor guess of rvm_device.h drift (8-term Stumpff series for |z| <= 0.3, the full
+// evaluation beyond), stopped once a correction is below 1e-6 |X| -- Halley is cubic, so the
+// remaining error is ~1e-18 |X|, and drift_hd's hyper-dual quadratic-model step refines the root
+// once more -- with the bracketed solver for hard steps or no convergence.
 __device__ __forceinline__ double kepler_primal(double r0, double eta, double zeta, double beta, double GM,
                                                 double dt) {
-    const double u = dt / r0, sg = eta / r0, g = GM / r0;
-    double X = u * (1.0 + u * (-0.5 * sg + u * (0.5 * sg * sg + (beta - g) / 6.0)));
+    const double ir0 = rcp_nr(r0);
+    const double u = dt * ir0, sg = eta * ir0, g = GM * ir0;
+    const double hs = 0.5 * sg;
+    const double T3 = fma(hs, sg, (beta - g) * (1.0 / 6.0));
+    const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
+    double X = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
     bool done = false;
     if (fabs(beta) * (u * u) <= 0.5) {
         for (int it = 0; it < 12 && !done; it++) {
+            const double X2 = X * X, z = beta * X2;
             double c0, c1, c2, c3;
-            stumpff_full(beta * X * X, c0, c1, c2, c3);
-            const double G1 = X * c1, G2 = X * X * c2, G3 = X * X * X * c3;
-            const double f = r0 * G1 + eta * G2 + GM * G3 - dt;
-            const double fp = r0 * c0 + eta * G1 + GM * G2;
-            const double fpp = eta * c0 + zeta * G1;
-            const double dX = f * fp / (fp * fp - 0.5 * f * fpp);
+            if (fabs(z) <= 0.3) {
+                stumpff23<8>(z, c2, c3);
+                c1 = fma(-z, c3, 1.0);
+                c0 = fma(-z, c2, 1.0);
+            } else {
+                stumpff_full(z, c0, c1, c2, c3);
+            }
+            const double G1 = X * c1, G2 = X2 * c2, G3 = X2 * X * c3;
+            const double f = fma(GM, G3, fma(eta, G2, fma(r0, G1, -dt)));
+            const double fp = fma(GM, G2, fma(eta, G1, r0 * c0));
+            const double fpp = fma(zeta, G1, eta * c0);
+            const double dX = (f * fp) * rcp_nr(fma(-0.5 * f, fpp, fp * fp));
             X -= dX;
-            done = !(fabs(dX) > 4e-16 * fabs(X)) || !isfinite(dX);
+            done = !(fabs(dX) > 1e-6 * fabs(X)) || !isfinite(dX);
         }
     }
     if (!done || !isfinite(X)) {
@@ -160,13 +176,21 @@ struct LaneHD {
     HD m[NP];       // planet masses
     HD iMi[NP + 1]; // 1 / interior masses (iMi[0] = 1)
     HD mu[NP];      // m_q / M_q
+    HD kA, kB, kC;  // closed-form two-planet kick coefficients of the own lane (kick2_hd)
+    HD c12;         // m_1 / M_1 (heliocentric x_2 = r'_2 + c12 r'_1)
     double dmin2;   // (hill_factor * max r_Hill)^2, primal (the encounter test is a primal decision)
     int p;
     uint64_t encm;
 };
 
-// Kepler drift of the own coordinate by dt (rvm_device.h drift, same physics): primal solve, two
-// hyper-dual Newton steps from the root, Gauss f and g.
+// Kepler drift of the own coordinate by dt (rvm_device.h drift, same physics).  The primal root X
+// of F(X) = r0 G1 + eta G2 + GM G3 - dt comes from kepler_primal; the G-functions are evaluated
+// ONCE, in hyper-dual arithmetic at that fixed X (their variations then carry only the
+// dependence on beta), and the variations of the root follow from the quadratic model
+//   F + F_X d + F_XX d^2 / 2 = 0,   d = X_hd - X:   d0 = -F / F_X,  d = -(F + F_XX d0^2 / 2) / F_X
+// (exact to second order: d0^2 has only an order-2 part), with F_X = r, F_XX = eta G0 + zeta G1.
+// G_k(X + d) = G_k + G_k' d + G_k'' d^2 / 2 with G_k' = G_(k-1), G_0' = -beta G1, G_0'' = -beta G0,
+// G_1'' = -beta G1.
 template <bool D3, int NP>
 __device__ __forceinline__ void drift_hd(LaneHD<NP>& s, double dt) {
     HD r2 = s.rx * s.rx + s.ry * s.ry;
@@ -181,22 +205,29 @@ __device__ __forceinline__ void drift_hd(LaneHD<NP>& s, double dt) {
     const HD ir0 = hd_inv(r0);
     const HD beta = 2.0 * (s.GM * ir0) - v2;
     const HD zeta = s.GM - beta * r0;
-    HD X = hd_c(kepler_primal(r0.v, eta.v, zeta.v, beta.v, s.GM.v, dt));
-    HD G0, G1, G2, G3;
-#pragma unroll
-    for (int it = 0; it < 2; it++) {
-        gfun_hd(X, beta, G0, G1, G2, G3);
-        const HD F = r0 * G1 + eta * G2 + s.GM * G3 - dt;
-        const HD Fp = r0 * G0 + eta * G1 + s.GM * G2;
-        X = X - F / Fp;
-    }
-    gfun_hd(X, beta, G0, G1, G2, G3);
-    const HD rr = r0 * G0 + eta * G1 + s.GM * G2;
+    const double X = kepler_primal(r0.v, eta.v, zeta.v, beta.v, s.GM.v, dt);
+    const double X2 = X * X;
+    HD c0, c1, c2, c3;
+    stumpff_hd(X2 * beta, c0, c1, c2, c3);
+    HD G0 = c0, G1 = X * c1, G2 = X2 * c2, G3 = (X2 * X) * c3;
+    const HD F = r0 * G1 + eta * G2 + s.GM * G3 - dt;
+    const HD Fx = r0 * G0 + eta * G1 + s.GM * G2;
+    const HD Fxx = eta * G0 + zeta * G1;
+    const HD iFx = hd_inv(Fx);
+    const HD d0 = -(F * iFx);
+    const HD d = -((F + 0.5 * (Fxx * (d0 * d0))) * iFx);
+    const HD hd2 = 0.5 * (d * d);
+    const HD nbG1 = -(beta * G1);
+    const HD H0 = G0 + nbG1 * d - (beta * G0) * hd2;
+    const HD H1 = G1 + G0 * d + nbG1 * hd2;
+    const HD H2 = G2 + G1 * d + G0 * hd2;
+    const HD H3 = G3 + G2 * d + G1 * hd2;
+    const HD rr = r0 * H0 + eta * H1 + s.GM * H2;
     const HD irr = hd_inv(rr);
-    const HD gG2 = s.GM * G2;
+    const HD gG2 = s.GM * H2;
     const HD f = 1.0 - gG2 * ir0;
-    const HD g = dt - s.GM * G3;
-    const HD fd = -((s.GM * G1) * (ir0 * irr));
+    const HD g = dt - s.GM * H3;
+    const HD fd = -((s.GM * H1) * (ir0 * irr));
     const HD gd = 1.0 - gG2 * irr;
     const HD rx = s.rx, ry = s.ry, vx = s.vx, vy = s.vy;
     s.rx = f * rx + g * vx;
@@ -208,6 +239,41 @@ __device__ __forceinline__ void drift_hd(LaneHD<NP>& s, double dt) {
         s.rz = f * rz + g * vz;
         s.vz = fd * rz + gd * vz;
     }
+}
+
+// x^(-3/2)
+__device__ __forceinline__ HD hd_rcube(HD x) {
+    const double y = rsq_nr(x.v), y2 = y * y;
+    const double f = y2 * y;  // x^(-3/2); x^(-1) = y^2
+    return hd_chain(f, -1.5 * f * y2, 3.75 * f * (y2 * y2), x);
+}
+
+// Two-planet kick in closed form (rvm_device.h kick2, same interaction), hyper-dual:
+//   v' += dt [ A r'/|r'|^3 + B x2/r02^3 + C d12/r12^3 ]
+// with the lane's (A, B, C) = (0, -m2, m2) for planet 1 and (M2, -M2/M1, -m1 M2/M1) for planet 2
+// (LaneHD::kA/kB/kC, set by lane_finish_hd); the encounter bit of planet 1's lane is the one read.
+template <int L, bool D3>
+__device__ __forceinline__ void kick2_hd(LaneHD<2>& s, double dt) {
+    const HD x1 = grp_get_hd<L, 0>(s.rx), y1 = grp_get_hd<L, 0>(s.ry);
+    const HD R2x = grp_get_hd<L, 1>(s.rx), R2y = grp_get_hd<L, 1>(s.ry);
+    const HD c = s.c12;
+    const HD x2 = R2x + c * x1, y2 = R2y + c * y1;
+    const HD dx = x2 - x1, dy = y2 - y1;
+    HD r02 = x2 * x2 + y2 * y2, r12 = dx * dx + dy * dy, own = s.rx * s.rx + s.ry * s.ry;
+    HD z2 = hd_c(0.0), dz = hd_c(0.0);
+    if constexpr (D3) {
+        const HD z1 = grp_get_hd<L, 0>(s.rz), R2z = grp_get_hd<L, 1>(s.rz);
+        z2 = R2z + c * z1;
+        dz = z2 - z1;
+        r02 = r02 + z2 * z2;
+        r12 = r12 + dz * dz;
+        own = own + s.rz * s.rz;
+    }
+    s.encm |= ballot(r02.v < s.dmin2) | ballot(r12.v < s.dmin2) | ballot(own.v < s.dmin2);
+    const HD A = s.kA * hd_rcube(own), B = s.kB * hd_rcube(r02), C = s.kC * hd_rcube(r12);
+    s.vx = s.vx + dt * (A * s.rx + B * x2 + C * dx);
+    s.vy = s.vy + dt * (A * s.ry + B * y2 + C * dy);
+    if constexpr (D3) s.vz = s.vz + dt * (A * s.rz + B * z2 + C * dz);
 }
 
 // Interaction kick (rvm_device.h kick_generic, same physics, hyper-dual): heliocentric positions
@@ -277,6 +343,27 @@ __device__ __forceinline__ void kick_hd(LaneHD<NP>& s, double dt) {
     s.vx = s.vx + dt * (ajx + kep * s.rx);
     s.vy = s.vy + dt * (ajy + kep * s.ry);
     if constexpr (D3) s.vz = s.vz + dt * (ajz + kep * s.rz);
+}
+
+template <int NP, int L, bool D3>
+__device__ __forceinline__ void kick_hd_any(LaneHD<NP>& s, double dt) {
+    if constexpr (NP == 2)
+        kick2_hd<L, D3>(s, dt);
+    else
+        kick_hd<NP, L, D3>(s, dt);
+}
+
+// kick2_hd's per-lane coefficients (after p, GM, m, iMi are set)
+template <int NP>
+__device__ __forceinline__ void lane_finish_hd(LaneHD<NP>& s) {
+    if constexpr (NP == 2) {
+        const bool p1 = s.p == 0;
+        const HD q = s.GM * s.iMi[1];
+        s.kA = p1 ? hd_c(0.0) : s.GM;
+        s.kB = p1 ? -s.m[1] : -q;
+        s.kC = p1 ? s.m[1] : -(q * s.m[0]);
+        s.c12 = s.m[0] * s.iMi[1];
+    }
 }
 
 // star barycentric x-velocity v0 = -sum_q (m_q / M_q) v'_q
