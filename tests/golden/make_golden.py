@@ -7,7 +7,10 @@ Reads (as text/JSON data, never executing reference code):
                                       cell 5 stdout (line 149)          -> G2 logp
                                       cell 19 stdout (lines 717-720)    -> G4 logp + params
   /root/reference/plotArchive/Ben's 2-1/log_Ben-2-1 line 4          -> G3 curve (1000 t, 1000 rv)
-and writes golden.json + g3_curve.npz.  SURVEY.md App. B documents each fixture.
+                                                     RDMGHOSTS lines -> G5: the RV curves (same
+      1000 times) of 45 states drawn from the second half of the reference's SMALA chain on
+      TEST_2-1_COMPACT.vels (mcmc_benchmark_smala.py:79-85 writes them): posterior samples
+and writes golden.json + g3_curve.npz + g5_ghosts.npz.  SURVEY.md App. B documents G1-G4.
 """
 import json
 import os
@@ -48,6 +51,11 @@ def main():
     vals = np.array([float(v) for v in lines[3].split()])
     assert vals.size == 2000
     np.savez(os.path.join(HERE, "g3_curve.npz"), t=vals[:1000], rv=vals[1000:])
+    # G5: posterior RV curves of the reference's SMALA run (the line after each RDMGHOSTS tag)
+    ghosts = [np.array([float(v) for v in lines[i + 1].split()]) for i, l in enumerate(lines)
+              if l.strip() == "RDMGHOSTS"]
+    assert len(ghosts) == 45 and all(g.size == 2000 and np.array_equal(g[:1000], vals[:1000]) for g in ghosts)
+    np.savez_compressed(os.path.join(HERE, "g5_ghosts.npz"), t=vals[:1000], rv=np.array([g[1000:] for g in ghosts]))
     golden = {
         "G1": {
             "source": "(Ex)HD155358.ipynb:82-97 (cell %d stdout)" % i_plot,
