@@ -127,3 +127,13 @@ def test_t2_kernel_algorithm_vs_ias15(which, levels, spo, hd_obs_oracle, golden)
     ok = st == 0
     assert ok.sum() >= W - 1
     assert np.max(np.abs(got[ok] - ref[ok])) < T2_LOGL_ABS
+
+
+def test_g5_ghost_fixture_consistent_with_g3():
+    """G5 (log_Ben-2-1 RDMGHOSTS) shares G3's 1000 times; 45 distinct posterior RV curves whose
+    spread (~8.5 m/s median) is far above the print precision."""
+    g3 = np.load(os.path.join(GOLDEN, "g3_curve.npz"))
+    g5 = np.load(os.path.join(GOLDEN, "g5_ghosts.npz"))
+    assert np.array_equal(g5["t"], g3["t"]) and g5["rv"].shape == (45, 1000)
+    assert len({r.tobytes() for r in g5["rv"]}) == 45
+    assert 5.0 < np.median(g5["rv"].std(0)) / 3.355e-5 < 15.0
