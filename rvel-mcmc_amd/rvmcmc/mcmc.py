@@ -93,11 +93,32 @@ class Ensemble(Mcmc):
 
 
 class Mh(Mcmc):
-    """mcmc.py:80-121 -- one chain, numpy global RNG in the reference's draw order."""
+    """mcmc.py:80-121 -- one chain, numpy global RNG in the reference's draw order.
 
-    def __init__(self, initial_state, obs):
+    speculate = K > 1 (opt-in): the single chain is launch-latency-bound (one 1-walker likelihood
+    launch per proposal), so K proposals are generated ahead -- with exactly the draws the
+    sequential chain would make if they were all rejected (normal, then a uniform only for a
+    proposal that passes priorHard) -- and evaluated in ONE launch.  step() then consumes them in
+    order with the reference's test; at the first acceptance (or at an encounter, after which the
+    reference draws no uniform) the rest is dropped and the global RNG is rewound to where the
+    sequential chain would be.  The chain, the logp values and the RNG stream are bit-identical to
+    speculate=1, provided nothing else draws from np.random between step() calls; flush() puts
+    the RNG back where the sequential chain has it (e.g. after the last step)."""
+
+    def __init__(self, initial_state, obs, speculate=1):
         super(Mh, self).__init__(initial_state, obs)
+        self._buf = []
         self.step_size = 3e-5
+        self.speculate = int(speculate)
+
+    @property
+    def step_size(self):
+        return self._step_size
+
+    @step_size.setter
+    def step_size(self, v):
+        self._step_size = v
+        self._buf = []  # proposals drawn ahead used the old step size
 
     def generate_proposal(self):
         prop = self.state.deepcopy()
@@ -107,8 +128,11 @@ class Mh(Mcmc):
 
     def set_scales(self, scales):
         self.scales = _scales_vector(self.state, scales)
+        self._buf = []
 
     def step(self):
+        if self.speculate > 1:
+            return self._step_speculative()
         while True:
             try:
                 logp = self.state.get_logp(self.obs)
@@ -122,6 +146,59 @@ class Mh(Mcmc):
                 return False
             except Encounter:
                 return False
+
+    def flush(self):
+        """Drop the proposals drawn ahead and put the global RNG where the sequential chain would
+        have it (call before drawing from np.random yourself between steps)."""
+        if self._buf:
+            np.random.set_state(self._rng_consumed)
+            self._buf = []
+
+    def _fill(self):
+        import torch
+
+        self._base_logp = self.state.get_logp(self.obs)
+        entries, live = [], []
+        for _ in range(self.speculate):
+            prop = self.generate_proposal()
+            after_normal = np.random.get_state()
+            if prop.priorHard():
+                entries.append([prop, True, after_normal, None, None, 0])
+                continue
+            u = np.random.uniform()
+            entries.append([prop, False, after_normal, u, np.random.get_state(), 0])
+            live.append(entries[-1])
+        # one launch per plan: a proposal's own scalar get_logp would use the plan of its own
+        # (gridded) base step, so proposals are grouped by it to give bit-identical values
+        groups = {}
+        for e in live:
+            groups.setdefault(e[0].integrator.plan_args(e[0].planets), []).append(e)
+        for grp in groups.values():
+            X = torch.as_tensor(np.array([e[0].get_params() for e in grp]).T.copy(), device=engine.default_device())
+            lp, st, _ = grp[0][0].get_logp_batch(self.obs, X)
+            lp, st = lp.cpu().numpy(), st.cpu().numpy()
+            for e, l, s_ in zip(grp, lp, st):
+                e[0].logp = float(l)
+                e[5] = int(s_)
+        self._buf = entries
+
+    def _step_speculative(self):
+        if not self._buf:
+            self._fill()
+        prop, prior_bad, after_normal, u, after_u, status = self._buf.pop(0)
+        self._rng_consumed = after_normal if prior_bad else after_u
+        if prior_bad:
+            return False
+        if status == _lib.RVM_STATUS_ENCOUNTER:  # Encounter raised before the uniform is drawn
+            np.random.set_state(after_normal)
+            self._buf = []
+            return False
+        if np.exp(prop.logp - self._base_logp) > u:
+            self.state = prop
+            np.random.set_state(after_u)
+            self._buf = []
+            return True
+        return False
 
 
 class MhChains:

@@ -122,11 +122,11 @@ def config5(W=8192):
     return {"config": "5: affine, 3-planet synthetic, 8192 walkers per GPU (65536 / 8)", **_affine(s, obs, W)}
 
 
-def config1(steps=200):
+def config1(steps=200, speculate=1):
     np.random.seed(2017)
     s = State(planets=[dict(p) for p in S2])
     obs = FakeObservation(s, Npoints=200, error=1.5e-4, errorVar=2.5e-5, tmax=120.)   # mcmc_benchmark_mh.py:34
-    mh = mcmc.Mh(s, obs)
+    mh = mcmc.Mh(s, obs, speculate=speculate)
     mh.set_scales({"m": 1.e-3, "a": 0.3, "h": 0.5, "k": 0.5, "l": np.pi / 2.})       # :52
     mh.step_size = 10.0e-3                                                            # :53
     tries = 0
@@ -134,14 +134,19 @@ def config1(steps=200):
     for _ in range(steps):
         tries += mh.step_force()
     dt = time.perf_counter() - t0
-    return {"config": "1: reference-API Mh, single chain (mcmc_benchmark_mh.py)", "accepted_steps_per_s": steps / dt,
-            "logl_evals_per_s": tries / dt, "acceptance": steps / tries}
+    return {"config": "1: reference-API Mh, single chain (mcmc_benchmark_mh.py)" +
+            (f", speculative x{speculate} (bit-identical chain)" if speculate > 1 else ""),
+            "accepted_steps_per_s": steps / dt, "logl_evals_per_s": tries / dt, "acceptance": steps / tries}
+
+
+def config1s():
+    return config1(speculate=int(os.environ.get("RVM_SPECULATE", "3")))
 
 
 def main():
-    which = sys.argv[1:] or ["2", "2w", "3", "4", "4x", "5", "1"]
+    which = sys.argv[1:] or ["2", "2w", "3", "4", "4x", "5", "1", "1s"]
     for c in which:
-        out = {"1": config1, "2": config2, "2w": config2w, "3": config3, "4": config4, "4x": config4x, "5": config5}[c]()
+        out = {"1": config1, "2": config2, "2w": config2w, "3": config3, "4": config4, "4x": config4x, "5": config5, "1s": config1s}[c]()
         print(json.dumps(out), flush=True)
 
 

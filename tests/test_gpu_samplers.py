@@ -186,6 +186,29 @@ def test_fused_half_step_matches_three_launch_path(case):
         assert not np.isfinite(runs[0][1]).all() or acc < 0.5  # prior / encounter proposals exercised
 
 
+def test_speculative_mh_is_bit_identical_to_sequential():
+    """Mh(speculate=8): proposals drawn ahead and evaluated in one launch, consumed with the
+    reference's test -- same chain, same logp values and the same global RNG stream as the
+    sequential reference Mh (mcmc.py:107-121), including prior rejections (no uniform drawn)."""
+    from rvmcmc import mcmc
+
+    s, obs = _state_and_obs()
+    runs = []
+    for spec in (1, 8):
+        np.random.seed(11)
+        mh = mcmc.Mh(s, obs, speculate=spec)
+        mh.set_scales({"m": 1.e-3, "a": 0.3, "h": 0.5, "k": 0.5, "l": np.pi / 2.})
+        mh.step_size = 4e-2  # large enough for prior rejections (h, k scales 0.5)
+        out = []
+        for _ in range(60):
+            out.append((mh.step(), mh.state.logp, tuple(mh.state.get_params())))
+        mh.flush()  # proposals drawn ahead are dropped, the RNG rewound to the sequential chain's
+        runs.append((out, np.random.uniform()))
+    assert runs[0] == runs[1]
+    moves = sum(o[0] for o in runs[0][0])
+    assert 0 < moves < 60
+
+
 def test_reference_api_ensemble_and_mh_step():
     from rvmcmc import mcmc
 
