@@ -267,6 +267,45 @@ class EnsembleSampler:
             out.append(buf)
         return torch.cat(out, 0).cpu().numpy()
 
+    def _gather_int(self, local):
+        """[2*nloc] per-rank counters (half 0 slice | half 1 slice) -> [W] in global order."""
+        torch = _torch()
+        n = self.nloc
+        if self.world == 1:
+            return local.cpu().numpy()
+        out = []
+        for h in (0, 1):
+            buf = torch.empty(self.world * n, dtype=local.dtype, device=self.device)
+            torch.distributed.all_gather_into_tensor(buf, local[h * n:(h + 1) * n].contiguous(), group=self.group)
+            out.append(buf)
+        return torch.cat(out).cpu().numpy()
+
+    def checkpoint(self, path):
+        """Save the whole ensemble (every rank takes part; rank 0 writes path, an .npz): positions
+        [W][dim] and lnprob [W] in global order, accept counters, iteration, seed and stretch scale.
+        With counter-based draws keyed by (seed, iteration, half, global walker) a restored sampler
+        continues bit-identically, on any number of ranks (checkpoint / resume)."""
+        pos, lnp, acc = self.gather_positions(), self.gather_lnprob(), self._gather_int(self.naccepted)
+        if self.rank == 0:
+            np.savez(path, positions=pos, lnprob=lnp, naccepted=acc, iteration=self.iteration, seed=self.seed,
+                     a=self.a, nwalkers=self.k, dim=self.dim)
+
+    def restore(self, path):
+        """Load a checkpoint written by checkpoint() (same nwalkers and dim; any world size)."""
+        torch = _torch()
+        d = np.load(path)
+        if int(d["nwalkers"]) != self.k or int(d["dim"]) != self.dim:
+            raise ValueError("checkpoint was written for a different ensemble size or dimension")
+        self.set_positions(d["positions"])
+        s0, s1 = self.local_slices()
+        lnp = torch.as_tensor(d["lnprob"], device=self.device)
+        self.lnp = [lnp[s0].contiguous(), lnp[s1].contiguous()]
+        acc = torch.as_tensor(d["naccepted"].astype(np.int32), device=self.device)
+        self.naccepted = torch.cat([acc[s0], acc[s1]]).contiguous()
+        self.iteration = int(d["iteration"])
+        self.seed = int(d["seed"])
+        self.a = float(d["a"])
+
     def check_initial(self, lnp):
         torch = _torch()
         if bool(torch.isnan(lnp).any()):

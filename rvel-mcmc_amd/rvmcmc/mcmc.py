@@ -232,6 +232,24 @@ class MhChains:
         self.Q = torch.empty_like(self.X)
         self.accepted = torch.zeros(self.n, dtype=torch.int32, device=self.device)
 
+    def checkpoint(self, path):
+        """Chains, their logp, accept counters, iteration and seed to an .npz; a restored sampler
+        continues bit-identically (Philox draws keyed by seed, iteration and chain)."""
+        np.savez(path, X=self.X.cpu().numpy(), lnp=self.lnp.cpu().numpy(), accepted=self.accepted.cpu().numpy(),
+                 iteration=self.iteration, seed=self.seed, step_size=self.step_size)
+
+    def restore(self, path):
+        import torch
+
+        d = np.load(path)
+        if d["X"].shape != tuple(self.X.shape):
+            raise ValueError("checkpoint was written for a different number of chains or parameters")
+        self.X = torch.as_tensor(d["X"], device=self.device).contiguous()
+        self.lnp = torch.as_tensor(d["lnp"], device=self.device).contiguous()
+        self.accepted = torch.as_tensor(d["accepted"], device=self.device).contiguous()
+        self.iteration, self.seed, self.step_size = int(d["iteration"]), int(d["seed"]), float(d["step_size"])
+        self.Q = torch.empty_like(self.X)
+
     def step(self, draws_propose=None, draws_accept=None):
         st = _lib.stream_handle()
         _lib.check(self.lib.rvm_mh_propose(self.dim, self.n, 0, self.X.data_ptr(), self.scales.data_ptr(),

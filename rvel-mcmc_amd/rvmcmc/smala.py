@@ -180,6 +180,25 @@ class SmalaChains:
                                              self.inv_sigma2.data_ptr(), float(self.obs.Npoints), self.alpha,
                                              self.eps, C.byref(cache["_c"]), st_h), "rvm_smala_derive")
 
+    def checkpoint(self, path):
+        """Chains, counters, iteration and seed to an .npz.  The per-chain derivative caches are not
+        stored: restore() re-derives them from the chains (the same launches, so the same values)."""
+        np.savez(path, X=self.X.cpu().numpy(), accepted=self.accepted.cpu().numpy(),
+                 failures=self.failures.cpu().numpy(), iteration=self.iteration, seed=self.seed, eps=self.eps,
+                 alpha=self.alpha, hessian=self.hessian)
+
+    def restore(self, path):
+        torch = _torch()
+        d = np.load(path)
+        if d["X"].shape != tuple(self.X.shape) or str(d["hessian"]) != self.hessian:
+            raise ValueError("checkpoint was written for a different sampler configuration")
+        self.X = torch.as_tensor(d["X"], device=self.device).contiguous()
+        self.accepted = torch.as_tensor(d["accepted"], device=self.device).contiguous()
+        self.failures = torch.as_tensor(d["failures"], device=self.device).contiguous()
+        self.iteration, self.seed = int(d["iteration"]), int(d["seed"])
+        self.eps, self.alpha = float(d["eps"]), float(d["alpha"])
+        self._derive_into(self.X, self.cache)
+
     @property
     def linalg_failures(self):
         return int(self.failures.sum().item())

@@ -90,7 +90,7 @@ def _initial_positions(state):
     return state.get_params()[None] + 1e-3 * scales * rng.standard_normal((W, state.Nvars))
 
 
-def _run_sampler(fused=False):
+def _run_sampler(fused=False, ckpt=None):
     from rvmcmc.ensemble import EnsembleSampler
     from rvmcmc.state import State
 
@@ -99,17 +99,28 @@ def _run_sampler(fused=False):
     assert ens.fused == fused
     ens.set_positions(_initial_positions(state))
     ens.compute_lnprob()
-    for _ in range(ITERS):
-        ens.step()
+    if ckpt is None:
+        for _ in range(ITERS):
+            ens.step()
+    else:  # half the iterations, checkpoint, continue in a fresh sampler from the file
+        for _ in range(ITERS // 2):
+            ens.step()
+        ens.checkpoint(ckpt)
+        if dist.is_initialized():
+            dist.barrier()
+        ens = EnsembleSampler(W, state, obs=None, seed=0, device="cpu", ops=FusedNumpyOps if fused else NumpyOps)
+        ens.restore(ckpt)
+        for _ in range(ITERS - ITERS // 2):
+            ens.step()
     return ens.gather_positions(), ens.gather_lnprob(), ens.naccepted.clone()
 
 
-def _worker(rank, world, port, out_dir, fused=False):
+def _worker(rank, world, port, out_dir, fused=False, ckpt=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pos, lnp, acc = _run_sampler(fused)
+        pos, lnp, acc = _run_sampler(fused, os.path.join(out_dir, "ckpt.npz") if ckpt else None)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), pos=pos, lnp=lnp, acc=acc.numpy())
     finally:
         dist.destroy_process_group()
@@ -144,6 +155,22 @@ def test_sharded_ensemble_bit_identical_to_single_process(tmp_path, world, fused
     got = np.concatenate([np.concatenate([a[:n] for a in accs]), np.concatenate([a[n:] for a in accs])])
     np.testing.assert_array_equal(got, acc1.numpy())
     assert 0 < acc1.sum() < W * ITERS
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_checkpoint_resume_is_bit_identical(tmp_path, world):
+    """Checkpoint after half the iterations, restore into a new sampler, continue: the same
+    ensemble as the uninterrupted run (SURVEY.md §5 checkpoint / resume; counter-based draws)."""
+    pos1, lnp1, acc1 = _run_sampler()
+    if world == 1:
+        pos, lnp, acc = _run_sampler(ckpt=str(tmp_path / "ckpt.npz"))
+        np.testing.assert_array_equal(acc.numpy(), acc1.numpy())
+    else:
+        mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), False, True), nprocs=world, join=True)
+        d = np.load(tmp_path / "rank0.npz")
+        pos, lnp = d["pos"], d["lnp"]
+    np.testing.assert_array_equal(pos, pos1)
+    np.testing.assert_array_equal(lnp, lnp1)
 
 
 def test_sampler_rejects_bad_sizes():

@@ -209,6 +209,36 @@ def test_speculative_mh_is_bit_identical_to_sequential():
     assert 0 < moves < 60
 
 
+@pytest.mark.parametrize("kind", ["mh", "smala", "smala_exact"])
+def test_chain_samplers_checkpoint_resume_bit_identical(kind, tmp_path):
+    """MhChains / SmalaChains: checkpoint after 2 steps, restore into a fresh sampler, 2 more
+    steps == 4 uninterrupted steps (SURVEY.md §5 checkpoint / resume)."""
+    from rvmcmc.mcmc import MhChains
+    from rvmcmc.smala import SmalaChains
+
+    s, obs = _state_and_obs()
+
+    def make():
+        if kind == "mh":
+            return MhChains(s, obs, S2_SCALES, 1e-3, 32, seed=3)
+        return SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=16, seed=3,
+                           hessian="exact" if kind == "smala_exact" else "gauss-newton")
+
+    a = make()
+    for _ in range(4):
+        a.step()
+    b = make()
+    for _ in range(2):
+        b.step()
+    b.checkpoint(tmp_path / "c.npz")
+    c = make()
+    c.restore(tmp_path / "c.npz")
+    for _ in range(2):
+        c.step()
+    np.testing.assert_array_equal(c.X.cpu().numpy(), a.X.cpu().numpy())
+    np.testing.assert_array_equal(c.accepted.cpu().numpy(), a.accepted.cpu().numpy())
+
+
 def test_reference_api_ensemble_and_mh_step():
     from rvmcmc import mcmc
 
