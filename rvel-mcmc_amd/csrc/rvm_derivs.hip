@@ -167,8 +167,8 @@ __global__ __launch_bounds__(MAXT) void derivs_kernel(const DevPlan P, const Der
     }
     s.encm = 0;
     lane_finish_hd(s);
-    {
-        LaneHD<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
+    if (S.n_epochs > 0) {  // REBOUND checks exit_min_distance before the first step too (when the
+        LaneHD<NP> t0 = s; // direction has any epoch: state.py:61-73 integrates nothing otherwise)
         kick_hd_any<NP, L, D3>(t0, 0.0);
         s.encm = t0.encm;
     }

@@ -311,8 +311,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     s.ir = 1.0 / s.r;
     s.encm = 0;
     lane_finish(s);
-    {
-        Lane<NP> t0 = s;  // REBOUND checks exit_min_distance before the first step too
+    if (S.n_epochs > 0) {  // REBOUND checks exit_min_distance before the first step too -- when
+        Lane<NP> t0 = s;   // it integrates at all: get_rv of an empty epoch list never does
         kick<NP, L, D3>(t0, 0.0);
         s.encm = t0.encm;
     }

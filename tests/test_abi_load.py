@@ -49,6 +49,14 @@ def test_argument_errors_do_not_touch_the_device():
     assert lib.rvm_stretch_half_step(None, C.byref(m), 10, 1, 0, 0, 0, 0, 1, 0, 2.0, 0, 0, 0, 1.0, 0, 0, 0, 0) < 0
     rows = (C.c_int32 * 2)(0, 1)
     assert lib.rvm_logl_derivs(None, 1, 0, 2, rows, 1.0, 0, 0, 0, 0, 0, 0) < 0
+    # more epochs in one direction than the LDS-staged schedule holds: an argument error, caught
+    # before any HIP call
+    n = 1701
+    t = (C.c_double * n)(*[0.01 * (i + 1) for i in range(n)])
+    ones = (C.c_double * n)(*([1.0] * n))
+    cfg2 = _lib.RvmConfig(2, 0.5, 4, 100.0)
+    rc = lib.rvm_plan_create(C.byref(cfg2), t, ones, ones, n, 64, C.byref(h))
+    assert rc < 0 and b"too many epochs" in lib.rvm_last_error()
     # workspace: per (chain, pair i >= j) and direction, 4 f64 partial sums and an int32 status
     assert lib.rvm_logl_derivs_workspace_bytes(256, 10) == 256 * 55 * 2 * (4 * 8 + 4)
 

@@ -385,3 +385,46 @@ def test_t1_inclined_planet_counts(n_planets):
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS, has_inc=1)
     _assert_t1(got, st, ref, st_ref)
+
+
+def test_empty_observation_set_and_odd_batch_sizes():
+    """No epochs at all: chi2 = 0, logl = -0 for valid walkers; the prior still applies
+    (state.py:104) but no encounter can be raised -- get_rv of an empty epoch list integrates
+    nothing (state.py:61-73), so REBOUND never checks exit_min_distance; batch sizes that do not
+    fill a wave (1, 33)."""
+    o = O.OracleObs(tf=np.zeros(0), tb=np.zeros(0), rvf=np.zeros(0), rvb=np.zeros(0), errorf=np.zeros(0),
+                    errorb=np.zeros(0), Npoints=100)
+    plan, dt = _plan(o, S2_PLANETS)
+    for W in (1, 33):
+        P = _ball(S2_PLANETS, W, seed=W)
+        if W > 1:
+            P[1, 0, 1] = 0.01                      # prior
+            P[2, 1, :5] = P[2, 0, :5]              # planets on top of each other: would be an encounter
+            P[2, 1, 1] += 0.01                     # at t = 0, but nothing is integrated
+        got, st, _ = _run(plan, P)
+        ref, st_ref = O.logl_whx_batch(P, 2, o, dt, LEVELS)
+        assert list(st) == list(st_ref)
+        ok = st == 0
+        assert np.all(got[ok] == 0.0) and np.all(np.isneginf(got[~ok]))
+        if W > 1:
+            assert st[1] == 1 and st[2] == 0
+
+
+def test_maximum_epochs_per_direction():
+    """RVM_MAX_EPOCHS_PER_DIRECTION epochs in each direction (the LDS-staged schedule at its
+    limit) against the oracle; one more is an argument error (tests/test_abi_load.py)."""
+    from rvmcmc import _lib
+
+    n = 1700
+    rng = np.random.default_rng(5)
+    tf = np.sort(rng.uniform(0.0, 60.0, n))
+    tb = -np.sort(rng.uniform(0.0, 60.0, n))
+    o = O.OracleObs(tf=tf, tb=tb, rvf=1e-4 * np.sin(tf), rvb=1e-4 * np.cos(tb), errorf=np.full(n, 1.5e-4),
+                    errorb=np.full(n, 1.5e-4), Npoints=2 * n)
+    plan, dt = _plan(o, S2_PLANETS, max_walkers=64)
+    info = plan.info()
+    assert info["epochs_fwd"] == n and info["epochs_bwd"] == n
+    P = _ball(S2_PLANETS, 3, seed=2)
+    got, st, _ = _run(plan, P)
+    ref, st_ref = O.logl_whx_batch(P, 2, o, dt, LEVELS)
+    _assert_t1(got, st, ref, st_ref)
