@@ -12,12 +12,13 @@
 //               RV (sum_L w_L rv_L, the h^2 -> 0 limit) and accumulates chi2 in registers.
 //   lanes     = the planets of one walker sit on L = 1/2/4 adjacent lanes (one Kepler drift per
 //               lane, positions exchanged by DPP quad permutes for the kick); solver state in
-//               registers; the epoch schedule is wave-uniform (scalar loads); walker parameters
-//               are read once from SoA [n_params][n_walkers].
-// The second of a walker group's two direction blocks to finish combines them (atomic counter per
-// block column): logl = -(chi2_b + chi2_f)/Npoints.  With StretchArgs the same launch is a whole
-// emcee stretch half-step: the walkers' parameters are their proposals, formed in the prologue,
-// and the combining block runs the accept (rvm_stretch.h).
+//               registers; the epoch schedule is staged once into LDS and read wave-uniformly;
+//               walker parameters are read once from SoA [n_params][n_walkers].
+// A walker's two directions meet in one 8-byte slot per walker (agent-scope atomic exchange): the
+// lane that gets the other direction's result back finishes the walker, logl =
+// -(chi2_b + chi2_f)/Npoints.  With StretchArgs the same launch is a whole emcee stretch
+// half-step: the walkers' parameters are their proposals (formed in the prologue from the
+// walker-major complement), and the finishing lane runs the accept (rvm_stretch.h).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
