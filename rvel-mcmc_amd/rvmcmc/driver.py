@@ -1,7 +1,7 @@
 """Run orchestration and chain diagnostics (mirror of the non-plotting parts of /root/reference/driver.py).
 
 Kept: McmcBundle (driver.py:20-33), auto_correlation (:37-43), writing_to_log (:45-53),
-run_mh / run_emcee / run_smala (:57-147), pre_eps_smala (:149-169), create_obs / read_obs /
+run_mh / run_emcee / run_smala (:57-147), pre_eps_smala (:149-169), run_alsmala (:171-202), create_obs / read_obs /
 save_obs (:207-222), the non-plotting part of return_trimmed_results (:265-333, trimmed_results),
 efficacy (:412-414), calc_kstatistic (:423-425), load_data / save_data / save_aux_* (:429-448), the
 per-parameter "AC time" of plot_ACTimes / inLinePlotEmceeAcTimes (:343-410).
@@ -128,6 +128,30 @@ def run_smala(label, Niter, true_state, obs, eps, alpha, printing_every=40):  # 
     clocktimes.append(datetime.utcnow())
     print("Acceptance rate: %.2f%%" % ((tries / float(Niter)) * 100))
     return McmcBundle(smala, chain, chainlogp, clocktimes, obs, Niter, true_state), _hash(true_state, label)
+
+
+def run_alsmala(label, Niter, true_state, obs, eps, alpha, bern_a, bern_b, printing_every=40):  # driver.py:171-202
+    """Full SMALA step with probability exp(-bern_a i / Niter), else the cheap derivative-reusing
+    step (bern_b is unused, as in the reference)."""
+    alsmala = mcmc.Alsmala(true_state, obs, eps, alpha)
+    chain = np.zeros((Niter + 1, alsmala.state.Nvars))
+    chainlogp = np.zeros(Niter + 1)
+    tries = 0
+    clocktimes = [datetime.utcnow()]
+    chainlogp[0] = true_state.get_logp(obs)
+    chain[0] = true_state.get_params()
+    for i in range(Niter):
+        if np.exp(-bern_a * i / Niter) > np.random.uniform():
+            tries += bool(alsmala.step())
+        else:
+            tries += bool(alsmala.step_mala())
+        chainlogp[i + 1] = alsmala.state.get_logp(obs)
+        chain[i + 1] = alsmala.state.get_params()
+        if i % printing_every == 1:
+            clocktimes.append(datetime.utcnow())
+    clocktimes.append(datetime.utcnow())
+    print("Acceptance rate: %.2f%%" % ((tries / float(Niter)) * 100))
+    return McmcBundle(alsmala, chain, chainlogp, clocktimes, obs, Niter, true_state), _hash(true_state, label)
 
 
 def create_obs(state, npoint, err, errVar, t):  # driver.py:207-209

@@ -5,6 +5,7 @@
 * Ensemble                    mcmc.py:40-75   (emcee 2.2.1 stretch move; here the whole ensemble
                                                lives on the GPU, see ensemble.EnsembleSampler)
 * Mh                          mcmc.py:80-121  (single chain, host RNG as the reference)
+* Alsmala                     mcmc.py:191-230 (SMALA with cheap derivative-reusing MALA steps)
 * Smala                       mcmc.py:126-187 (SoftAbs SMALA on State.get_logp_d_dd: exact
                                                derivatives, rvm_logl_derivs)
 * MhChains                    batched independent MH chains on the device (new; the batched
@@ -264,6 +265,6 @@ class MhChains:
         self.iteration += 1
 
 
-from .smala import Smala, SmalaChains  # noqa: E402  (re-export with the reference's module layout)
+from .smala import Alsmala, Smala, SmalaChains  # noqa: E402  (re-export with the reference's module layout)
 
-__all__ = ["Mcmc", "lnprob", "Ensemble", "Mh", "MhChains", "Smala", "SmalaChains", "EnsembleSampler"]
+__all__ = ["Mcmc", "lnprob", "Ensemble", "Mh", "MhChains", "Smala", "Alsmala", "SmalaChains", "EnsembleSampler"]

@@ -283,3 +283,54 @@ class Smala:
             self.state = stateStar
             return True
         return False
+
+
+class Alsmala(Smala):
+    """mcmc.py:191-230: SMALA whose cheap "MALA" step reuses the current state's derivatives --
+    the proposal inherits logp_d / logp_dd, only its logp is evaluated (one likelihood launch
+    instead of a derivative launch).  driver.run_alsmala mixes the two steps with probability
+    exp(-bern_a i / Niter) of a full SMALA step.  As in the reference, a state accepted by the
+    cheap step keeps the inherited (stale) derivatives, and get_logp_d_dd returns them while its
+    logp is cached."""
+
+    def generate_proposal_mala(self):  # mcmc.py:195-206
+        self.state.get_logp(self.obs)
+        logp_d, logp_dd = self.state.logp_d, self.state.logp_dd
+        Ginv = np.linalg.inv(self.softabs(logp_dd))
+        Ginvsqrt = np.linalg.cholesky(Ginv)
+        mu = self.state.get_params() + (self.epsilon) ** 2 * np.dot(Ginv, logp_d) / 2.
+        newparams = mu + self.epsilon * np.dot(Ginvsqrt, np.random.normal(0., 1., self.state.Nvars))
+        prop = self.state.deepcopy()
+        prop.set_params(newparams)
+        prop.logp_d = logp_d
+        prop.logp_dd = logp_dd
+        return prop
+
+    def transitionProbability_mala(self, state_from, state_to):  # mcmc.py:208-212
+        from scipy import stats
+
+        state_from.get_logp(self.obs)
+        logp_d, logp_dd = state_from.logp_d, state_from.logp_dd
+        Ginv = np.linalg.inv(self.softabs(logp_dd))
+        mu = state_from.get_params() + (self.epsilon) ** 2 * np.dot(Ginv, logp_d) / 2.
+        return stats.multivariate_normal.logpdf(state_to.get_params(), mean=mu, cov=(self.epsilon) ** 2 * Ginv)
+
+    def step_mala(self):  # mcmc.py:214-230
+        from .state import Encounter
+
+        if self.state.logp_d is None:  # no derivatives yet: the reference would fail on None
+            self.state.get_logp_d_dd(self.obs)
+        try:
+            stateStar = self.generate_proposal_mala()
+            if stateStar.priorHard():
+                return False
+            q_ts_t = self.transitionProbability_mala(self.state, stateStar)
+            q_t_ts = self.transitionProbability_mala(stateStar, self.state)
+        except Encounter:
+            return False
+        except np.linalg.LinAlgError:
+            return False  # the reference quit()s (mcmc.py:226-229); we reject
+        if np.exp(stateStar.logp - self.state.logp + q_t_ts - q_ts_t) > np.random.uniform():
+            self.state = stateStar
+            return True
+        return False

@@ -351,6 +351,23 @@ def test_reference_api_smala_step_with_exact_derivatives():
     assert np.isfinite(lp) and np.isfinite(g).all() and np.allclose(H, H.T) and acc >= 1
 
 
+def test_alsmala_and_run_alsmala():
+    """mcmc.Alsmala (mcmc.py:191-230) and driver.run_alsmala (driver.py:171-202): the cheap step
+    carries the current derivatives to the proposal; both step kinds run and move the chain."""
+    from rvmcmc import driver, mcmc
+
+    s, obs = _state_and_obs()
+    np.random.seed(5)
+    al = mcmc.Alsmala(s, obs, 0.3, 1e3)
+    assert al.step_mala() in (True, False)
+    lp, g, H = al.state.get_logp_d_dd(obs)
+    prop = al.generate_proposal_mala()
+    assert prop.logp_d is g and prop.logp_dd is H  # derivatives inherited, not recomputed
+    bundle, h = driver.run_alsmala("t", 12, s, obs, 0.3, 1e3, 2.0, 0.0)
+    assert bundle.mcmc_chain.shape == (13, s.Nvars) and np.isfinite(bundle.mcmc_chainlogp).all()
+    assert len({tuple(r) for r in bundle.mcmc_chain}) > 1
+
+
 def test_smala_step_matches_numpy_with_injected_draws():
     """One device SMALA step with injected z and u == mcmc.py:167-187 restated in numpy on the
     device's cached derivatives (proposal bit-close, decisions identical away from ties)."""
