@@ -138,6 +138,22 @@ class State(object):
         return False
 
     # -- likelihood -------------------------------------------------------------------------------
+    @staticmethod
+    def lnprior(theta):  # state.py:115-119 (the reference's emcee-style flat prior on one planet's m, a, h, k, l)
+        m, a, h, k, l = theta
+        if (1e-7 < m < 0.1) and (1e-2 < a < 500.0) and ((h ** 2 + k ** 2) < 1.0) and (-2 * np.pi < l < 2 * np.pi):
+            return 0.0
+        return -np.inf
+
+    def var_pindex_vname(self, vindex):  # state.py:218-225: free-parameter index -> (planet index + 1, key)
+        vi = 0
+        for pindex, p in enumerate(self.planets_vars):
+            for v in p:
+                if vindex == vi:
+                    return pindex + 1, v
+                vi += 1
+        return None
+
     def param_map(self):
         return engine.ParamMap(self)
 

@@ -87,3 +87,17 @@ def test_trimmed_results_burn_in_and_thinning():
     b2 = driver.McmcBundle(_M(), chain, -np.arange(Niter, dtype=float), [], None, Niter, s)
     states, lp, _ = driver.trimmed_results(b2, 0.25, take_every_n=2)
     assert list(-lp) == list(range(10, 40, 2)) and len(states) == 15
+
+
+def test_state_bookkeeping_helpers():
+    """State.lnprior (state.py:115-119) and var_pindex_vname (state.py:218-225)."""
+    from rvmcmc.state import State
+
+    s = State(planets=[{"m": 1e-3, "a": 0.9, "h": 0.1, "k": 0.0, "l": 0.3},
+                       {"m": 2e-3, "a": 1.5, "h": 0.1, "k": 0.0, "l": 2.0}], ignore_vars=["h"])
+    assert [s.var_pindex_vname(i) for i in range(s.Nvars)] == [(1, "m"), (1, "a"), (1, "k"), (1, "l"),
+                                                               (2, "m"), (2, "a"), (2, "k"), (2, "l")]
+    assert s.var_pindex_vname(s.Nvars) is None
+    assert State.lnprior([1e-3, 0.9, 0.1, 0.0, 0.3]) == 0.0
+    assert State.lnprior([1e-3, 0.009, 0.1, 0.0, 0.3]) == -np.inf
+    assert State.lnprior([1e-3, 0.9, 0.8, 0.8, 0.3]) == -np.inf
