@@ -72,36 +72,6 @@ def fd_logp_grad_metric(state, obs, X, rel_step=FD_REL_STEP, pmap=None, hill_fac
     return lp[0], grad, H, status
 
 
-def softabs_inv(H, alpha):
-    """Batched SoftAbs: H [P][P][C] -> (Ginv [C][P][P], chol(Ginv) [C][P][P], logdet(Ginv) [C], ok [C])."""
-    torch = _torch()
-    A = (-H).permute(2, 0, 1).contiguous()                    # [C][P][P]
-    A = 0.5 * (A + A.transpose(1, 2))
-    lam, Q = torch.linalg.eigh(A)
-    al = alpha * lam
-    small = al.abs() < 1e-8
-    lt = torch.where(small, torch.full_like(lam, 1.0 / alpha), lam / torch.tanh(torch.where(small, torch.ones_like(al), al)))
-    inv = 1.0 / lt
-    Ginv = (Q * inv[:, None, :]) @ Q.transpose(1, 2)
-    Ginv = 0.5 * (Ginv + Ginv.transpose(1, 2))
-    L, info = torch.linalg.cholesky_ex(Ginv)
-    ok = (info == 0) & torch.isfinite(lt).all(1)
-    logdet = torch.log(inv).sum(1)
-    return Ginv, L, logdet, ok
-
-
-def _mvn_logpdf(x, mu, Ginv, logdetGinv, eps):
-    """log N(x; mu, eps^2 Ginv) for batches: x, mu [C][P]."""
-    torch = _torch()
-    P = x.shape[1]
-    d = (x - mu)[:, :, None]
-    cov = (eps * eps) * Ginv
-    sol = torch.linalg.solve(cov, d)
-    maha = (d * sol).sum((1, 2))
-    logdet = P * math.log(eps * eps) + logdetGinv
-    return -0.5 * (maha + logdet + P * math.log(2.0 * math.pi))
-
-
 class SmalaChains:
     """C independent SMALA chains on the device (config 4: 256 chains).
 

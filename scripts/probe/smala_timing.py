@@ -34,7 +34,6 @@ def main():
     sm = smala.SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=256, seed=0)
     X = sm.X
     ms_fd, (lp, g, H, st) = timed(lambda: smala.fd_logp_grad_metric(sm.state, obs, X, sm.rel_step, sm.pmap, 1.0))
-    ms_sa, _ = timed(lambda: smala.softabs_inv(H, sm.alpha))
     A = (-H).permute(2, 0, 1).contiguous()
     ms_eigh, _ = timed(lambda: torch.linalg.eigh(A))
     ms_chol, _ = timed(lambda: torch.linalg.cholesky_ex(A @ A.transpose(1, 2) + torch.eye(10, device=A.device, dtype=A.dtype)))
@@ -43,7 +42,7 @@ def main():
     stencil = torch.empty((P, (2 * P + 1) * 256), dtype=torch.float64, device=X.device)
     ms_logl, _ = timed(lambda: sm.state.get_logp_batch(obs, stencil.copy_(X.repeat(1, 2 * P + 1)), hill_factor=1.0,
                                                        want_rv=True, pmap=sm.pmap))
-    print(dict(step_ms=ms_step, fd_logp_grad_metric_ms=ms_fd, logl_launch_5376_ms=ms_logl, softabs_inv_ms=ms_sa,
+    print(dict(step_ms=ms_step, fd_logp_grad_metric_ms=ms_fd, logl_launch_5376_ms=ms_logl,
                eigh_ms=ms_eigh, cholesky_ms=ms_chol))
 
 
