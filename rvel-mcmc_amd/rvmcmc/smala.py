@@ -18,7 +18,6 @@ defined; parity is statistical.
 from __future__ import annotations
 
 import ctypes as C
-import math
 
 import numpy as np
 
