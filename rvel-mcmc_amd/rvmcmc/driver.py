@@ -288,3 +288,18 @@ def ess(chain_steps_walkers_params):
     n, w, P = c.shape
     taus = np.array([integrated_time(c[:, :, p]) for p in range(P)])
     return n * w / taus, taus
+
+
+# The notebooks' older names for the same functions ((Ex)HD155358.ipynb,
+# (Ex)Full Test + Usage Example.ipynb, generator.py); they return (bundle, hash) like run_*.
+createEns = run_emcee
+createMH = run_mh
+createSMALA = run_smala
+createALSMALA = run_alsmala
+createObs = CreateObs = create_obs
+ReadObs = read_obs
+saveData = save_data
+loadData = load_data
+saveAuxSmala = save_aux_smala
+saveAuxEmcee = save_aux_emcee
+saveAuxMH = save_aux_mh

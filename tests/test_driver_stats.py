@@ -101,3 +101,13 @@ def test_state_bookkeeping_helpers():
     assert State.lnprior([1e-3, 0.9, 0.1, 0.0, 0.3]) == 0.0
     assert State.lnprior([1e-3, 0.009, 0.1, 0.0, 0.3]) == -np.inf
     assert State.lnprior([1e-3, 0.9, 0.8, 0.8, 0.3]) == -np.inf
+
+
+def test_notebook_era_driver_aliases():
+    """The older driver names the reference notebooks call map onto the kept
+    functions."""
+    assert driver.createEns is driver.run_emcee and driver.createMH is driver.run_mh
+    assert driver.createSMALA is driver.run_smala and driver.createALSMALA is driver.run_alsmala
+    assert driver.createObs is driver.create_obs and driver.CreateObs is driver.create_obs
+    assert driver.ReadObs is driver.read_obs and driver.saveData is driver.save_data
+    assert driver.saveAuxSmala is driver.save_aux_smala and driver.saveAuxMH is driver.save_aux_mh
