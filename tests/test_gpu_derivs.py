@@ -162,10 +162,11 @@ def fd_of_gradient(plan, x, d, rows_dir=None):
     return 0.5 * (Hr + Hr.T)
 
 
-@pytest.mark.parametrize("name", ["S2", "S2_inclined", "3planet"])
+@pytest.mark.parametrize("name", ["S2", "S2_inclined", "1planet", "3planet", "4planet"])
 def test_derivs_match_fd_of_the_kernel_algorithm(name):
-    if name == "3planet":
-        planets = S2_PLANETS + [{"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}]
+    if name in ("1planet", "3planet", "4planet"):
+        extra = [{"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}, {"m": 5e-4, "a": 3.9, "h": 0.0, "k": 0.03, "l": 4.0}]
+        planets = {"1planet": S2_PLANETS[:1], "3planet": S2_PLANETS + extra[:1], "4planet": S2_PLANETS + extra}[name]
         np.random.seed(5)
         obs = O.fake_obs(planets, Npoints=30, error=1.5e-4, errorVar=2.5e-5, tmax=40.)
     else:
@@ -179,7 +180,11 @@ def test_derivs_match_fd_of_the_kernel_algorithm(name):
     for w in range(Pw.shape[0]):
         assert np.allclose(H[:, :, w], H[:, :, w].T, rtol=0, atol=0)  # written symmetric
         x = _kernel_params(Pw[w:w + 1], rows)[:, 0]
-        d = sigma_steps(H[:, :, w], x, rows)
+        # 4 planets: the outer one (m 5e-4, a 3.9, 30 points over 40 time units) is weakly
+        # constrained and logp is far from quadratic over one posterior width, so the FD step
+        # shrinks to 0.4 widths (measured: grad err 1.9e-6 -> 4.9e-8, FD(grad) hess err
+        # 1.4e-5 -> 3.4e-7 as the step goes 1 -> 0.4 widths: FD truncation, not the kernel)
+        d = (0.4 if name == "4planet" else 1.0) * sigma_steps(H[:, :, w], x, rows)
         f0, g_fd, H_fd = fd_derivs(lambda P: O.logl_whx_batch(P, len(planets), obs, dt, LEVELS, has_inc=int(inclined))[0],
                                    x, len(planets), rows, d=d)
         eg, eH2 = scaled_errors(g[:, w], H[:, :, w], g_fd, H_fd)
