@@ -269,6 +269,7 @@ struct Lane {
     double dmin2, idmin2;   // (hill_factor * max r_Hill)^2 and its reciprocal
     double kA, kB, kC;      // closed-form 2-planet kick coefficients of the own lane (kick2)
     double kAh, kBh, kCh;   // the same times the current step (lane_set_step)
+    double pair_s;          // kick2: -0.0 on planet 1's lane (pair 0-2), -1.0 on planet 2's (pair 1-2)
     double kP[KickPairs<NP>::n];   // NP >= 3 (kickN): own-lane coefficient of every pair but (0,1)
     double kPh[KickPairs<NP>::n];  // the same times the current step
     int p;                  // own planet index (lane % L, clamped to NP-1)
@@ -301,7 +302,9 @@ __device__ __forceinline__ void lane_finish(Lane<NP>& s) {
         s.kA = p1 ? 0.0 : s.GM;
         s.kB = p1 ? -s.m[1] : -q;
         s.kC = p1 ? s.m[1] : -q * s.m[0];
+        s.pair_s = p1 ? -0.0 : -1.0;
     } else {
+        s.pair_s = 0.0;
         s.kB = s.kC = 0.0;
         s.kA = 0.0;
 #pragma unroll
@@ -714,26 +717,35 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
 //   dv'_2 = dt [ M_2 r'_2/|r'_2|^3 - (M_2/M_1)(d02/r02^3 + m_1 d12/r12^3) ]
 // with heliocentric x_1 = r'_1, x_2 = r'_2 + (m_1/M_1) r'_1, d02 = x_2, d12 = x_2 - x_1.  The
 // own |r'| (= star--planet-1 distance on planet 1's lane) is carried from the drift: 2 rsq per kick.
+//
+// The two pair distances are split over the walker's two lanes: planet 1's lane takes d02 = x2,
+// planet 2's lane d12 = x2 - x1 (the same expressions, so the same bits), one inverse cube each,
+// exchanged by DPP: one v_rsq_f64 per lane and kick instead of two.  The encounter bits of both
+// lanes count (kick_enc_mask: the logl epilogue ORs a walker's lane pair).
 template <int L, bool D3 = false>
 __device__ __forceinline__ void kick2(Lane<2>& s, double c1875 = 1.875) {
+    static_assert(L == 2, "kick2 pairs the two planets' lanes");
     const double x1 = grp_get<L, 0>(s.rx), y1 = grp_get<L, 0>(s.ry);
     const double R2x = grp_get<L, 1>(s.rx), R2y = grp_get<L, 1>(s.ry);
     const double c = s.m[0] * s.iMi[1];  // m_1 / M_1
     const double x2 = fma(c, x1, R2x), y2 = fma(c, y1, R2y);
     const double dx12 = x2 - x1, dy12 = y2 - y1;
-    double r02sq = fma(x2, x2, y2 * y2);
-    double r12sq = fma(dx12, dx12, dy12 * dy12);
+    // own pair: fma(-0, x1, x2) = x2 on planet 1's lane, fma(-1, x1, x2) = x2 - x1 on planet 2's
+    const double ox = fma(s.pair_s, x1, x2), oy = fma(s.pair_s, y1, y2);
+    double rsq = fma(ox, ox, oy * oy);
     double z2 = 0.0, dz12 = 0.0;
     if constexpr (D3) {
         const double z1 = grp_get<L, 0>(s.rz), R2z = grp_get<L, 1>(s.rz);
         z2 = fma(c, z1, R2z);
         dz12 = z2 - z1;
-        r02sq = fma(z2, z2, r02sq);
-        r12sq = fma(dz12, dz12, r12sq);
+        const double oz = fma(s.pair_s, z1, z2);
+        rsq = fma(oz, oz, rsq);
     }
-    // star--planet-1 exit check from |r'_1| on planet 1's lane, the only encounter bit read
-    s.encm |= ballot(r02sq < s.dmin2) | ballot(r12sq < s.dmin2) | ballot(s.ir * s.ir > s.idmin2);
-    const double i02c = rcube_nr(r02sq, c1875), i12c = rcube_nr(r12sq, c1875);
+    // own pair on every lane; star--planet-1 from |r'_1| on planet 1's lanes only (|r'_2| is a
+    // Jacobi distance, not a pair)
+    s.encm |= ballot(rsq < s.dmin2) | (ballot(s.ir * s.ir > s.idmin2) & 0x5555555555555555ull);
+    const double ic = rcube_nr(rsq, c1875);
+    const double i02c = grp_get<L, 0>(ic), i12c = grp_get<L, 1>(ic);
     // coefficients carry the step (lane_set_step): v += A r' + B x2/r02^3 + C d12/r12^3
     const double A = s.kAh * (s.ir * (s.ir * s.ir));
     const double bx = s.kBh * i02c, cx = s.kCh * i12c;
@@ -801,6 +813,13 @@ __device__ __forceinline__ void kick(Lane<NP>& s, double dt, double c1875 = 1.87
         kickN<NP, L, D3>(s, c1875);
     else
         kick_generic<NP, L, D3>(s, dt);
+}
+
+// Encounter bits of a walker in Lane::encm relative to its first lane: kick2 splits the pair
+// tests over both lanes of the walker, kickN / kick_generic put all of them on every lane.
+template <int NP>
+__device__ __forceinline__ constexpr uint64_t kick_enc_bits() {
+    return NP == 2 ? 3ull : 1ull;
 }
 
 // star barycentric x-velocity: v0 = -sum_q (m_q / M_q) v'_q (gathered over the lane group)

@@ -390,7 +390,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #endif
     }
 #undef prm
-    if (pl_idx == 0) s_enc[lvl][slot] = (int)((s.encm >> lane) & 1) | (status == RVM_STATUS_PRIOR ? 2 : 0);
+    if (pl_idx == 0)
+        s_enc[lvl][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
     __syncthreads();
     if (lvl == 0 && lane < WPB) {
         const int wo = w0 + lane;
