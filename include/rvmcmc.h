@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 6
+#define RVM_ABI_VERSION 7
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -138,6 +138,36 @@ int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_
                           int64_t s0_begin, double* x, double* x_aos, double* lnp, int32_t n_s1, const double* c_aos,
                           double a, uint64_t seed, uint64_t iteration, uint32_t half, double hill_factor,
                           double* lnp_new_out, int32_t* status_out, int32_t* accepted, void* stream);
+
+/* One whole stretch-move ITERATION (both half-steps, mcmc.py:57-65 / emcee 2.2.1 sample()) in one
+ * likelihood launch plus one small accept launch, bit-identical to two rvm_stretch_half_step calls.
+ * The second half's proposal against partner j depends on j's first-half decision, so begin
+ * evaluates it both ways (partner rejected: c0[j]; accepted: its proposal q0(j)) next to the first
+ * half's own proposals -- 3 n_loc walker slots in one launch, which keeps a chip that one half-step
+ * fills only partly busy (n_loc walkers of each half per rank; the plan needs max_walkers >= 3 n_loc).
+ *
+ * begin: half 0's proposals against c1, its logl and accepts (x0, lnp0 in place; accepted0 +=);
+ *   half 1's proposals x1 against both variants of its partner in c0; logl of all 3 n_loc slots to
+ *   lnp_spec / status_spec [3 n_loc] (slot n_loc + v n_loc + k: half 1's walker k, variant v);
+ *   half 0's decisions to dec [n_loc] (1 accepted).  c0, c1: both halves walker-major
+ *   [n_half][n_params] as at the start of the iteration, global order (on one rank: the walker-major
+ *   mirrors); they must not be written before end has run.  s0_begin / s1_begin: global index of
+ *   this rank's first walker of half 0 (its index within the half) and of half 1 (n_half + its
+ *   index within half 1): the Philox keys.
+ * end: half 1's accepts with the variant dec_all[j] selects (dec_all: half 0's decisions in
+ *   global order, [n_half]; on one rank dec itself); x1, lnp1 in place, x1_aos / x0_aos (nullable)
+ *   mirrors updated; lnp_new_out / status_new_out (nullable): the chosen proposals' logl, status. */
+int rvm_stretch_iteration_begin(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_loc,
+                                int64_t s0_begin, int64_t s1_begin, double* x0, double* lnp0, const double* x1,
+                                int32_t n_half, const double* c0, const double* c1, double a, uint64_t seed,
+                                uint64_t iteration, double hill_factor, double* lnp_spec, int32_t* status_spec,
+                                int32_t* dec, int32_t* accepted0, void* stream);
+int rvm_stretch_iteration_end(int32_t n_params, int32_t n_loc, int64_t s0_begin, int64_t s1_begin, const double* x0,
+                              double* x0_aos, const int32_t* dec, const int32_t* dec_all, double* x1, double* x1_aos,
+                              double* lnp1, int32_t n_half, const double* c0, const double* c1,
+                              const double* lnp_spec, const int32_t* status_spec, double a, uint64_t seed,
+                              uint64_t iteration, int32_t* accepted1, double* lnp_new_out, int32_t* status_new_out,
+                              void* stream);
 
 /* Gaussian random-walk Metropolis-Hastings (mcmc.py:89-121), n_chains independent chains:
  * propose: q = x + step_size * scales[p] * N(0,1)        draws layout: [n_params][n_chains]

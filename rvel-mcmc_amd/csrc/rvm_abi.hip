@@ -27,6 +27,7 @@ hipError_t launch_mh_propose(int P, int n, int64_t b, const double* x, const dou
                              uint64_t seed, uint64_t it, const double* draws, double* q, hipStream_t st);
 hipError_t launch_mh_accept(int P, int n, int64_t b, double* x, double* lnp, const double* q, const double* lnp_new,
                             uint64_t seed, uint64_t it, const double* draws, int32_t* acc, hipStream_t st);
+hipError_t launch_stretch_iteration_end(const IterEndArgs& g, hipStream_t st);
 hipError_t launch_fd_params(int P, int n, const double* x, double rel, const double* fl, double* out, hipStream_t st);
 hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,
                                const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
@@ -276,6 +277,7 @@ int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_
     sa.n1 = n_s1;
     sa.dim = n_params;
     sa.half = half;
+    sa.xstride = n_s0;
     for (int r = 0; r < RVM_MAX_PARAM_ROWS; r++) {
         const int k = r < rows ? map->src[r] : -1;
         if (k >= n_params) return fail(-1, "rvm_stretch_half_step: map source index out of range");
@@ -285,6 +287,93 @@ int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_
     hipError_t e = rvm::launch_logl(plan->dev, n_s0, nullptr, hill_factor, plan->slots, lnp_new_out, status_out,
                                     nullptr, sa, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_half_step");
+}
+
+int rvm_stretch_iteration_begin(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_loc,
+                                int64_t s0_begin, int64_t s1_begin, double* x0, double* lnp0, const double* x1,
+                                int32_t n_half, const double* c0, const double* c1, double a, uint64_t seed,
+                                uint64_t iteration, double hill_factor, double* lnp_spec, int32_t* status_spec,
+                                int32_t* dec, int32_t* accepted0, void* stream) {
+    if (!plan || !map) return fail(-1, "rvm_stretch_iteration_begin: null plan or map");
+    if (n_loc == 0) return 0;
+    if (n_loc < 0 || (int64_t)3 * n_loc > plan->max_walkers)
+        return fail(-1, "rvm_stretch_iteration_begin: 3 n_loc exceeds the plan's max_walkers");
+    if (n_params < 1 || n_half < n_loc || !x0 || !lnp0 || !x1 || !c0 || !c1 || !lnp_spec || !status_spec || !dec)
+        return fail(-1, "rvm_stretch_iteration_begin: bad arguments");
+    if (s0_begin < 0 || s0_begin + n_loc > n_half || s1_begin < n_half || s1_begin + n_loc > 2 * (int64_t)n_half)
+        return fail(-1, "rvm_stretch_iteration_begin: walker ranges outside the halves");
+    if (!(a > 1.0)) return fail(-1, "rvm_stretch_iteration_begin: stretch scale a must be > 1");
+    if (!(hill_factor >= 0.0)) return fail(-1, "rvm_stretch_iteration_begin: hill_factor must be >= 0");
+    const int rows = (plan->dev.inclined ? 7 : 5) * plan->dev.n_planets;
+    if (map->n_rows != rows) return fail(-1, "rvm_stretch_iteration_begin: map rows do not match the plan");
+    rvm::StretchArgs sa{};
+    sa.c = c1;
+    sa.x = x0;
+    sa.x_aos = nullptr;  // c0 must stay as it was until rvm_stretch_iteration_end
+    sa.lnp = lnp0;
+    sa.accepted = accepted0;
+    sa.s0_begin = s0_begin;
+    sa.seed = seed;
+    sa.iteration = iteration;
+    sa.a = a;
+    sa.n1 = n_half;
+    sa.dim = n_params;
+    sa.half = 0;
+    sa.xstride = n_loc;
+    sa.n_spec = n_loc;
+    sa.c0 = c0;
+    sa.x1 = x1;
+    sa.s1_begin = s1_begin;
+    sa.dec = dec;
+    for (int r = 0; r < RVM_MAX_PARAM_ROWS; r++) {
+        const int k = r < rows ? map->src[r] : -1;
+        if (k >= n_params) return fail(-1, "rvm_stretch_iteration_begin: map source index out of range");
+        sa.src[r] = k < 0 ? -1 : k;
+        sa.base[r] = r < rows ? map->base[r] : 0.0;
+    }
+    hipError_t e = rvm::launch_logl(plan->dev, 3 * n_loc, nullptr, hill_factor, plan->slots, lnp_spec, status_spec,
+                                    nullptr, sa, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_iteration_begin");
+}
+
+int rvm_stretch_iteration_end(int32_t n_params, int32_t n_loc, int64_t s0_begin, int64_t s1_begin, const double* x0,
+                              double* x0_aos, const int32_t* dec, const int32_t* dec_all, double* x1, double* x1_aos,
+                              double* lnp1, int32_t n_half, const double* c0, const double* c1,
+                              const double* lnp_spec, const int32_t* status_spec, double a, uint64_t seed,
+                              uint64_t iteration, int32_t* accepted1, double* lnp_new_out, int32_t* status_new_out,
+                              void* stream) {
+    if (n_loc == 0) return 0;
+    if (n_params < 1 || n_loc < 0 || n_half < n_loc || !x0 || !dec || !dec_all || !x1 || !lnp1 || !c0 || !c1 ||
+        !lnp_spec || !status_spec)
+        return fail(-1, "rvm_stretch_iteration_end: bad arguments");
+    if (s0_begin < 0 || s0_begin + n_loc > n_half || s1_begin < n_half || s1_begin + n_loc > 2 * (int64_t)n_half)
+        return fail(-1, "rvm_stretch_iteration_end: walker ranges outside the halves");
+    if (!(a > 1.0)) return fail(-1, "rvm_stretch_iteration_end: stretch scale a must be > 1");
+    rvm::IterEndArgs g{};
+    g.dim = n_params;
+    g.n = n_loc;
+    g.n_half = n_half;
+    g.s0_begin = s0_begin;
+    g.s1_begin = s1_begin;
+    g.x0 = x0;
+    g.x0_aos = x0_aos;
+    g.dec_local = dec;
+    g.dec_all = dec_all;
+    g.x1 = x1;
+    g.x1_aos = x1_aos;
+    g.lnp1 = lnp1;
+    g.c0 = c0;
+    g.c1 = c1;
+    g.lnp_spec = lnp_spec;
+    g.st_spec = status_spec;
+    g.a = a;
+    g.seed = seed;
+    g.iteration = iteration;
+    g.accepted1 = accepted1;
+    g.lnp_new_out = lnp_new_out;
+    g.status_new_out = status_new_out;
+    hipError_t e = rvm::launch_stretch_iteration_end(g, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_iteration_end");
 }
 
 int rvm_stretch_propose(int32_t n_params, int32_t n_s0, int64_t s0_begin, const double* x, int32_t n_s1,

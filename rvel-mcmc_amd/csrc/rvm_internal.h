@@ -34,9 +34,17 @@ struct DevPlan {
 
 // Fused stretch half-step (rvm_stretch_half_step) by value as a kernel argument; c == nullptr
 // for a plain likelihood launch.
+//
+// Speculative whole iteration (rvm_stretch_iteration_begin, n_spec > 0): the launch has 3 n_spec
+// walker slots.  Slots [0, n) are half 0's walkers (proposal against c = half 1, accept at the
+// end as a plain half-step, decision to dec[]); slots [n, 2n) and [2n, 3n) are half 1's walkers
+// proposed against their partner j in half 0 as it will be after this iteration's first
+// half-step, both ways: c = c0[j] (the partner rejects) and c = q0(j) (it accepts; q0 recomputed
+// from c0, c and the partner's own draws).  Their logl go to logl_out[n + v n + k]; the second
+// half-step's accepts run afterwards (rvm_stretch_iteration_end) once dec[] is known.
 struct StretchArgs {
     const double* c;    // complement half, walker-major [n1][dim] (one contiguous row per c_j)
-    double* x;          // this half's free parameters [dim][W] (accepted proposals written back)
+    double* x;          // this half's free parameters [dim][xstride] (accepted proposals written back)
     double* x_aos;      // walker-major mirror of x [W][dim] kept in step on accept (nullable)
     double* lnp;        // their log-probabilities [W]
     int32_t* accepted;  // accept counters [W] (nullable)
@@ -45,8 +53,37 @@ struct StretchArgs {
     double a;
     int32_t n1, dim;
     uint32_t half;
+    int32_t xstride;    // row stride of x (W for a half-step, n_spec for a speculative iteration)
+    // speculative iteration only (n_spec = 0 otherwise)
+    int32_t n_spec;     // walkers per half on this rank
+    const double* c0;   // half 0 walker-major [n1][dim] as at the start of the iteration
+    const double* x1;   // half 1's free parameters [dim][n_spec]
+    int64_t s1_begin;   // global index of half 1's walker 0 (Philox key)
+    int32_t* dec;       // [n_spec] half 0's accept decisions (1 accepted)
     int32_t src[RVM_MAX_PARAM_ROWS];  // rvm_param_map
     double base[RVM_MAX_PARAM_ROWS];
+};
+
+// Second half of a speculative stretch iteration (rvm_stretch_iteration_end) by value.
+struct IterEndArgs {
+    int32_t dim, n, n_half;     // free parameters, walkers per half on this rank, walkers per half
+    int64_t s0_begin, s1_begin;  // global index of this rank's first walker of half 0 / half 1
+    const double* x0;           // half 0 [dim][n] after the first half-step
+    double* x0_aos;             // its walker-major mirror [n][dim], refreshed here (nullable)
+    const int32_t* dec_local;   // [n] half 0's decisions on this rank
+    const int32_t* dec_all;     // [n_half] half 0's decisions, global order
+    double* x1;                 // half 1 [dim][n], updated in place
+    double* x1_aos;             // its walker-major mirror [n][dim] (nullable)
+    double* lnp1;               // [n]
+    const double* c0;           // half 0 walker-major [n_half][dim] at the start of the iteration
+    const double* c1;           // half 1 walker-major [n_half][dim] at the start of the iteration
+    const double* lnp_spec;     // [3 n] logl of the begin launch (half 1's two variants at n and 2n)
+    const int32_t* st_spec;     // [3 n] their statuses
+    double a;
+    uint64_t seed, iteration;
+    int32_t* accepted1;         // [n] (nullable)
+    double* lnp_new_out;        // [n] logl of half 1's chosen proposals (nullable)
+    int32_t* status_new_out;    // [n] (nullable)
 };
 
 // rvm_smala_cache by value as a kernel argument (same layout)

@@ -99,12 +99,18 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, double h, int ns, int& redo
 
 // kernel parameter row r of walker w: from the SoA input, or (fused stretch half-step) the row's
 // fixed value or the walker's proposal of the free parameter feeding it
+// (kind 1 / 2: half 1's walker of a speculative iteration against its partner's rejected /
+// accepted position, StretchArgs)
 __device__ __forceinline__ double walker_param(bool stretch, const double* __restrict__ params, int W, int w,
-                                               const StretchArgs& sa, int r, double z, int j) {
+                                               const StretchArgs& sa, int r, double z, int j, int kind, double zp,
+                                               int jp) {
     if (!stretch) return params[(size_t)r * W + w];
     const int k = sa.src[r];
     if (k < 0) return sa.base[r];
-    return stretch_q(sa.c[(size_t)j * sa.dim + k], z, sa.x[(size_t)k * W + w]);
+    if (kind == 0) return stretch_q(sa.c[(size_t)j * sa.dim + k], z, sa.x[(size_t)k * sa.xstride + w]);
+    double c = sa.c0[(size_t)j * sa.dim + k];
+    if (kind == 2) c = stretch_q(sa.c[(size_t)jp * sa.dim + k], zp, c);  // q0(j): bit-identical to slot j's
+    return stretch_q(c, z, sa.x1[(size_t)k * sa.n_spec + w]);
 }
 
 __device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, int gi, int r, double v) {
@@ -196,9 +202,22 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const bool stretch = sa.c != nullptr;
     double zst = 0.0;
     int jst = 0;
-    const bool stager = stretch && lvl == 0 && pl_idx == 0;  // one lane per walker stages for the end
+    // slot kind (speculative iteration, StretchArgs): 0 = a half-step walker / half 0, 1 and 2 =
+    // half 1's walker wk against its partner's rejected / accepted position
+    const int nsp = sa.n_spec;
+    const int kind = (stretch && nsp > 0) ? (wl < nsp ? 0 : (wl < 2 * nsp ? 1 : 2)) : 0;
+    const int wk = wl - kind * nsp;
+    double zp = 0.0;
+    int jp = 0;
+    const bool stager = stretch && lvl == 0 && pl_idx == 0 && kind == 0;  // one lane per walker stages
     if (stretch) {
-        stretch_draw(sa.seed, (uint64_t)(sa.s0_begin + wl), sa.iteration, sa.half, sa.a, sa.n1, zst, jst);
+        if (kind == 0) {
+            stretch_draw(sa.seed, (uint64_t)(sa.s0_begin + wk), sa.iteration, sa.half, sa.a, sa.n1, zst, jst);
+        } else {
+            stretch_draw(sa.seed, (uint64_t)(sa.s1_begin + wk), sa.iteration, 1u, sa.a, sa.n1, zst, jst);
+            // the partner's own draws (half 0's keys are its global indices 0 .. n1-1)
+            if (kind == 2) stretch_draw(sa.seed, (uint64_t)jst, sa.iteration, 0u, sa.a, sa.n1, zp, jp);
+        }
         if (stager) {
             constexpr int R = PR * NP;
             l_q[R * GW + gi] = zst;
@@ -206,7 +225,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             l_q[(R + 2) * GW + gi] = sa.lnp[wl];
         }
     }
-#define prm(r) stage_row(stager, l_q, GW, gi, (r), walker_param(stretch, params, W, wl, sa, (r), zst, jst))
+#define prm(r) stage_row(stager, l_q, GW, gi, (r), walker_param(stretch, params, W, wk, sa, (r), zst, jst, kind, zp, jp))
     Lane<NP> s;
     double pa[NP], ph[NP], pk[NP], pl[NP], pix[NP], piy[NP];
     int status = RVM_STATUS_OK;
@@ -418,22 +437,26 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 const double lp = stw == RVM_STATUS_OK ? lp0 : -INFINITY;
                 if (logl_out) logl_out[wo] = lp;
                 if (status_out) status_out[wo] = stw;
-                if (stretch) {  // emcee accept with the proposal staged in the prologue
+                if (stretch && (sa.n_spec == 0 || wo < sa.n_spec)) {
+                    // emcee accept with the proposal staged in the prologue (half 1's slots of a
+                    // speculative iteration only deliver their logl: rvm_stretch_iteration_end)
                     constexpr int R = PR * NP;
                     const int gl = grp * WPB + lane;
                     const double z = l_q[R * GW + gl], u3 = l_q[(R + 1) * GW + gl];
-                    if (stretch_accepts(sa.dim, z, lp, l_q[(R + 2) * GW + gl], u3)) {
+                    const bool acc = stretch_accepts(sa.dim, z, lp, l_q[(R + 2) * GW + gl], u3);
+                    if (acc) {
 #pragma unroll
                         for (int r = 0; r < R; r++) {
                             if (sa.src[r] >= 0) {
                                 const double v = l_q[r * GW + gl];
-                                sa.x[(size_t)sa.src[r] * W + wo] = v;
+                                sa.x[(size_t)sa.src[r] * sa.xstride + wo] = v;
                                 if (sa.x_aos) sa.x_aos[(size_t)wo * sa.dim + sa.src[r]] = v;
                             }
                         }
                         sa.lnp[wo] = lp;
                         if (sa.accepted) sa.accepted[wo] += 1;
                     }
+                    if (sa.dec) sa.dec[wo] = acc ? 1 : 0;
                 }
             }
         }

@@ -51,6 +51,52 @@ __global__ void stretch_accept_kernel(int P, int n0, int64_t s0_begin, double* _
     }
 }
 
+// Second half-step of a speculative iteration (rvm_stretch_iteration_end): threads [0, n) accept
+// or reject half 1's walkers with the logl of the variant their partner's decision selects;
+// threads [n, 2n) refresh half 0's walker-major mirror rows that the first half-step changed.
+// A partner on this rank is read from x0 (already updated); any other is rebuilt from the
+// iteration's starting positions and its own draws -- the same bits either way.
+__global__ void stretch_iteration_end_kernel(const IterEndArgs g) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = g.n, P = g.dim;
+    if (t < n) {
+        const int k = t;
+        double z;
+        int j;
+        stretch_draw(g.seed, (uint64_t)(g.s1_begin + k), g.iteration, 1u, g.a, g.n_half, z, j);
+        const int v = g.dec_all[j] != 0 ? 1 : 0;
+        const int64_t jl = (int64_t)j - g.s0_begin;
+        const bool local = jl >= 0 && jl < n;
+        const double lnew = g.lnp_spec[(size_t)(1 + v) * n + k];
+        if (g.lnp_new_out) g.lnp_new_out[k] = lnew;
+        if (g.status_new_out) g.status_new_out[k] = g.st_spec[(size_t)(1 + v) * n + k];
+        const double u3 = stretch_u3(g.seed, (uint64_t)(g.s1_begin + k), g.iteration, 1u);
+        if (stretch_accepts(P, z, lnew, g.lnp1[k], u3)) {
+            double zp = 0.0;
+            int jp = 0;
+            if (!local && v) stretch_draw(g.seed, (uint64_t)j, g.iteration, 0u, g.a, g.n_half, zp, jp);
+            for (int p = 0; p < P; p++) {
+                double c;
+                if (local) {
+                    c = g.x0[(size_t)p * n + jl];
+                } else {
+                    c = g.c0[(size_t)j * P + p];
+                    if (v) c = stretch_q(g.c1[(size_t)jp * P + p], zp, c);
+                }
+                const double q = stretch_q(c, z, g.x1[(size_t)p * n + k]);
+                g.x1[(size_t)p * n + k] = q;
+                if (g.x1_aos) g.x1_aos[(size_t)k * P + p] = q;
+            }
+            g.lnp1[k] = lnew;
+            if (g.accepted1) g.accepted1[k] += 1;
+        }
+    } else if (t < 2 * n) {
+        const int i = t - n;
+        if (g.x0_aos && g.dec_local[i])
+            for (int p = 0; p < P; p++) g.x0_aos[(size_t)i * P + p] = g.x0[(size_t)p * n + i];
+    }
+}
+
 __device__ __forceinline__ double box_muller(double u0, double u1) {
     return sqrt(-2.0 * log(u0)) * cospi(2.0 * u1);
 }
@@ -126,6 +172,10 @@ hipError_t launch_stretch_accept(int P, int n0, int64_t s0b, double* x, double* 
                                  const double* lnp_new, const double* z, uint64_t seed, uint64_t it, uint32_t half,
                                  const double* draws, int32_t* acc, hipStream_t st) {
     stretch_accept_kernel<<<grid1(n0), 256, 0, st>>>(P, n0, s0b, x, lnp, q, lnp_new, z, seed, it, half, draws, acc);
+    return hipGetLastError();
+}
+hipError_t launch_stretch_iteration_end(const IterEndArgs& g, hipStream_t st) {
+    stretch_iteration_end_kernel<<<grid1(2 * g.n), 256, 0, st>>>(g);
     return hipGetLastError();
 }
 hipError_t launch_mh_propose(int P, int n, int64_t b, const double* x, const double* scales, double step,

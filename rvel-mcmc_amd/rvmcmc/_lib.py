@@ -17,7 +17,7 @@ RVM_STATUS_ENCOUNTER = 2
 RVM_STATUS_NONFINITE = 3
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
-ABI_VERSION = 6  # include/rvmcmc.h RVM_ABI_VERSION
+ABI_VERSION = 7  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):
@@ -78,6 +78,12 @@ SIGNATURES = {
     "rvm_stretch_half_step": (C.c_int, [C.c_void_p, C.POINTER(ParamMapC), C.c_int32, C.c_int32, C.c_int64, _dp, _dp,
                                         _dp, C.c_int32, _dp, C.c_double, C.c_uint64, C.c_uint64, C.c_uint32,
                                         C.c_double, _dp, _dp, _dp, _dp]),
+    "rvm_stretch_iteration_begin": (C.c_int, [C.c_void_p, C.POINTER(ParamMapC), C.c_int32, C.c_int32, C.c_int64,
+                                              C.c_int64, _dp, _dp, _dp, C.c_int32, _dp, _dp, C.c_double, C.c_uint64,
+                                              C.c_uint64, C.c_double, _dp, _dp, _dp, _dp, _dp]),
+    "rvm_stretch_iteration_end": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, _dp, _dp, _dp, _dp, _dp,
+                                            _dp, _dp, C.c_int32, _dp, _dp, _dp, _dp, C.c_double, C.c_uint64,
+                                            C.c_uint64, _dp, _dp, _dp, _dp]),
     "rvm_mh_propose": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, _dp, C.c_double, C.c_uint64, C.c_uint64, _dp,
                                  _dp, _dp]),
     "rvm_mh_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, _dp, _dp, _dp, C.c_uint64, C.c_uint64, _dp, _dp,

@@ -240,6 +240,36 @@ class LoglPlan:
                 accepted.data_ptr() if accepted is not None else 0, _lib.stream_handle(stream))
         _lib.check(rc, "rvm_stretch_half_step")
 
+    def stretch_iteration_begin(self, pmap, X0, lnp0, X1, c0_aos, c1_aos, s0_begin, s1_begin, a, seed, iteration,
+                                lnp_spec, status_spec, dec, hill_factor=1.0, accepted0=None, stream=None):
+        """First launch of a speculative stretch iteration (rvm_stretch_iteration_begin): half 0's
+        half-step (X0 [dim][n], lnp0 [n] updated in place, decisions to dec [n]) and half 1's
+        proposals from X1 [dim][n] against both possible positions of their partners, logl of all
+        3 n slots to lnp_spec / status_spec [3 n].  c0_aos / c1_aos: both halves walker-major
+        [n_half][dim] as at the start of the iteration (unchanged until the end call)."""
+        torch = _torch()
+        for t in (X0, lnp0, X1, c0_aos, c1_aos, lnp_spec):
+            if t.dtype != torch.float64 or t.device != self.device or not t.is_contiguous():
+                raise ValueError("X0, lnp0, X1, c0_aos, c1_aos, lnp_spec must be contiguous float64 tensors on the "
+                                 "plan's device")
+        dim, n = X0.shape
+        n_half = c0_aos.shape[0]
+        if X1.shape != (dim, n) or lnp0.shape != (n,) or c0_aos.shape != (n_half, dim) or c1_aos.shape != (n_half, dim):
+            raise ValueError("shape mismatch between X0/X1 [dim][n], lnp0 [n] and c0_aos/c1_aos [n_half][dim]")
+        if lnp_spec.shape != (3 * n,) or status_spec.shape != (3 * n,) or dec.shape != (n,):
+            raise ValueError("lnp_spec / status_spec must be [3 n], dec [n]")
+        if status_spec.dtype != torch.int32 or dec.dtype != torch.int32:
+            raise ValueError("status_spec and dec must be int32")
+        if 3 * n > self.max_walkers:
+            raise ValueError(f"3 x {n} walker slots exceed the plan's max_walkers={self.max_walkers}")
+        with torch.cuda.device(self.device):
+            rc = self.lib.rvm_stretch_iteration_begin(
+                self._h, C.byref(pmap.c_map()), dim, n, int(s0_begin), int(s1_begin), X0.data_ptr(), lnp0.data_ptr(),
+                X1.data_ptr(), n_half, c0_aos.data_ptr(), c1_aos.data_ptr(), float(a), int(seed), int(iteration),
+                float(hill_factor), lnp_spec.data_ptr(), status_spec.data_ptr(), dec.data_ptr(),
+                accepted0.data_ptr() if accepted0 is not None else 0, _lib.stream_handle(stream))
+        _lib.check(rc, "rvm_stretch_iteration_begin")
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self.lib.rvm_plan_destroy(self._h)
@@ -250,6 +280,32 @@ class LoglPlan:
             self.close()
         except Exception:
             pass
+
+
+def stretch_iteration_end(X0, X0_aos, dec, dec_all, X1, X1_aos, lnp1, c0_aos, c1_aos, lnp_spec, status_spec,
+                          s0_begin, s1_begin, a, seed, iteration, accepted1=None, lnp_new=None, status_new=None,
+                          stream=None):
+    """Second launch of a speculative stretch iteration (rvm_stretch_iteration_end): half 1's
+    accepts with the logl variant its partner's decision (dec_all [n_half], global order)
+    selects; X1 [dim][n], lnp1, the mirrors X0_aos / X1_aos [n][dim] (nullable) updated."""
+    torch = _torch()
+    lib = _lib.load()
+    dim, n = X1.shape
+    n_half = c0_aos.shape[0]
+    if X0.shape != (dim, n) or lnp1.shape != (n,) or dec.shape != (n,) or dec_all.shape != (n_half,):
+        raise ValueError("shape mismatch in stretch_iteration_end")
+    for t in (X0_aos, X1_aos):
+        if t is not None and t.shape != (n, dim):
+            raise ValueError("mirrors must be [n][dim]")
+    ptr = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+    with torch.cuda.device(X1.device):
+        rc = lib.rvm_stretch_iteration_end(dim, n, int(s0_begin), int(s1_begin), X0.data_ptr(), ptr(X0_aos),
+                                           dec.data_ptr(), dec_all.data_ptr(), X1.data_ptr(), ptr(X1_aos),
+                                           lnp1.data_ptr(), n_half, c0_aos.data_ptr(), c1_aos.data_ptr(),
+                                           lnp_spec.data_ptr(), status_spec.data_ptr(), float(a), int(seed),
+                                           int(iteration), ptr(accepted1), ptr(lnp_new), ptr(status_new),
+                                           _lib.stream_handle(stream))
+    _lib.check(rc, "rvm_stretch_iteration_end")
 
 
 def obs_arrays(obs):

@@ -47,7 +47,8 @@ class DeviceOps:
         self.lib = _lib.load()
         st = sampler.state
         dt, mult, hint = st.integrator.plan_args(st.planets)
-        self.plan = engine.plan_for(sampler.obs, sampler.pmap.n_planets, dt, mult, sampler.nloc,
+        # room for the 3 n walker slots of a speculative iteration (iteration_begin)
+        self.plan = engine.plan_for(sampler.obs, sampler.pmap.n_planets, dt, mult, 3 * sampler.nloc,
                                     sampler.device, hint, sampler.pmap.inclined)
         self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
         self.track_status = False  # set True to histogram per-walker statuses (costs a small kernel)
@@ -91,6 +92,58 @@ class DeviceOps:
             self.timing.append((e0, e1, X0.shape[1]))
         if self.track_status:
             self.status_counts.index_add_(0, status.long(), torch.ones_like(status, dtype=torch.int64))
+
+    def speculation_pays(self):
+        """Whether one launch of 3 n walker slots (a whole speculative iteration) beats two
+        half-step launches of n, by the launch shape of launch_logl (rvm_logl.hip): a wave group of
+        64/L walkers per direction, one block per group while two blocks per group fit the CUs (the
+        longest level alone on its SIMD), else two groups per block with mirrored levels (SIMD
+        loads mult[i] + mult[nl-1-i]), one block per CU at a time."""
+        torch = _torch()
+        s = self.s
+        n_cu = torch.cuda.get_device_properties(s.device).multi_processor_count
+        npl = s.pmap.n_planets
+        wpb = 64 // (1 if npl == 1 else (2 if npl == 2 else 4))
+        mult = list(self.plan.mult)
+        t1 = max(mult)
+        t2 = max(mult[i] + mult[-1 - i] for i in range(len(mult)))
+
+        def units(W):
+            g = -(-W // wpb)
+            if 2 * g <= n_cu or 2 * len(mult) * 64 > 512:
+                return t1 * -(-2 * g // n_cu)
+            return t2 * -(-g // n_cu)
+
+        return units(3 * s.nloc) < 2 * units(s.nloc)
+
+    def iteration_begin(self, c0, c1):
+        """rvm_stretch_iteration_begin on the sampler's buffers (half 0 updated, all 3 n logl)."""
+        torch = _torch()
+        s = self.s
+        n = s.nloc
+        if self.timing is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        self.plan.stretch_iteration_begin(s.pmap, s.pos[0], s.lnp[0], s.pos[1], c0, c1, s.global_begin(0),
+                                          s.global_begin(1), s.a, s.seed, s.iteration, s._lnp_spec, s._st_spec,
+                                          s._dec, hill_factor=s.hill_factor, accepted0=s.naccepted[:n])
+        if self.timing is not None:
+            e1.record()
+            self.timing.append((e0, e1, 3 * n))
+        if self.track_status:
+            st = s._st_spec[:n]
+            self.status_counts.index_add_(0, st.long(), torch.ones_like(st, dtype=torch.int64))
+
+    def iteration_end(self, c0, c1, dec_all):
+        """rvm_stretch_iteration_end: half 1's accepts, both walker-major mirrors refreshed."""
+        torch = _torch()
+        s = self.s
+        n = s.nloc
+        engine.stretch_iteration_end(s.pos[0], s.pos_aos[0], s._dec, dec_all, s.pos[1], s.pos_aos[1], s.lnp[1], c0, c1,
+                                     s._lnp_spec, s._st_spec, s.global_begin(0), s.global_begin(1), s.a, s.seed,
+                                     s.iteration, accepted1=s.naccepted[n:], lnp_new=s._lnp_new, status_new=s._status)
+        if self.track_status:
+            self.status_counts.index_add_(0, s._status.long(), torch.ones_like(s._status, dtype=torch.int64))
 
     def accept(self, X0, lnp0, q, lnp_new, z, half, accepted, draws=None):
         s = self.s
@@ -144,6 +197,16 @@ class EnsembleSampler:
         self._aos_stale = True  # pos_aos (walker-major mirrors for the fused path) out of date
         self.naccepted = torch.zeros(2 * n, dtype=torch.int32, device=self.device)
         self.nevals = 0
+        # speculative whole iterations (iteration_begin / iteration_end, bit-identical to two
+        # half-steps): None = when the launch shape says they pay, True / False to force
+        self.speculative = None
+        self.nevals_speculative = 0  # walker-logL evaluations of the variants not taken
+        self._lnp_spec = torch.empty(3 * n, **f64)
+        self._st_spec = torch.empty(3 * n, dtype=torch.int32, device=self.device)
+        self._dec = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self._dec_all = torch.empty(self.halfk, dtype=torch.int32, device=self.device) if self.world > 1 else None
+        self._gather_aos0 = torch.empty((self.halfk, dim), **f64) if self.world > 1 else None
+        self._spec_pays = None
         # one launch per half-step (rvm_stretch_half_step) unless draws are injected or the ops
         # (e.g. the CPU restatements of the distributed tests) provide only the three-step path
         self.fused = hasattr(self.ops, "fused_half_step")
@@ -234,14 +297,50 @@ class EnsembleSampler:
         for h in (0, 1):
             self.check_initial(self.lnp[h])
 
+    def speculating(self):
+        """Whether step() runs speculative whole iterations (see `speculative`)."""
+        if not (self.fused and hasattr(self.ops, "iteration_begin")):
+            return False
+        if self.speculative is not None:
+            return bool(self.speculative)
+        if self._spec_pays is None:
+            self._spec_pays = bool(self.ops.speculation_pays())
+        return self._spec_pays
+
     def step(self):
         """One emcee iteration (both half-steps) over this rank's walkers."""
         if self.lnp[0] is None:
             self.compute_lnprob()
-        A, B = self.pos
-        self.half_step(A, self.lnp[0], B, 0)
-        self.half_step(B, self.lnp[1], A, 1)
+        if self.speculating():
+            self._speculative_iteration()
+        else:
+            A, B = self.pos
+            self.half_step(A, self.lnp[0], B, 0)
+            self.half_step(B, self.lnp[1], A, 1)
         self.iteration += 1
+
+    def _speculative_iteration(self):
+        """Both half-steps as one launch over 3 nloc walker slots (half 0, and half 1 against both
+        possible positions of each partner) plus a small accept launch; bit-identical to two
+        half_step calls.  Collectives (N > 1): the two halves' walker-major mirrors before the
+        launch, half 0's decisions between the two launches."""
+        torch = _torch()
+        if self._aos_stale:
+            self._refresh_aos()
+        if self.world == 1:
+            c0, c1 = self.pos_aos
+            dec_all = self._dec
+        else:
+            torch.distributed.all_gather_into_tensor(self._gather_aos0, self.pos_aos[0], group=self.group)
+            torch.distributed.all_gather_into_tensor(self._gather_aos, self.pos_aos[1], group=self.group)
+            c0, c1 = self._gather_aos0, self._gather_aos
+            dec_all = self._dec_all
+        self.ops.iteration_begin(c0, c1)
+        if self.world > 1:
+            torch.distributed.all_gather_into_tensor(self._dec_all, self._dec, group=self.group)
+        self.ops.iteration_end(c0, c1, dec_all)
+        self.nevals += 2 * self.nloc
+        self.nevals_speculative += self.nloc
 
     def gather_positions(self):
         """All walkers [W][dim] on every rank (host numpy), global order."""

@@ -19,7 +19,8 @@ def test_header_declares_expected_surface():
     fns = header_functions()
     for f in ("rvm_plan_create", "rvm_logl_batch", "rvm_stretch_propose", "rvm_stretch_accept",
               "rvm_mh_propose", "rvm_mh_accept", "rvm_fd_params", "rvm_smala_derive", "rvm_smala_propose",
-              "rvm_smala_accept", "rvm_stretch_half_step", "rvm_logl_derivs", "rvm_logl_derivs_workspace_bytes", "rvm_smala_metric",
+              "rvm_smala_accept", "rvm_stretch_half_step", "rvm_stretch_iteration_begin",
+              "rvm_stretch_iteration_end", "rvm_logl_derivs", "rvm_logl_derivs_workspace_bytes", "rvm_smala_metric",
               "rvm_last_error", "rvm_abi_version"):
         assert f in fns
 
@@ -28,7 +29,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 7
 
 
 def test_python_binding_matches_header():
@@ -47,6 +48,14 @@ def test_argument_errors_do_not_touch_the_device():
     assert lib.rvm_logl_batch(None, 1, 0, 1.0, 0, 0, 0, 0) < 0
     m = _lib.ParamMapC()
     assert lib.rvm_stretch_half_step(None, C.byref(m), 10, 1, 0, 0, 0, 0, 1, 0, 2.0, 0, 0, 0, 1.0, 0, 0, 0, 0) < 0
+    assert lib.rvm_stretch_iteration_begin(None, C.byref(m), 10, 1, 0, 8, 0, 0, 0, 8, 0, 0, 2.0, 0, 0, 1.0, 0, 0, 0,
+                                           0, 0) < 0
+    # end: half 1's walker range must lie in the second half (s1_begin >= n_half)
+    one = (C.c_double * 1)(0.0)
+    ione = (C.c_int32 * 1)(0)
+    assert lib.rvm_stretch_iteration_end(10, 1, 0, 0, one, 0, ione, ione, one, 0, one, 8, one, one, one, ione, 2.0,
+                                         0, 0, 0, 0, 0, 0) < 0
+    assert b"walker ranges" in lib.rvm_last_error()
     rows = (C.c_int32 * 2)(0, 1)
     assert lib.rvm_logl_derivs(None, 1, 0, 2, rows, 1.0, 0, 0, 0, 0, 0, 0) < 0
     # more epochs in one direction than the LDS-staged schedule holds: an argument error, caught

@@ -84,6 +84,73 @@ class FusedNumpyOps(NumpyOps):
         X0_aos.copy_(X0.t())
 
 
+class SpecNumpyOps(FusedNumpyOps):
+    """FusedNumpyOps plus the speculative iteration's contract (rvm_stretch_iteration_begin /
+    _end): both halves arrive walker-major and gathered (c0, c1, as at the start of the
+    iteration); begin does half 0's half-step and evaluates half 1's proposals against both
+    possible positions of their partners; end takes half 0's decisions in global order (dec_all)
+    and accepts half 1 with the variant they select."""
+
+    def speculation_pays(self):
+        return True
+
+    def _half0_proposals_all(self, C0, C1):
+        """Every half-0 walker's proposal [halfk][dim] from its own draws (keys 0 .. halfk-1)."""
+        s = self.s
+        u1, u2, _ = stretch_uniforms(s.seed, 0, s.halfk, s.iteration, 0)
+        zz = ((s.a - 1.0) * u1 + 1.0) * ((s.a - 1.0) * u1 + 1.0) / s.a
+        j = np.minimum(np.floor(u2 * s.halfk).astype(np.int64), s.halfk - 1)
+        return C1[j] - zz[:, None] * (C1[j] - C0)
+
+    def _half1_draws(self):
+        s = self.s
+        u1, u2, u3 = stretch_uniforms(s.seed, s.global_begin(1), s.nloc, s.iteration, 1)
+        zz = ((s.a - 1.0) * u1 + 1.0) * ((s.a - 1.0) * u1 + 1.0) / s.a
+        j = np.minimum(np.floor(u2 * s.halfk).astype(np.int64), s.halfk - 1)
+        return zz, j, u3
+
+    def iteration_begin(self, c0, c1):
+        s = self.s
+        n = s.nloc
+        assert c0.shape == c1.shape == (s.halfk, s.dim)
+        C0, C1 = c0.numpy().copy(), c1.numpy().copy()
+        dec0 = s.naccepted[:n].clone()
+        lnp_new = torch.empty(n, dtype=torch.float64)
+        st = torch.empty(n, dtype=torch.int32)
+        q = torch.empty_like(s.pos[0])
+        z = torch.empty(n, dtype=torch.float64)
+        self.propose(s.pos[0], c1.t().contiguous(), 0, q, z)
+        self.logl(q, out=lnp_new, status=st)
+        self.accept(s.pos[0], s.lnp[0], q, lnp_new, z, 0, s.naccepted[:n])
+        s._dec.copy_((s.naccepted[:n] - dec0).to(torch.int32))
+        s._lnp_spec[:n] = lnp_new
+        zz, j, _ = self._half1_draws()
+        Q0 = self._half0_proposals_all(C0, C1)
+        x1 = s.pos[1].numpy()
+        for v, C in enumerate((C0, Q0)):
+            qv = C[j].T - zz[None, :] * (C[j].T - x1)
+            s._lnp_spec[(1 + v) * n:(2 + v) * n] = self.logl(torch.from_numpy(qv))[0]
+        s._st_spec.zero_()
+
+    def iteration_end(self, c0, c1, dec_all):
+        s = self.s
+        n = s.nloc
+        assert dec_all.shape == (s.halfk,)
+        C0, C1 = c0.numpy(), c1.numpy()
+        zz, j, u3 = self._half1_draws()
+        v = dec_all.numpy()[j].astype(bool)
+        lnew = np.where(v, s._lnp_spec[2 * n:].numpy(), s._lnp_spec[n:2 * n].numpy())
+        c = np.where(v[:, None], self._half0_proposals_all(C0, C1)[j], C0[j])
+        x1 = s.pos[1].numpy()
+        q = c.T - zz[None, :] * (c.T - x1)
+        acc = torch.from_numpy((s.dim - 1.0) * np.log(zz) + lnew - s.lnp[1].numpy() > np.log(u3))
+        s.pos[1][:, acc] = torch.from_numpy(q)[:, acc]
+        s.lnp[1][acc] = torch.from_numpy(lnew)[acc]
+        s.naccepted[n:] += acc.to(torch.int32)
+        for h in (0, 1):
+            s.pos_aos[h].copy_(s.pos[h].t())
+
+
 def _initial_positions(state):
     rng = np.random.default_rng(3)
     scales = np.array([S2_SCALES[k] for k in state.get_rawkeys()])
@@ -95,8 +162,9 @@ def _run_sampler(fused=False, ckpt=None):
     from rvmcmc.state import State
 
     state = State(planets=[dict(p) for p in S2_PLANETS])
-    ens = EnsembleSampler(W, state, obs=None, seed=SEED, device="cpu", ops=FusedNumpyOps if fused else NumpyOps)
-    assert ens.fused == fused
+    ops = {False: NumpyOps, True: FusedNumpyOps, "spec": SpecNumpyOps}
+    ens = EnsembleSampler(W, state, obs=None, seed=SEED, device="cpu", ops=ops[fused])
+    assert ens.fused == bool(fused) and ens.speculating() == (fused == "spec")
     ens.set_positions(_initial_positions(state))
     ens.compute_lnprob()
     if ckpt is None:
@@ -108,7 +176,7 @@ def _run_sampler(fused=False, ckpt=None):
         ens.checkpoint(ckpt)
         if dist.is_initialized():
             dist.barrier()
-        ens = EnsembleSampler(W, state, obs=None, seed=0, device="cpu", ops=FusedNumpyOps if fused else NumpyOps)
+        ens = EnsembleSampler(W, state, obs=None, seed=0, device="cpu", ops=ops[fused])
         ens.restore(ckpt)
         for _ in range(ITERS - ITERS // 2):
             ens.step()
@@ -134,15 +202,21 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world,fused", [(2, False), (4, False), (2, True), (4, True)])
+@pytest.mark.parametrize("world,fused", [(2, False), (4, False), (2, True), (4, True), (1, "spec"), (2, "spec"),
+                                         (4, "spec")])
 def test_sharded_ensemble_bit_identical_to_single_process(tmp_path, world, fused):
-    """Three-launch path (SoA complement, all-gather + re-layout) and fused path (walker-major
-    complement gathered from the mirrors): every world size gives the single-process run."""
+    """Three-launch path (SoA complement, all-gather + re-layout), fused path (walker-major
+    complement gathered from the mirrors) and speculative whole iterations (both halves gathered,
+    half 0's decisions all-gathered between the two launches): every world size gives the
+    single-process three-launch run."""
     pos1, lnp1, acc1 = _run_sampler()
     if fused:
-        pf, lf, af = _run_sampler(fused=True)
+        pf, lf, af = _run_sampler(fused=fused)
         np.testing.assert_array_equal(pf, pos1)
         np.testing.assert_array_equal(lf, lnp1)
+        np.testing.assert_array_equal(af.numpy(), acc1.numpy())
+        if world == 1:
+            return
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), fused), nprocs=world, join=True)
     accs = []
     for r in range(world):

@@ -172,6 +172,7 @@ def test_fused_half_step_matches_three_launch_path(case):
         e = EnsembleSampler(W, s, obs, seed=77)
         assert e.fused
         e.fused = fused
+        e.speculative = False  # one launch per half-step (the speculative iteration: next test)
         e.set_positions(X0)
         for _ in range(iters):
             e.step()
@@ -184,6 +185,75 @@ def test_fused_half_step_matches_three_launch_path(case):
     assert 0.0 < acc < 1.0
     if case == "s2_wide":
         assert not np.isfinite(runs[0][1]).all() or acc < 0.5  # prior / encounter proposals exercised
+
+
+@pytest.mark.parametrize("case", ["s2", "s2_fixed_params", "s2_wide", "one_planet", "three_planets", "inclined",
+                                  "s2_large"])
+def test_speculative_iteration_matches_half_steps(case):
+    """rvm_stretch_iteration_begin / _end (both half-steps from one launch of 3 n walker slots,
+    half 1 evaluated against both possible positions of its partner) against two fused half-step
+    launches: positions, lnp, accept counts and the mirrors bit-identical after several
+    iterations.  Covers fixed kernel rows, prior / encounter proposals, 1 / 2 / 3 planets (1, 2 and
+    4 lanes per walker), inclined orbits and a batch whose 3 n slots need two-group blocks."""
+    torch = _torch()
+    from rvmcmc import state
+    from rvmcmc.ensemble import EnsembleSampler
+
+    planets = [dict(p) for p in S2_PLANETS]
+    kw = {}
+    W, rel, iters = 256, 1e-3, 5
+    if case == "s2_fixed_params":
+        kw = dict(ignore_params=[["h"], ["k", "l"]])
+    elif case == "s2_wide":
+        rel = 0.1
+    elif case == "one_planet":
+        planets = planets[:1]
+    elif case == "three_planets":
+        planets.append({"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0})
+    elif case == "inclined":
+        planets[0].update(ix=0.05, iy=-0.02)
+        planets[1].update(ix=0.01, iy=0.03)
+    elif case == "s2_large":
+        W, iters = 2 * 8256, 2
+    s = state.State(planets=planets, **kw)
+    obs = s2_obs_oracle()
+    rng = np.random.default_rng(5)
+    scales = np.array([S2_SCALES.get(k, 0.05) for k in s.get_rawkeys()])
+    X0 = s.get_params()[None] + rel * scales * rng.standard_normal((W, s.Nvars))
+    runs = []
+    for spec in (True, False):
+        e = EnsembleSampler(W, s, obs, seed=91)
+        e.speculative = spec
+        e.set_positions(X0)
+        for _ in range(iters):
+            e.step()
+        torch.cuda.synchronize()
+        assert e.speculating() == spec
+        mirrors = [m.cpu().numpy() for m in e.pos_aos]
+        for h in (0, 1):
+            np.testing.assert_array_equal(mirrors[h], e.pos[h].t().cpu().numpy())  # mirrors in step
+        runs.append((e.gather_positions(), e.gather_lnprob(), e.naccepted.cpu().numpy(), e.nevals))
+    np.testing.assert_array_equal(runs[0][0], runs[1][0])
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
+    np.testing.assert_array_equal(runs[0][2], runs[1][2])
+    assert runs[0][3] == runs[1][3] == W * iters + W  # useful evaluations only (+ the initial lnprob)
+    acc = runs[0][2].sum() / (W * iters)
+    assert 0.0 < acc < 1.0
+
+
+def test_speculation_is_chosen_by_launch_shape():
+    """The bench workload (4096 walkers, 2 planets: 2048 per half) speculates -- 6144 slots in one
+    launch of two-group blocks beat two launches of 2048 -- while 3 planets at 8192 walkers per GPU
+    (config 5: one half already needs two-group blocks) keep one launch per half-step."""
+    from rvmcmc import state
+    from rvmcmc.ensemble import EnsembleSampler
+
+    obs = s2_obs_oracle()
+    s2 = state.State(planets=[dict(p) for p in S2_PLANETS])
+    assert EnsembleSampler(4096, s2, obs, seed=1).speculating()
+    assert EnsembleSampler(1024, s2, obs, seed=1).speculating()
+    s3 = state.State(planets=[dict(p) for p in S2_PLANETS] + [{"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}])
+    assert not EnsembleSampler(8192, s3, obs, seed=1).speculating()
 
 
 def test_speculative_mh_is_bit_identical_to_sequential():
