@@ -11,9 +11,9 @@ cd /tmp
 i=0
 PMC_GROUPS=${GROUPS_OVERRIDE:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS SQ_INSTS_SMEM|SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE SQ_ACTIVE_INST_SCA|SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_THREAD_CYCLES_VALU SQ_IFETCH SQ_INSTS_BRANCH SQ_INST_CYCLES_SALU|FETCH_SIZE|WRITE_SIZE"}
 IFS='|' read -ra GRPS <<< "$PMC_GROUPS"
-# PMC_TARGET=bench (default): the bench's own launches (fused stretch half-steps, 2048 walkers
-# each; the 2 plain launches of the initial lnprob are skipped); PMC_TARGET=kbench: plain
-# likelihood launches of PMC_W walkers
+# PMC_TARGET=bench (default): the bench's own launches (speculative stretch iterations, 3 x 2048
+# walker slots each; the 1-walker get_logp and the 2 plain launches of the initial lnprob are
+# skipped); PMC_TARGET=kbench: plain likelihood launches of PMC_W walkers
 TARGET=${PMC_TARGET:-bench}
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
@@ -25,7 +25,7 @@ for grp in "${GRPS[@]}"; do
 done
 cd "$R"
 if [ "$TARGET" = "bench" ]; then
-  python3 scripts/pmc_summary.py gpurun_out/pmc 2048 2 "fused stretch half-step (bench.py)" | tee gpurun_out/pmc/summary.txt
+  python3 scripts/pmc_summary.py gpurun_out/pmc ${PMC_W:-6144} ${PMC_SKIP:-3} "speculative stretch iteration (bench.py)" | tee gpurun_out/pmc/summary.txt
 else
   python3 scripts/pmc_summary.py gpurun_out/pmc ${PMC_W:-2048} 0 "plain likelihood launch (kbench.py)" | tee gpurun_out/pmc/summary.txt
 fi
