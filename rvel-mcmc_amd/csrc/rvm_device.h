@@ -273,6 +273,7 @@ struct Lane {
     double kP[KickPairs<NP>::n];   // NP >= 3 (kickN): own-lane coefficient of every pair but (0,1)
     double kPh[KickPairs<NP>::n];  // the same times the current step
     int p;                  // own planet index (lane % L, clamped to NP-1)
+    int q;                  // lane index within the walker's group (lane % L, not clamped)
     uint64_t encm;          // wave mask of lanes that saw a pair closer than the exit distance
                             // (SGPRs: the kick's compares go straight into it; identical bits on
                             // all lanes of a walker's group)
@@ -304,7 +305,9 @@ __device__ __forceinline__ void lane_finish(Lane<NP>& s) {
         s.kC = p1 ? s.m[1] : -q * s.m[0];
         s.pair_s = p1 ? -0.0 : -1.0;
     } else {
-        s.pair_s = 0.0;
+        // kickN, 3 planets: round-0 pair of group lane q is (q >> 1, 2 + (q & 1)) in body indices:
+        // -0.0 for the star pairs (0,2), (0,3), -1.0 for (1,2), (1,3)
+        s.pair_s = (NP == 3 && s.q >= 2) ? -1.0 : -0.0;
         s.kB = s.kC = 0.0;
         s.kA = 0.0;
 #pragma unroll
@@ -779,8 +782,51 @@ __device__ __forceinline__ void kickN(Lane<NP>& s, double c1875) {
             if constexpr (D3) cmz = fma(s.m[i - 1], z[i], cmz);
         }
     }
-    uint64_t enc = ballot(s.ir * s.ir > s.idmin2);
     double vx = s.vx, vy = s.vy, vz = s.vz;
+    if constexpr (NP == 3 && L == 4) {
+        // The four pairs (0,2), (0,3), (1,2), (1,3) are split over the group's four lanes (lane q
+        // takes pair k = q: b = 2 + (q & 1), a = 1 on lanes 2 and 3), one inverse cube each,
+        // exchanged by DPP; (2,3) is formed on every lane.  The distances are the same expressions
+        // as in the generic loop below (fma(-0, x1, xb) = xb, fma(-1, x1, xb) = xb - x1), so the
+        // bits are the same: 2 v_rsq_f64 per lane and kick instead of 5.  Encounter bits: each
+        // lane's own pair, (2,3) everywhere, star--planet-1 on the planets' first lanes only
+        // (kick_enc_bits<3> reads all four lanes of a walker).
+        const bool b3 = (s.q & 1) != 0;
+        const double bx = b3 ? x[3] : x[2], by = b3 ? y[3] : y[2];
+        const double ox = fma(s.pair_s, x[1], bx), oy = fma(s.pair_s, y[1], by);
+        double ro = fma(ox, ox, oy * oy);
+        if constexpr (D3) {
+            const double bz = b3 ? z[3] : z[2];
+            const double oz = fma(s.pair_s, z[1], bz);
+            ro = fma(oz, oz, ro);
+        }
+        const double dx = x[3] - x[2], dy = y[3] - y[2], dz = z[3] - z[2];
+        double r23 = fma(dx, dx, dy * dy);
+        if constexpr (D3) r23 = fma(dz, dz, r23);
+        s.encm |= (ballot(s.ir * s.ir > s.idmin2) & 0x1111111111111111ull) | ballot(ro < s.dmin2) |
+                  ballot(r23 < s.dmin2);
+        const double io = rcube_nr(ro, c1875);
+        const double i23 = rcube_nr(r23, c1875);
+        const double ic[4] = {grp_get<L, 0>(io), grp_get<L, 1>(io), grp_get<L, 2>(io), grp_get<L, 3>(io)};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int a = k >> 1, b = 2 + (k & 1);
+            const double cf = s.kPh[k] * ic[k];
+            vx = fma(cf, x[b] - x[a], vx);
+            vy = fma(cf, y[b] - y[a], vy);
+            if constexpr (D3) vz = fma(cf, z[b] - z[a], vz);
+        }
+        const double cf = s.kPh[4] * i23;
+        vx = fma(cf, dx, vx);
+        vy = fma(cf, dy, vy);
+        if constexpr (D3) vz = fma(cf, dz, vz);
+        const double A = s.kAh * (s.ir * (s.ir * s.ir));
+        s.vx = fma(A, s.rx, vx);
+        s.vy = fma(A, s.ry, vy);
+        if constexpr (D3) s.vz = fma(A, s.rz, vz);
+        return;
+    }
+    uint64_t enc = ballot(s.ir * s.ir > s.idmin2);
     int k = 0;
 #pragma unroll
     for (int a = 0; a < NB; a++) {
@@ -815,11 +861,12 @@ __device__ __forceinline__ void kick(Lane<NP>& s, double dt, double c1875 = 1.87
         kick_generic<NP, L, D3>(s, dt);
 }
 
-// Encounter bits of a walker in Lane::encm relative to its first lane: kick2 splits the pair
-// tests over both lanes of the walker, kickN / kick_generic put all of them on every lane.
+// Encounter bits of a walker in Lane::encm relative to its first lane: kick2 and the 3-planet
+// kickN split the pair tests over the walker's lanes, kickN (4 planets) / kick_generic put all of
+// them on every lane.
 template <int NP>
 __device__ __forceinline__ constexpr uint64_t kick_enc_bits() {
-    return NP == 2 ? 3ull : 1ull;
+    return NP == 2 ? 3ull : (NP == 3 ? 0xFull : 1ull);
 }
 
 // star barycentric x-velocity: v0 = -sum_q (m_q / M_q) v'_q (gathered over the lane group)

@@ -258,6 +258,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 
     // ---- setup_sim: Pal -> heliocentric (own planet) -> Jacobi; Hill-radius exit distance -------
     s.p = pl_idx < NP ? pl_idx : NP - 1;
+    s.q = pl_idx;
     double Mi[NP + 1];
     Mi[0] = 1.0;
     double hill = 0.0;

@@ -12,7 +12,9 @@ import torch  # noqa: E402
 
 import oracle as O  # noqa: E402
 from conftest import S2_PLANETS, s2_obs_oracle  # noqa: E402
-from rvmcmc import engine  # noqa: E402
+from rvmcmc import _lib, engine  # noqa: E402
+
+_lib.LIB_PATH = os.environ.get("RVM_LIB", _lib.LIB_PATH)  # A/B runs against another build
 
 
 def main():
@@ -22,15 +24,19 @@ def main():
     nl = tuple(int(v) for v in lv.split(",")) if "," in lv else int(lv)
     spo = float(os.environ.get("SPO", "8"))
     obs = s2_obs_oracle()
-    pmin = engine.min_period(S2_PLANETS)
+    planets = [dict(p) for p in S2_PLANETS]
+    if os.environ.get("NPL") == "3":  # config 5's added planet
+        planets.append({"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0})
+    npl = len(planets)
+    pmin = engine.min_period(planets)
     dt = pmin / spo
     t, rv, er = engine.obs_arrays(obs)
-    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, nl, max(Ws), period_hint=pmin)
+    plan = engine.LoglPlan(t, rv, er, obs.Npoints, npl, dt, nl, max(Ws), period_hint=pmin)
     rng = np.random.default_rng(0)
     for W in Ws:
-        P = np.repeat(O.pal_params(S2_PLANETS)[None], W, 0)
-        P[:, :, :5] *= 1 + float(os.environ.get("BALL", "1e-3")) * rng.standard_normal((W, 2, 5))
-        K = torch.as_tensor(np.concatenate([P[:, p, :5].T for p in range(2)], 0).copy(), device="cuda")
+        P = np.repeat(O.pal_params(planets)[None], W, 0)
+        P[:, :, :5] *= 1 + float(os.environ.get("BALL", "1e-3")) * rng.standard_normal((W, npl, 5))
+        K = torch.as_tensor(np.concatenate([P[:, p, :5].T for p in range(npl)], 0).copy(), device="cuda")
         lp, st, _ = plan.logl(K)
         torch.cuda.synchronize()
         times = []
@@ -42,7 +48,7 @@ def main():
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1))
         idx = np.arange(0, W, max(1, W // 16))
-        ref, sref = O.logl_whx_batch(P[idx], 2, obs, dt, nl)
+        ref, sref = O.logl_whx_batch(P[idx], npl, obs, dt, nl)
         got = lp.cpu().numpy()[idx]
         err = np.max(np.abs(got - ref) / np.maximum(1, np.abs(ref)))
         ms = float(np.median(times))
