@@ -48,6 +48,7 @@ hipError_t launch_derivs(const DevPlan& P, int C, const double* params, int n_di
 struct rvm_plan {
     rvm::DevPlan dev;
     void* dmem = nullptr;        // one device allocation: schedule + workspace
+    void* lvmem = nullptr;       // level-split layout workspace (DevPlan::lv_*), when usable
     unsigned long long* slots = nullptr;  // [max_walkers] direction meeting slots (rvm_logl.hip)
     int32_t max_walkers = 0;
     int32_t steps[2] = {0, 0};
@@ -217,12 +218,49 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             P.spec[k] = zn <= 0.04 ? 1 : 0;
         }
     }
+    // level-split layout (rvm_logl.hip launch_logl): four strictly increasing levels and batches
+    // big enough that the plan's largest launch would need two-group blocks
+    P.lv_rv = nullptr;
+    P.lv_enc = nullptr;
+    P.lv_cnt = nullptr;
+    P.lv_emax = 0;
+    P.lv_stride = 0;
+    {
+        const int wpb = cfg->n_planets == 1 ? 64 : (cfg->n_planets == 2 ? 32 : 16);
+        const int64_t groups = ((int64_t)max_walkers + wpb - 1) / wpb;
+        bool inc = cfg->n_levels == 4;
+        for (int k = 1; inc && k < 4; k++) inc = mult[k] > mult[k - 1];
+        if (inc && P.n_cu > 0 && 2 * groups > P.n_cu) {
+            const int64_t emax = (int64_t)(nf > nb ? nf : nb) > 0 ? (int64_t)(nf > nb ? nf : nb) : 1;
+            const int64_t units = 2 * groups + 8;
+            const size_t b_rv = (size_t)(2 * 4 * emax * max_walkers) * sizeof(double);
+            const size_t b_enc = (size_t)(2 * 4 * (int64_t)max_walkers) * sizeof(int32_t);
+            const size_t b_cnt = (size_t)units * sizeof(int32_t);
+            if (hipMalloc(&plan->lvmem, b_rv + b_enc + b_cnt) == hipSuccess) {
+                unsigned char* base = reinterpret_cast<unsigned char*>(plan->lvmem);
+                P.lv_rv = reinterpret_cast<double*>(base);
+                P.lv_enc = reinterpret_cast<int32_t*>(base + b_rv);
+                P.lv_cnt = reinterpret_cast<int32_t*>(base + b_rv + b_enc);
+                P.lv_emax = (int32_t)emax;
+                P.lv_stride = max_walkers;
+                if (hipMemset(P.lv_cnt, 0, b_cnt) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                    (void)hipFree(plan->lvmem);
+                    plan->lvmem = nullptr;
+                    P.lv_rv = nullptr;
+                    P.lv_enc = nullptr;
+                    P.lv_cnt = nullptr;
+                }
+            }
+            // (no workspace: launches keep the LDS-coupled layout)
+        }
+    }
     *out = plan;
     return 0;
 }
 
 void rvm_plan_destroy(rvm_plan* plan) {
     if (!plan) return;
+    if (plan->lvmem) (void)hipFree(plan->lvmem);
     if (plan->dmem) (void)hipFree(plan->dmem);
     delete plan;
 }

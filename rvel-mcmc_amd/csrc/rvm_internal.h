@@ -29,6 +29,12 @@ struct DevPlan {
     int32_t n_obs;
     int32_t inclined;  // 1: 7 parameter rows per planet (ix, iy), 3-D integration
     int32_t n_cu;      // compute units of the plan's device (launch shape, launch_logl)
+    // level-split layout (launch_logl, rvm_logl.hip): each level wave of a walker group may run in
+    // its own workgroup; the waves meet through HBM instead of LDS.  Null when the plan cannot use it.
+    double* lv_rv;     // [2][n_levels][lv_emax][lv_stride] star vx per direction, level, epoch, walker
+    int32_t* lv_enc;   // [2][n_levels][lv_stride] encounter / prior flags per level
+    int32_t* lv_cnt;   // [units] level waves arrived per (walker group, direction); 0 between launches
+    int32_t lv_emax, lv_stride;
     DirSched fwd, bwd;
 };
 

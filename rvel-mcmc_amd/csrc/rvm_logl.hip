@@ -22,6 +22,14 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
+// FMA contraction only within one source expression (explicit fma() everywhere it matters): the
+// same step code then rounds identically in every loop it is inlined into (speculative and gated
+// segments, both launch layouts), so a walker's bits never depend on its wave-mates or the layout.
+// (The default -ffp-contract=fast fuses across statements depending on the surrounding code.)
+#pragma clang fp contract(on)
+
 #include "rvm_device.h"
 #include "rvm_internal.h"
 #include "rvm_stretch.h"
@@ -113,6 +121,25 @@ __device__ __forceinline__ double walker_param(bool stretch, const double* __res
     return stretch_q(c, z, sa.x1[(size_t)k * sa.n_spec + w]);
 }
 
+// a fused launch's walker slot: its kind (0 = half-step / half 0, 1 / 2 = half 1 against its
+// partner's rejected / accepted position), walker index within its half, its stretch draws and
+// (kind 2) the partner's
+__device__ __forceinline__ void stretch_slot(const StretchArgs& sa, int wl, int& kind, int& wk, double& z, int& j,
+                                             double& zp, int& jp) {
+    const int nsp = sa.n_spec;
+    kind = nsp > 0 ? (wl < nsp ? 0 : (wl < 2 * nsp ? 1 : 2)) : 0;
+    wk = wl - kind * nsp;
+    zp = 0.0;
+    jp = 0;
+    if (kind == 0) {
+        stretch_draw(sa.seed, (uint64_t)(sa.s0_begin + wk), sa.iteration, sa.half, sa.a, sa.n1, z, j);
+    } else {
+        stretch_draw(sa.seed, (uint64_t)(sa.s1_begin + wk), sa.iteration, 1u, sa.a, sa.n1, z, j);
+        // the partner's own draws (half 0's keys are its global indices 0 .. n1-1)
+        if (kind == 2) stretch_draw(sa.seed, (uint64_t)j, sa.iteration, 0u, sa.a, sa.n1, zp, jp);
+    }
+}
+
 __device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, int gi, int r, double v) {
     if (stager) l_q[r * GW + gi] = v;
     return v;
@@ -123,7 +150,7 @@ __device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, in
 #define RVM_SLOT_EMPTY 0x7FF4DEADBEEF0001ULL  // a NaN pattern no direction result can take
 
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
-template <int NP, bool D3>
+template <int NP, bool D3, bool DEC>
 __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                                                                    const double* __restrict__ params,
                                                                    const double hill_factor,
@@ -131,7 +158,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                                                                    double* __restrict__ rv_out,
                                                                    double* __restrict__ logl_out,
                                                                    int32_t* __restrict__ status_out,
-                                                                   const StretchArgs sa) {
+                                                                   const StretchArgs sa, const int nA) {
     constexpr int L = LanesPerWalker<NP>::value;  // lanes per walker (one per planet)
     constexpr int WPB = 64 / L;                    // walkers per block (= per wave)
     PROF_T(t_start);
@@ -142,16 +169,41 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // runs the levels in mirrored order: consecutive waves of a block land on consecutive SIMDs,
     // so wave i of group 1 shares a SIMD with wave i of group 0 and every SIMD carries
     // mult[i] + mult[nl-1-i] steps per base step instead of up to 2 mult[nl-1].
+    //
+    // Level-split layout (nA > 0; four levels m0 < m1 < m2 < m3, 1-D grid of 8-wave blocks, wave i
+    // on SIMD i % 4): a unit = (walker group, direction), u = 2 group + direction.  Blocks b < nA
+    // carry levels (3, 3, 2, 2, -, -, 0, 0) of units 2b and 2b + 1 -- SIMD loads m3, m3, m2 + m0,
+    // m2 + m0; waves 4 and 5 only help stage the schedule -- and the others level 1 of eight
+    // units (2 m1 on every SIMD).  (136 VGPRs per lane: one such block per CU.)  A unit's level waves then sit in
+    // different workgroups: they hand their star velocities over through HBM (P.lv_*), and the
+    // last one to arrive forms the Richardson RVs and chi^2 (same arithmetic as the LDS path).
     const int nl = P.n_levels;
     const int wv = threadIdx.x >> 6;
-    const int grp = wv >= nl ? 1 : 0;
-    const int lvl = grp ? 2 * nl - 1 - wv : wv;    // wave-uniform extrapolation level
-    const int G = (blockDim.x >> 6) / nl;
+    constexpr bool dec = DEC;  // (nA > 0)
+    int grp, lvl, G, d, w0;
+    bool idle = false;
+    // (recomputed where needed, not kept live through the integration)
+    auto unit_of = [&]() { return (int)blockIdx.x < nA ? 2 * (int)blockIdx.x + (wv & 1) : 8 * ((int)blockIdx.x - nA) + wv; };
+    if (dec) {
+        const int b = blockIdx.x;
+        const int unit = __builtin_amdgcn_readfirstlane(unit_of());  // wave-uniform (SGPRs)
+        lvl = __builtin_amdgcn_readfirstlane(b < nA ? (wv < 2 ? 3 : (wv < 4 ? 2 : 0)) : 1);
+        idle = b < nA && (wv == 4 || wv == 5);
+        grp = 0;
+        G = 1;
+        d = unit & 1;
+        w0 = (unit >> 1) * WPB;
+    } else {
+        grp = wv >= nl ? 1 : 0;
+        lvl = grp ? 2 * nl - 1 - wv : wv;  // wave-uniform extrapolation level
+        G = (blockDim.x >> 6) / nl;
+        d = blockIdx.y;
+        w0 = (blockIdx.x * G + grp) * WPB;  // first walker of the group
+    }
+    const bool live = w0 < W && !idle;  // level-split: waves past the last unit only help stage the schedule
     const int lane = threadIdx.x & 63;
     const int slot = lane / L;                     // walker slot within the group
     const int pl_idx = lane % L;
-    const int d = blockIdx.y;
-    const int w0 = (blockIdx.x * G + grp) * WPB;   // first walker of the group
     const int w = w0 + slot;
     const bool valid = w < W;
     const int wl = valid ? w : (W - 1);
@@ -172,10 +224,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const bool spec = P.spec[lvl_u] != 0 && nt <= 6;
     const double inv_mult = P.inv_mult[lvl_u];
     const int E = S.n_epochs;
-    double* l_len = s_sched;
-    double* l_rv = s_sched + E;
-    double* l_s2 = s_sched + 2 * E;
-    int* l_n = reinterpret_cast<int*>(s_sched + 3 * E);
+    const int emax2 = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
+    double* l_dir = dec ? s_sched + (size_t)d * 4 * emax2 : s_sched;  // level-split: both directions staged
+    double* l_len = l_dir;
+    double* l_rv = l_dir + E;
+    double* l_s2 = l_dir + 2 * E;
+    int* l_n = reinterpret_cast<int*>(l_dir + 3 * E);
     int* l_idx = l_n + E;
     // fused stretch half-step: the proposal rows, z, u3 and the current lnp of every walker of the
     // block, for the lane that finishes the walker (end of the kernel)
@@ -187,7 +241,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const int i0 = threadIdx.x;
     double st_h = 0.0, st_rv = 0.0, st_s2 = 0.0;
     int st_n = 0, st_idx = 0;
-    if (i0 < E) {
+    if (!dec && i0 < E) {
         st_h = S.seg_h1[i0];
         st_rv = S.obs_rv[i0];
         st_s2 = S.obs_s2[i0];
@@ -200,24 +254,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // q = c_j - z (c_j - x) mapped onto the kernel rows (rvm_stretch.h, rvm_param_map).
     constexpr int PR = D3 ? 7 : 5;  // parameter rows per planet
     const bool stretch = sa.c != nullptr;
-    double zst = 0.0;
-    int jst = 0;
-    // slot kind (speculative iteration, StretchArgs): 0 = a half-step walker / half 0, 1 and 2 =
-    // half 1's walker wk against its partner's rejected / accepted position
-    const int nsp = sa.n_spec;
-    const int kind = (stretch && nsp > 0) ? (wl < nsp ? 0 : (wl < 2 * nsp ? 1 : 2)) : 0;
-    const int wk = wl - kind * nsp;
-    double zp = 0.0;
-    int jp = 0;
-    const bool stager = stretch && lvl == 0 && pl_idx == 0 && kind == 0;  // one lane per walker stages
+    double zst = 0.0, zp = 0.0;
+    int jst = 0, jp = 0, kind = 0, wk = wl;
+    const bool stager = !dec && stretch && lvl == 0 && pl_idx == 0 && kind == 0;  // one lane per walker stages
     if (stretch) {
-        if (kind == 0) {
-            stretch_draw(sa.seed, (uint64_t)(sa.s0_begin + wk), sa.iteration, sa.half, sa.a, sa.n1, zst, jst);
-        } else {
-            stretch_draw(sa.seed, (uint64_t)(sa.s1_begin + wk), sa.iteration, 1u, sa.a, sa.n1, zst, jst);
-            // the partner's own draws (half 0's keys are its global indices 0 .. n1-1)
-            if (kind == 2) stretch_draw(sa.seed, (uint64_t)jst, sa.iteration, 0u, sa.a, sa.n1, zp, jp);
-        }
+        // slot kind (speculative iteration, StretchArgs): see stretch_slot
+        stretch_slot(sa, wl, kind, wk, zst, jst, zp, jp);
         if (stager) {
             constexpr int R = PR * NP;
             l_q[R * GW + gi] = zst;
@@ -338,23 +380,40 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         s.encm = t0.encm;
     }
 
-    if (i0 < E) {
-        l_len[i0] = st_h;
-        l_rv[i0] = st_rv;
-        l_s2[i0] = st_s2;
-        l_n[i0] = st_n;
-        l_idx[i0] = st_idx;
-    }
-    for (int i = i0 + blockDim.x; i < E; i += blockDim.x) {
-        l_len[i] = S.seg_h1[i];
-        l_rv[i] = S.obs_rv[i];
-        l_s2[i] = S.obs_s2[i];
-        l_n[i] = S.seg_n[i];
-        l_idx[i] = S.obs_idx[i];
+    if (!dec) {
+        if (i0 < E) {
+            l_len[i0] = st_h;
+            l_rv[i0] = st_rv;
+            l_s2[i0] = st_s2;
+            l_n[i0] = st_n;
+            l_idx[i0] = st_idx;
+        }
+        for (int i = i0 + blockDim.x; i < E; i += blockDim.x) {
+            l_len[i] = S.seg_h1[i];
+            l_rv[i] = S.obs_rv[i];
+            l_s2[i] = S.obs_s2[i];
+            l_n[i] = S.seg_n[i];
+            l_idx[i] = S.obs_idx[i];
+        }
+    } else {
+        for (int dd = 0; dd < 2; dd++) {
+            const DirSched& SD = dd ? P.bwd : P.fwd;
+            double* b = s_sched + (size_t)dd * 4 * emax2;
+            const int ED = SD.n_epochs;
+            int* bn = reinterpret_cast<int*>(b + 3 * ED);
+            for (int i = i0; i < ED; i += blockDim.x) {
+                b[i] = SD.seg_h1[i];
+                b[ED + i] = SD.obs_rv[i];
+                b[2 * ED + i] = SD.obs_s2[i];
+                bn[i] = SD.seg_n[i];
+                bn[ED + i] = SD.obs_idx[i];
+            }
+        }
     }
 
     // ---- integrate outward from t = 0 through this direction's epochs -------------------------
     __syncthreads();  // schedule staged
+    if (dec && !live) return;  // (no block barrier follows in the level-split layout)
     PROF_T(t_pro);
 #ifdef RVM_PROFILE
     unsigned long long t_seg = 0, t_epo = 0;
@@ -362,6 +421,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     int redo = 0;      // speculative segments redone gated (counted in the timing build only)
     int spec_off = 0;  // wave-uniform: segments left to run gated after a redo
     double chi2 = 0.0;
+    // level-split: this lane's column of P.lv_rv (advanced by one epoch row per epoch)
+    double* rvp = dec ? P.lv_rv + (size_t)(d * nl + lvl) * P.lv_emax * P.lv_stride + wl : nullptr;
+    const int rv_stride = dec ? P.lv_stride : 0;
     int n1 = E > 0 ? l_n[0] : 0;
     double len = E > 0 ? l_len[0] : 0.0;
     for (int e = 0; e < E; e++) {
@@ -391,9 +453,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         }
         PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
-        if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
-        __syncthreads();
-        if (lvl == 0 && lane < WPB) {  // lane `lane` of wave 0 owns walker slot `lane`
+        if (dec) {
+            if (pl_idx == 0 && valid) *rvp = v0;
+            rvp += rv_stride;
+        } else {
+            if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
+            __syncthreads();
+        }
+        if (!dec && lvl == 0 && lane < WPB) {  // lane `lane` of wave 0 owns walker slot `lane`
             double rvx = 0.0;
             for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv[e & 1][k][lane];
             const double r = rvx - l_rv[e];
@@ -410,55 +477,130 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #endif
     }
 #undef prm
-    if (pl_idx == 0)
-        s_enc[lvl][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
-    __syncthreads();
-    if (lvl == 0 && lane < WPB) {
-        const int wo = w0 + lane;
-        if (wo < W) {
-            int enc = 0;
-            for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
-            int st = (enc & 2) ? RVM_STATUS_PRIOR : RVM_STATUS_OK;
-            if (st == RVM_STATUS_OK && (enc & 1)) st = RVM_STATUS_ENCOUNTER;
-            if (st == RVM_STATUS_OK && !isfinite(chi2)) st = RVM_STATUS_NONFINITE;
-            // ---- the two directions of a walker meet: the second to arrive finishes it ----------
-            // (one agent-scope exchange carries the other direction's result: no fence, no barrier)
-            const double mine = st == RVM_STATUS_OK ? chi2 : -(double)st;
-            const unsigned long long old = __hip_atomic_exchange(
-                slots + wo, (unsigned long long)__double_as_longlong(mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (old != RVM_SLOT_EMPTY) {
-                __hip_atomic_store(slots + wo, RVM_SLOT_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const double other = __longlong_as_double((long long)old);
-                const int st_o = other < 0.0 ? (int)(-other) : RVM_STATUS_OK;
-                const int sf = d == 0 ? st : st_o, sb = d == 0 ? st_o : st;
-                const double cf = d == 0 ? chi2 : other, cb = d == 0 ? other : chi2;
-                int stw = sf != RVM_STATUS_OK ? sf : sb;  // both directions see the same PRIOR verdict
-                const double lp0 = -((cb + cf) / P.npoints);  // state.py:98, 109
-                if (stw == RVM_STATUS_OK && !isfinite(lp0)) stw = RVM_STATUS_NONFINITE;
-                const double lp = stw == RVM_STATUS_OK ? lp0 : -INFINITY;
-                if (logl_out) logl_out[wo] = lp;
-                if (status_out) status_out[wo] = stw;
-                if (stretch && (sa.n_spec == 0 || wo < sa.n_spec)) {
-                    // emcee accept with the proposal staged in the prologue (half 1's slots of a
-                    // speculative iteration only deliver their logl: rvm_stretch_iteration_end)
-                    constexpr int R = PR * NP;
-                    const int gl = grp * WPB + lane;
-                    const double z = l_q[R * GW + gl], u3 = l_q[(R + 1) * GW + gl];
-                    const bool acc = stretch_accepts(sa.dim, z, lp, l_q[(R + 2) * GW + gl], u3);
-                    if (acc) {
+    const int encflag = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
+    constexpr int R = PR * NP;
+    // ---- the two directions of a walker meet: the second to arrive finishes it ----------------
+    // (one agent-scope exchange carries the other direction's result: no fence, no barrier).
+    // row(r), z, u3, lnp0: the walker's proposal and accept inputs (fused stretch half-step)
+    auto finish = [&](const int wo, const double chi2w, const int enc, auto&& row, const double z, const double u3,
+                      const double lnp0) {
+        int st = (enc & 2) ? RVM_STATUS_PRIOR : RVM_STATUS_OK;
+        if (st == RVM_STATUS_OK && (enc & 1)) st = RVM_STATUS_ENCOUNTER;
+        if (st == RVM_STATUS_OK && !isfinite(chi2w)) st = RVM_STATUS_NONFINITE;
+        const double mine = st == RVM_STATUS_OK ? chi2w : -(double)st;
+        const unsigned long long old = __hip_atomic_exchange(
+            slots + wo, (unsigned long long)__double_as_longlong(mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == RVM_SLOT_EMPTY) return;
+        __hip_atomic_store(slots + wo, RVM_SLOT_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double other = __longlong_as_double((long long)old);
+        const int st_o = other < 0.0 ? (int)(-other) : RVM_STATUS_OK;
+        const int sf = d == 0 ? st : st_o, sb = d == 0 ? st_o : st;
+        const double cf = d == 0 ? chi2w : other, cb = d == 0 ? other : chi2w;
+        int stw = sf != RVM_STATUS_OK ? sf : sb;  // both directions see the same PRIOR verdict
+        const double lp0 = -((cb + cf) / P.npoints);  // state.py:98, 109
+        if (stw == RVM_STATUS_OK && !isfinite(lp0)) stw = RVM_STATUS_NONFINITE;
+        const double lp = stw == RVM_STATUS_OK ? lp0 : -INFINITY;
+        if (logl_out) logl_out[wo] = lp;
+        if (status_out) status_out[wo] = stw;
+        if (stretch && (sa.n_spec == 0 || wo < sa.n_spec)) {
+            // emcee accept (half 1's slots of a speculative iteration only deliver their logl:
+            // rvm_stretch_iteration_end)
+            const bool acc = stretch_accepts(sa.dim, z, lp, lnp0, u3);
+            if (acc) {
 #pragma unroll
-                        for (int r = 0; r < R; r++) {
-                            if (sa.src[r] >= 0) {
-                                const double v = l_q[r * GW + gl];
-                                sa.x[(size_t)sa.src[r] * sa.xstride + wo] = v;
-                                if (sa.x_aos) sa.x_aos[(size_t)wo * sa.dim + sa.src[r]] = v;
-                            }
-                        }
-                        sa.lnp[wo] = lp;
-                        if (sa.accepted) sa.accepted[wo] += 1;
+                for (int r = 0; r < R; r++) {
+                    if (sa.src[r] >= 0) {
+                        const double v = row(r);
+                        sa.x[(size_t)sa.src[r] * sa.xstride + wo] = v;
+                        if (sa.x_aos) sa.x_aos[(size_t)wo * sa.dim + sa.src[r]] = v;
                     }
-                    if (sa.dec) sa.dec[wo] = acc ? 1 : 0;
                 }
+                sa.lnp[wo] = lp;
+                if (sa.accepted) sa.accepted[wo] += 1;
+            }
+            if (sa.dec) sa.dec[wo] = acc ? 1 : 0;
+        }
+    };
+    if (!dec) {
+        if (pl_idx == 0) s_enc[lvl][slot] = encflag;
+        __syncthreads();
+        if (lvl == 0 && lane < WPB) {
+            const int wo = w0 + lane;
+            if (wo < W) {
+                int enc = 0;
+                for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
+                const int gl = grp * WPB + lane;
+                auto row = [&](int r) { return l_q[r * GW + gl]; };
+                if (stretch)
+                    finish(wo, chi2, enc, row, l_q[R * GW + gl], l_q[(R + 1) * GW + gl], l_q[(R + 2) * GW + gl]);
+                else
+                    finish(wo, chi2, enc, row, 0.0, 0.0, 0.0);
+            }
+        }
+    } else {
+        // level-split: publish this level's flags, count the unit's arrivals; the last level wave
+        // to arrive combines all levels (their RVs went to P.lv_rv at every epoch)
+        if (pl_idx == 0 && valid) P.lv_enc[(size_t)(d * nl + lvl) * P.lv_stride + w] = encflag;
+        __threadfence();  // release this wave's RVs and flags (agent scope: the units span XCDs)
+        int arrived = 0;
+        const int unit = unit_of();
+        if (lane == 0) arrived = atomicAdd(P.lv_cnt + unit, 1);
+        arrived = __builtin_amdgcn_readfirstlane(arrived);
+        if (arrived != nl - 1) return;
+        if (lane == 0) P.lv_cnt[unit] = 0;  // all nl arrived: ready for the next launch
+        __threadfence();  // acquire the other levels' stores
+        if (pl_idx == 0 && valid) {
+            int enc = 0;
+            for (int k = 0; k < nl; k++) enc |= __builtin_nontemporal_load(P.lv_enc + (size_t)(d * nl + k) * P.lv_stride + w);
+            // (nl = 4 here) epochs in chunks of CH, software-pipelined: the next chunk's 4 CH loads
+            // are in flight while this chunk is combined (the other levels' values come from other
+            // XCDs' stores, an HBM round trip each)
+            constexpr int CH = 8;
+            const size_t ls = (size_t)P.lv_emax * P.lv_stride;
+            const double* rvb = P.lv_rv + (size_t)(d * 4) * ls + w;
+            auto load_chunk = [&](int e0, double (&v)[CH][4]) {
+#pragma unroll
+                for (int i = 0; i < CH; i++) {
+                    const int e = e0 + i < E ? e0 + i : E - 1;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) v[i][k] = __builtin_nontemporal_load(rvb + k * ls + (size_t)e * P.lv_stride);
+                }
+            };
+            double chi2w = 0.0;
+            double va[CH][4], vb[CH][4];
+            if (E > 0) load_chunk(0, va);
+            for (int e0 = 0; e0 < E; e0 += CH) {
+                if (e0 + CH < E) load_chunk(e0 + CH, vb);
+#pragma unroll
+                for (int i = 0; i < CH; i++) {
+                    const int e = e0 + i;
+                    if (e < E) {
+                        double rvx = 0.0;
+#pragma unroll
+                        for (int k = 0; k < 4; k++) rvx += P.lw[k] * va[i][k];
+                        const double r = rvx - l_rv[e];
+                        chi2w += (r * r) / l_s2[e];
+                        if (rv_out != nullptr) rv_out[(size_t)l_idx[e] * W + w] = rvx;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < CH; i++)
+#pragma unroll
+                    for (int k = 0; k < 4; k++) va[i][k] = vb[i][k];
+            }
+            if (stretch) {
+                // the slot's draws again (recomputed from an opaque index rather than kept live
+                // through the integration)
+                int wo = w, k2, wk2, j2, jp2;
+                double z2, zp2;
+                asm volatile("" : "+v"(wo));
+                stretch_slot(sa, wo, k2, wk2, z2, j2, zp2, jp2);
+                auto row = [&](int r) { return walker_param(true, params, W, wk2, sa, r, z2, j2, k2, zp2, jp2); };
+                finish(w, chi2w, enc, row, z2, stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half),
+                       sa.lnp[wo]);
+            } else {
+                auto row = [&](int) { return 0.0; };
+                finish(w, chi2w, enc, row, 0.0, 0.0, 0.0);
             }
         }
     }
@@ -491,13 +633,38 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
     // latency-bound); beyond that two groups with mirrored level order per block, which pairs
     // the heaviest level with the lightest on each SIMD (logl_kernel)
     const int G = (P.n_cu > 0 && 2 * groups > P.n_cu && 2 * P.n_levels * 64 <= 512) ? 2 : 1;
-    const dim3 grid((groups + G - 1) / G, 2);
-    const dim3 block(64 * P.n_levels * G);
+    dim3 grid((groups + G - 1) / G, 2);
+    dim3 block(64 * P.n_levels * G);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t rows = (size_t)(P.inclined ? 7 : 5) * P.n_planets;
-    const size_t smem = (size_t)emax * 4 * sizeof(double) + (sa.c ? (rows + 3) * G * wpb * sizeof(double) : 0);
-#define RVM_LAUNCH(NPV, D3V) \
-    logl_kernel<NPV, D3V><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, logl, status, sa)
+    size_t smem = (size_t)emax * 4 * sizeof(double) + (sa.c ? (rows + 3) * G * wpb * sizeof(double) : 0);
+    // level-split layout (logl_kernel) when it lowers the heaviest SIMD's load: in steps per base
+    // step, max(m3, m2 + m0, 2 m1) for one round of <= n_cu blocks, against m3 per round of
+    // single-group blocks or max_i(m_i + m_{n-1-i}) per round of two-group blocks
+    int nA = 0;
+    if (P.lv_rv != nullptr && W <= P.lv_stride && P.n_levels == 4 && P.n_cu > 0) {
+        const int* m = P.mult;
+        const int units = 2 * groups;
+        const int na = groups, nb = (units + 7) / 8;
+        const int c_dec = std::max(m[3], std::max(m[2] + m[0], 2 * m[1]));
+        const int c_cpl = G == 1 ? m[3] * ((2 * groups + P.n_cu - 1) / P.n_cu)
+                                 : std::max(m[0] + m[3], m[1] + m[2]) * ((groups + P.n_cu - 1) / P.n_cu);
+        if (na + nb <= P.n_cu && c_dec < c_cpl) {
+            nA = na;
+            grid = dim3(na + nb, 1);
+            block = dim3(8 * 64);
+            smem = (size_t)emax * 8 * sizeof(double);
+        }
+    }
+#define RVM_LAUNCH(NPV, D3V)                                                                                \
+    do {                                                                                                 \
+        if (nA > 0)                                                                                      \
+            logl_kernel<NPV, D3V, true><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, \
+                                                                       logl, status, sa, nA);            \
+        else                                                                                             \
+            logl_kernel<NPV, D3V, false><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots,  \
+                                                                        rv_out, logl, status, sa, nA);   \
+    } while (0)
     const bool inc = P.inclined != 0;
     switch (P.n_planets) {
         case 1:

@@ -98,7 +98,8 @@ class DeviceOps:
         half-step launches of n, by the launch shape of launch_logl (rvm_logl.hip): a wave group of
         64/L walkers per direction, one block per group while two blocks per group fit the CUs (the
         longest level alone on its SIMD), else two groups per block with mirrored levels (SIMD
-        loads mult[i] + mult[nl-1-i]), one block per CU at a time."""
+        loads mult[i] + mult[nl-1-i]), one block per CU at a time, or the level-split layout (SIMD
+        loads max(m3, m2 + m0, 2 m1)) when its blocks fit the CUs."""
         torch = _torch()
         s = self.s
         n_cu = torch.cuda.get_device_properties(s.device).multi_processor_count
@@ -112,7 +113,12 @@ class DeviceOps:
             g = -(-W // wpb)
             if 2 * g <= n_cu or 2 * len(mult) * 64 > 512:
                 return t1 * -(-2 * g // n_cu)
-            return t2 * -(-g // n_cu)
+            c = t2 * -(-g // n_cu)
+            # level-split layout (four increasing levels, one round of g + ceil(2g / 8) blocks; the
+            # plan of a speculative sampler has its workspace: 2 g > n_cu here)
+            if len(mult) == 4 and all(a < b for a, b in zip(mult, mult[1:])) and g + -(-2 * g // 8) <= n_cu:
+                c = min(c, max(mult[3], mult[2] + mult[0], 2 * mult[1]))
+            return c
 
         return units(3 * s.nloc) < 2 * units(s.nloc)
 

@@ -272,11 +272,14 @@ def test_fake_observation_matches_oracle():
     np.testing.assert_allclose(o.rvb, r2.rvb, rtol=0, atol=1e-10)
 
 
-@pytest.mark.parametrize("W", [4096, 4128, 8192])
+@pytest.mark.parametrize("W", [4096, 4128, 6000, 8192])
 def test_large_batch_size_independent_results(W):
     """A walker's logL does not depend on the batch it is launched in (W vs 1).  4096 runs one
     walker group per block; 4128 and 8192 exceed one block per CU and run two groups per block
-    with mirrored level order (4128: the last block's second group is partly empty)."""
+    with mirrored level order (4128: the last block's second group is partly empty); 6000 runs
+    the level-split layout (each level wave in its own block, levels meeting through HBM; the
+    last type-B block partly empty) and must give the same bits as the LDS-coupled single
+    launches."""
     obs = s2_obs_oracle()
     plan, _ = _plan(obs, S2_PLANETS, max_walkers=W)
     P = _ball(S2_PLANETS, W, seed=21)
@@ -288,19 +291,21 @@ def test_large_batch_size_independent_results(W):
     assert np.isfinite(big).all()
 
 
-def test_two_group_blocks_vs_oracle_three_planets():
-    """3 planets, 4160 walkers: 16 walkers per wave, two mirrored groups per block; T1 on a
-    subset against the oracle, and the full batch against single launches."""
+@pytest.mark.parametrize("W", [4160, 2900])
+def test_two_group_blocks_vs_oracle_three_planets(W):
+    """3 planets: 16 walkers per wave; 4160 walkers run two mirrored groups per block, 2900 the
+    level-split layout.  T1 on a subset against the oracle, and the full batch against single
+    launches (bit-identical)."""
     planets = (S2_PLANETS + EXTRA_PLANETS)[:3]
     np.random.seed(11)
     obs = O.fake_obs(planets, Npoints=40, error=1.5e-4, errorVar=2.5e-5, tmax=60.)
-    plan, dt = _plan(obs, planets, max_walkers=4160)
-    P = _ball(planets, 4160, seed=5)
+    plan, dt = _plan(obs, planets, max_walkers=W)
+    P = _ball(planets, W, seed=5)
     got, st, _ = _run(plan, P)
-    idx = np.r_[0:24, 2000:2024, 4136:4160]
+    idx = np.r_[0:24, 2000:2024, W - 24:W]
     ref, st_ref = O.logl_whx_batch(P[idx], 3, obs, dt, LEVELS)
     _assert_t1(got[idx], st[idx], ref, st_ref)
-    for i in (15, 16, 4159):
+    for i in (15, 16, W - 1):
         one, st1, _ = _run(plan, P[i:i + 1])
         assert one[0] == got[i] and st1[0] == st[i]
 
