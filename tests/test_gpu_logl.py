@@ -284,7 +284,7 @@ def test_large_batch_size_independent_results(W):
     plan, _ = _plan(obs, S2_PLANETS, max_walkers=W)
     P = _ball(S2_PLANETS, W, seed=21)
     big, st_big, rv_big = _run(plan, P, want_rv=True)
-    for i in (0, 1000, 4095, W - 1):
+    for i in (0, 32, 1000, 4095, W - 1):  # 0 and 32: walkers whose bits once depended on the layout
         one, st1, rv1 = _run(plan, P[i:i + 1], want_rv=True)
         assert one[0] == big[i] and st1[0] == st_big[i]
         np.testing.assert_array_equal(rv1[:, 0], rv_big[:, i])
