@@ -542,13 +542,17 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         // to arrive combines all levels (their RVs went to P.lv_rv at every epoch)
         if (pl_idx == 0 && valid) P.lv_enc[(size_t)(d * nl + lvl) * P.lv_stride + w] = encflag;
         __threadfence();  // release this wave's RVs and flags (agent scope: the units span XCDs)
+        // the write-back must complete before the counter add (MI355X_MICROARCH.md, compiler
+        // hazard: the wait after buffer_wbl2 can be dropped; inline asm is invisible to that pass)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int arrived = 0;
         const int unit = unit_of();
         if (lane == 0) arrived = atomicAdd(P.lv_cnt + unit, 1);
         arrived = __builtin_amdgcn_readfirstlane(arrived);
         if (arrived != nl - 1) return;
         if (lane == 0) P.lv_cnt[unit] = 0;  // all nl arrived: ready for the next launch
-        __threadfence();  // acquire the other levels' stores
+        __threadfence();  // acquire the other levels' stores (invalidates this CU's L1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (pl_idx == 0 && valid) {
             int enc = 0;
             for (int k = 0; k < nl; k++) enc |= __builtin_nontemporal_load(P.lv_enc + (size_t)(d * nl + k) * P.lv_stride + w);
