@@ -81,7 +81,10 @@ typedef struct rvm_plan rvm_plan;
 
 /* Build the epoch schedule for one observation set (host arrays, n_obs epochs in any order and
  * sign; t = 0 is the initial condition).  Allocates device memory and workspace for up to
- * max_walkers walkers per launch.  observations.py:6-69 (tf/tb/rvf/rvb/errorf/errorb). */
+ * max_walkers walkers per launch -- with four increasing levels and max_walkers large enough for
+ * the level-split launch layout (more walker groups than half the CUs) also its hand-off
+ * workspace, 64 * max(epochs per direction) * max_walkers bytes.
+ * observations.py:6-69 (tf/tb/rvf/rvb/errorf/errorb). */
 int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, const double* sigma, int32_t n_obs,
                     int32_t max_walkers, rvm_plan** out);
 void rvm_plan_destroy(rvm_plan* plan);
