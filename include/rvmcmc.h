@@ -29,6 +29,10 @@
  *     stream-ordered on `stream` (a hipStream_t; NULL = the null stream), so they are capturable
  *     into a hipGraph.  rvm_plan_create is the only call that allocates (device buffers owned by
  *     the plan) and it synchronises once.
+ *   - A plan is single-stream: it owns per-launch workspace (the direction-exchange slots and the
+ *     level-split hand-off buffers and arrival counters), so launches that use one plan must be
+ *     serialised on one stream at a time.  Concurrent launches on two streams need two plans (the
+ *     Python layer keys its plan cache by stream, rvmcmc/engine.py).
  *   - Walker parameters are SoA, [n_params][n_walkers] float64, n_params = 5*n_planets with the
  *     canonical per-planet key order  m, a, h, k, l  (the Python layer maps a
  *     State's dict order onto it), or 7*n_planets (m, a, h, k, l, ix, iy) for inclined plans.

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -230,13 +231,19 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const int64_t groups = ((int64_t)max_walkers + wpb - 1) / wpb;
         bool inc = cfg->n_levels == 4;
         for (int k = 1; inc && k < 4; k++) inc = mult[k] > mult[k - 1];
+        // RVM_NO_LEVEL_SPLIT=1 forces the LDS-coupled layout (tests: the no-workspace fallback)
+        const char* nols = getenv("RVM_NO_LEVEL_SPLIT");
+        if (nols && nols[0] == '1') inc = false;
         if (inc && P.n_cu > 0 && 2 * groups > P.n_cu) {
             const int64_t emax = (int64_t)(nf > nb ? nf : nb) > 0 ? (int64_t)(nf > nb ? nf : nb) : 1;
             const int64_t units = 2 * groups + 8;
             const size_t b_rv = (size_t)(2 * 4 * emax * max_walkers) * sizeof(double);
             const size_t b_enc = (size_t)(2 * 4 * (int64_t)max_walkers) * sizeof(int32_t);
             const size_t b_cnt = (size_t)units * sizeof(int32_t);
-            if (hipMalloc(&plan->lvmem, b_rv + b_enc + b_cnt) == hipSuccess) {
+            if (hipMalloc(&plan->lvmem, b_rv + b_enc + b_cnt) != hipSuccess) {
+                plan->lvmem = nullptr;
+                (void)hipGetLastError();  // the fallback is not an error: clear the runtime's sticky status
+            } else {
                 unsigned char* base = reinterpret_cast<unsigned char*>(plan->lvmem);
                 P.lv_rv = reinterpret_cast<double*>(base);
                 P.lv_enc = reinterpret_cast<int32_t*>(base + b_rv);
@@ -249,6 +256,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
                     P.lv_rv = nullptr;
                     P.lv_enc = nullptr;
                     P.lv_cnt = nullptr;
+                    (void)hipGetLastError();
                 }
             }
             // (no workspace: launches keep the LDS-coupled layout)

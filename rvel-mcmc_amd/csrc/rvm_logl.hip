@@ -256,10 +256,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const bool stretch = sa.c != nullptr;
     double zst = 0.0, zp = 0.0;
     int jst = 0, jp = 0, kind = 0, wk = wl;
-    const bool stager = !dec && stretch && lvl == 0 && pl_idx == 0 && kind == 0;  // one lane per walker stages
+    // slot kind (speculative iteration, StretchArgs): see stretch_slot
+    if (stretch) stretch_slot(sa, wl, kind, wk, zst, jst, zp, jp);
+    // one lane per walker stages the accept inputs; only kind-0 slots accept in this launch, and
+    // sa.lnp holds just their n_spec (or W) entries -- half 1's slots must not read it
+    const bool stager = !dec && stretch && lvl == 0 && pl_idx == 0 && kind == 0;
     if (stretch) {
-        // slot kind (speculative iteration, StretchArgs): see stretch_slot
-        stretch_slot(sa, wl, kind, wk, zst, jst, zp, jp);
         if (stager) {
             constexpr int R = PR * NP;
             l_q[R * GW + gi] = zst;
@@ -600,8 +602,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 asm volatile("" : "+v"(wo));
                 stretch_slot(sa, wo, k2, wk2, z2, j2, zp2, jp2);
                 auto row = [&](int r) { return walker_param(true, params, W, wk2, sa, r, z2, j2, k2, zp2, jp2); };
+                // (lnp0 exists for the accepting kind-0 slots only: sa.lnp is n_spec long)
                 finish(w, chi2w, enc, row, z2, stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half),
-                       sa.lnp[wo]);
+                       k2 == 0 ? sa.lnp[wo] : 0.0);
             } else {
                 auto row = [&](int) { return 0.0; };
                 finish(w, chi2w, enc, row, 0.0, 0.0, 0.0);

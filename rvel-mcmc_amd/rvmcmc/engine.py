@@ -320,11 +320,14 @@ PLAN_CACHE_SIZE = 32  # plans kept per observation set
 
 
 def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0.0, inclined=False) -> LoglPlan:
-    """Cached LoglPlan on an Observation object (keyed by device and integrator settings)."""
-    dev = _torch().device(device) if device is not None else default_device()
+    """Cached LoglPlan on an Observation object (keyed by device, the caller's current stream and
+    the integrator settings: a plan's workspace is single-stream, include/rvmcmc.h)."""
+    torch = _torch()
+    dev = torch.device(device) if device is not None else default_device()
     cache = obs.__dict__.setdefault("_rvm_plans", {})
     mult = level_multipliers(levels)
-    key = (str(dev), int(n_planets), float(dt), mult, float(period_hint), bool(inclined))
+    stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
+    key = (str(dev), int(stream), int(n_planets), float(dt), mult, float(period_hint), bool(inclined))
     plan = cache.pop(key, None)
     if plan is None or plan.max_walkers < max_walkers:
         t, rv, er = obs_arrays(obs)

@@ -30,7 +30,12 @@ for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=T
 per = {}
 for k, v in vals.items():
     per[k] = v
-out = {"walkers_per_launch": W, "kernel": "rvm::logl_kernel<2>", "launch": what}
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_signature  # noqa: E402
+
+# keyed to the kernel sources it was measured on: bench.py refuses a summary of another kernel
+out = {"walkers_per_launch": W, "kernel": "rvm::logl_kernel<2>", "launch": what,
+       "kernel_signature": kernel_signature()}
 def mean(k):
     v = per.get(k)
     return sum(v) / len(v) if v else None
