@@ -1,0 +1,268 @@
+"""Sampler decisions on the device vs the same samplers driven by the IAS15 oracle.
+
+The reference evaluates every proposal with REBOUND's IAS15 (state.py:36-110); the kernel
+integrates Wisdom-Holman + Richardson.  Each test runs the PRODUCTION device path (Philox draws,
+speculative stretch iterations on the bench shape), reconstructs the draws with
+tests/philox_ref.py (or injects them), restates the reference sampler step in numpy with the IAS15
+restatement as the likelihood, and compares every accept/reject decision
+(tests/ias15_parity.py: near-margin walkers and status disagreements are exempt and counted;
+everything else must be identical).  Each test prints one JSON line with the counts (and appends
+it to $RVM_PARITY_REPORT when set; profiles/ keeps the round's report).
+
+Cases: the bench config (2-planet synthetic, 4096 walkers, tight ball), a wide ball with prior
+rejections and encounters, HD155358 (real data, `sol` of (Ex)HD155358.ipynb:64-66), 3 planets
+(config 5's system), batched MH chains (mcmc.py:107-121) on S2 and HD155358, and one SMALA step
+(mcmc.py:167-187; likelihood terms from IAS15, proposal-density terms from the device metric,
+which test_gpu_derivs.py pins against IAS15 differences).
+"""
+import numpy as np
+import pytest
+
+import ias15_parity as IP
+import oracle as O
+from conftest import S2_PLANETS, S2_SCALES, s2_obs_oracle
+from philox_ref import stretch_uniforms
+
+pytestmark = pytest.mark.gpu
+
+T2_ABS = 5e-8  # tests/test_gpu_logl.py: kernel vs IAS15 at the default integrator settings
+THIRD = {"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}  # scripts/configs_bench.py config 5
+HD_SOL = [6.57730330e-01, -9.72263877e-02, -7.82798396e-02, 8.84031737e-04, 4.42804990e+00,
+          1.04404207e+00, -2.05622789e-02, -1.08797961e-01, 8.30379710e-04, 1.49919861e+00]
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _hd():
+    import os
+
+    from conftest import GOLDEN
+
+    planets = [{"m": HD_SOL[3], "a": HD_SOL[0], "h": HD_SOL[1], "k": HD_SOL[2], "l": HD_SOL[4]},
+               {"m": HD_SOL[8], "a": HD_SOL[5], "h": HD_SOL[6], "k": HD_SOL[7], "l": HD_SOL[9]}]
+    return planets, O.obs_from_file(os.path.join(GOLDEN, "HD155358.vels"), Npoints=100)
+
+
+def _device_logl(ens_or_plan, pm, Q, hill):
+    """Kernel logL + status of proposals Q [n][dim] (plain launch; bit-identical to the fused and
+    speculative launches, test_gpu_samplers.py)."""
+    torch = _torch()
+    plan = ens_or_plan
+    X = torch.as_tensor(np.ascontiguousarray(Q.T), device="cuda")
+    lp, st, _ = plan.logl(pm.to_kernel(X), hill_factor=hill)
+    torch.cuda.synchronize()
+    return lp.cpu().numpy(), st.cpu().numpy()
+
+
+def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, explain=False, seed=2017, ball_seed=0):
+    """Run the device EnsembleSampler (default path) and compare its decisions, iteration by
+    iteration, with emcee 2.2.1 restated in numpy on IAS15 logL and the same Philox draws."""
+    torch = _torch()
+    from rvmcmc.ensemble import EnsembleSampler
+    from rvmcmc.state import State
+
+    s = State(planets=[dict(p) for p in planets])
+    pm = s.param_map()
+    dim = s.Nvars
+    scales = np.array([S2_SCALES[k] for k in s.get_rawkeys()])
+    rng = np.random.default_rng(ball_seed)
+    X0 = s.get_params()[None] + ball * scales * rng.standard_normal((W, dim))
+    ens = EnsembleSampler(W, s, obs, seed=seed)
+    ens.set_positions(X0)
+    ens.compute_lnprob()
+    for _ in range(warm):
+        ens.step()
+    torch.cuda.synchronize()
+    n, hk, hill, npl = ens.nloc, ens.halfk, ens.hill_factor, pm.n_planets
+    lnp_ref = [IP.ias15_logl(IP.to_oracle(pm, p.t().cpu().numpy()), npl, obs, hill)[0] for p in ens.pos]
+    tally = IP.Tally(name)
+    for _ in range(iterations):
+        it = ens.iteration
+        before = [p.t().cpu().numpy().copy() for p in ens.pos]
+        lnp_dev = [l.cpu().numpy().copy() for l in ens.lnp]
+        spec = ens.speculating()
+        ens.step()
+        torch.cuda.synchronize()
+        after = [p.t().cpu().numpy() for p in ens.pos]
+        for h in (0, 1):
+            c = before[1] if h == 0 else after[0]  # half 1 proposes against the updated half 0
+            u1, u2, u3 = stretch_uniforms(ens.seed, ens.global_begin(h), n, it, h)
+            q, z = IP.stretch_proposal(before[h], c, u1, u2, ens.a)
+            lq_ref, sq_ref = IP.ias15_logl(IP.to_oracle(pm, q), npl, obs, hill)
+            lq_dev, sq_dev = _device_logl(ens.plan, pm, q, hill)
+            with np.errstate(invalid="ignore"):
+                d_ref = (dim - 1.0) * np.log(z) + lq_ref - lnp_ref[h]
+                d_dev = (dim - 1.0) * np.log(z) + lq_dev - lnp_dev[h]
+                acc_ref = d_ref > np.log(u3)
+                margin = np.abs(d_ref - np.log(u3))
+                margin = np.where(np.isnan(margin), np.inf, margin)
+                expl = margin <= np.abs(d_dev - d_ref)
+            acc_dev = np.any(after[h] != before[h], axis=1)
+            # the device sampler itself is exact: its decisions follow its own logL bit for bit
+            np.testing.assert_array_equal(acc_dev, d_dev > np.log(u3))
+            np.testing.assert_array_equal(after[h][acc_dev], q[acc_dev])
+            tally.add(acc_dev, acc_ref, margin, sq_dev, sq_ref, lq_dev, lq_ref, idx_offset=h * hk,
+                      explained=expl if explain else None)
+            lnp_ref[h] = np.where(acc_dev, lq_ref, lnp_ref[h])  # follow the device chain
+    return tally, dict(walkers=W, ball=ball, iterations=iterations, warm_iterations=warm, speculative=bool(spec))
+
+
+def test_stretch_vs_ias15_bench_config():
+    """The bench workload itself: 2-planet synthetic, 101 epochs, 4096 walkers, tight ball,
+    speculative whole iterations (one 6144-slot launch)."""
+    tally, info = stretch_parity("stretch/bench-config S2 4096 walkers", S2_PLANETS, s2_obs_oracle(), 4096, 1e-3)
+    rep = tally.report(**info)
+    assert info["speculative"]
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["exempt_status_disagreement"] == 0
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
+    assert rep["decisions"] == 2 * 4096 and rep["accepted_ias15"] > 1000
+
+
+def test_stretch_vs_ias15_wide_ball_encounters():
+    """A wide initial ball (0.6 x the emcee scales): prior rejections and close-encounter exits
+    occur; walkers far from the plan's period basis leave the T2 regime (their logL is still
+    compared, and a flipped decision must be explained by the measured logL difference)."""
+    tally, info = stretch_parity("stretch/wide-ball S2 2048 walkers", S2_PLANETS, s2_obs_oracle(), 2048, 0.6,
+                                 warm=0, explain=True, ball_seed=3)
+    rep = tally.report(**info)
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["encounters_ias15"] > 20 and rep["prior_rejections"] > 20
+    assert rep["exempt_status_disagreement"] <= max(2, rep["decisions"] // 100)
+    assert rep["identical"] >= rep["decisions"] - rep["exempt_status_disagreement"] - rep["exempt_near_margin"] \
+        - rep["exempt_explained_by_dlogl"]
+
+
+def test_stretch_vs_ias15_hd155358():
+    planets, obs = _hd()
+    tally, info = stretch_parity("stretch/HD155358 512 walkers", planets, obs, 512, 1e-3)
+    rep = tally.report(**info)
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["exempt_status_disagreement"] == 0
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
+
+
+def test_stretch_vs_ias15_three_planets():
+    """Config 5's system (S2 + the named third planet), 1024 walkers."""
+    np.random.seed(2017)
+    planets = [dict(p) for p in S2_PLANETS] + [dict(THIRD)]
+    obs = O.fake_obs(planets, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    tally, info = stretch_parity("stretch/3-planet 1024 walkers", planets, obs, 1024, 1e-3)
+    rep = tally.report(**info)
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["exempt_status_disagreement"] == 0
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
+
+
+def mh_parity(name, planets, obs, chains, step, steps=3, seed=5):
+    """MhChains (batched mcmc.Mh) with injected N(0,1) and U(0,1) vs mcmc.py:107-121 on IAS15."""
+    torch = _torch()
+    from rvmcmc.mcmc import MhChains
+    from rvmcmc.state import State
+
+    s = State(planets=[dict(p) for p in planets])
+    scal = {"m": 1.e-3, "a": 0.3, "h": 0.5, "k": 0.5, "l": np.pi / 2.}  # mcmc_benchmark_mh.py:52
+    mh = MhChains(s, obs, scal, step, chains, seed=seed)
+    pm, dim, hill = mh.pmap, mh.dim, mh.state.hillRadiusFactor
+    sc = np.array([scal[k] for k in mh.state.get_rawkeys()])
+    X = mh.X.cpu().numpy().copy()  # [dim][C]
+    lnp_ref = IP.ias15_logl(IP.to_oracle(pm, X.T), pm.n_planets, obs, hill)[0]
+    rng = np.random.default_rng(seed)
+    tally = IP.Tally(name)
+    for _ in range(steps):
+        g = rng.standard_normal((dim, chains))
+        u = rng.random(chains)
+        lnp_dev = mh.lnp.cpu().numpy().copy()
+        mh.step(draws_propose=torch.as_tensor(g, device="cuda"), draws_accept=torch.as_tensor(u, device="cuda"))
+        torch.cuda.synchronize()
+        Q = X + (step * sc)[:, None] * g  # mcmc.py:89-93 (shift_params by step_size * scales * N(0,1))
+        got = mh.X.cpu().numpy()
+        np.testing.assert_array_equal(got[:, np.any(got != X, axis=0)], Q[:, np.any(got != X, axis=0)])
+        lq_ref, sq_ref = IP.ias15_logl(IP.to_oracle(pm, Q.T), pm.n_planets, obs, hill)
+        lq_dev, sq_dev = _device_logl(mh.plan, pm, Q.T, hill)
+        with np.errstate(invalid="ignore", over="ignore"):
+            # mcmc.py:112-121: priorHard / Encounter -> reject; accept if exp(lp* - lp) > U
+            acc_ref = (sq_ref == IP.ST_OK) & (np.exp(lq_ref - lnp_ref) > u)
+            margin = np.abs((lq_ref - lnp_ref) - np.log(u))
+            margin = np.where(np.isnan(margin), np.inf, margin)
+        acc_dev = np.any(got != X, axis=0)
+        with np.errstate(over="ignore", invalid="ignore"):
+            np.testing.assert_array_equal(acc_dev, np.exp(lq_dev - lnp_dev) > u)
+        tally.add(acc_dev, acc_ref, margin, sq_dev, sq_ref, lq_dev, lq_ref)
+        lnp_ref = np.where(acc_dev, lq_ref, lnp_ref)
+        X = got.copy()
+    return tally, dict(chains=chains, step_size=step, steps=steps)
+
+
+@pytest.mark.parametrize("case", ["S2", "HD155358"])
+def test_mh_vs_ias15(case):
+    if case == "S2":
+        planets, obs = S2_PLANETS, s2_obs_oracle()
+    else:
+        planets, obs = _hd()
+    tally, info = mh_parity(f"mh/{case} 512 chains", planets, obs, 512, 2e-3)
+    rep = tally.report(**info)
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["exempt_status_disagreement"] == 0
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
+    assert 0 < rep["accepted_ias15"] < rep["decisions"]
+
+
+def test_smala_step_vs_ias15():
+    """One batched SMALA step (mcmc.py:167-187) with injected z, u: the accept ratio's likelihood
+    terms from IAS15, its proposal-density terms from the device metric (exact derivatives, pinned
+    against IAS15 differences in test_gpu_derivs.py)."""
+    torch = _torch()
+    from rvmcmc.smala import SmalaChains
+    from rvmcmc.state import State
+
+    s = State(planets=[dict(p) for p in S2_PLANETS])
+    obs = s2_obs_oracle()
+    C_, dim, eps = 128, s.Nvars, 0.5
+    sm = SmalaChains(s, obs, eps=eps, alpha=1e3, n_chains=C_, seed=5, hessian="exact")
+    for _ in range(2):
+        sm.step()
+    pm, hill = sm.pmap, sm.state.hillRadiusFactor
+    rng = np.random.default_rng(6)
+    z = rng.standard_normal((C_, dim))
+    u = rng.random(C_)
+    x0 = sm.X.cpu().numpy().copy()
+    c0 = {k: v.cpu().numpy().copy() for k, v in sm.cache.items() if k != "_c"}
+    acc0 = sm.accepted.cpu().numpy().copy()
+    sm.step(z=torch.as_tensor(z, device="cuda"), u=torch.as_tensor(u, device="cuda"))
+    torch.cuda.synchronize()
+    xs = sm.Xs.cpu().numpy()
+    p = {k: v.cpu().numpy() for k, v in sm.prop.items() if k != "_c"}
+    acc_dev = (sm.accepted.cpu().numpy() - acc0) == 1
+    l0_ref, s0_ref = IP.ias15_logl(IP.to_oracle(pm, x0.T), pm.n_planets, obs, hill)
+    ls_ref, ss_ref = IP.ias15_logl(IP.to_oracle(pm, xs.T), pm.n_planets, obs, hill)
+    _, ss_dev, _ = sm.state.get_logp_batch(obs, torch.as_tensor(xs, device="cuda"), hill_factor=hill, pmap=pm)
+    ss_dev = ss_dev.cpu().numpy()
+    ls_dev = p["lp"]  # the proposal's logp as the device step used it (exact-derivative launch)
+
+    def logq(y, mu, G, logdet):
+        d = y - mu
+        return -0.5 * (d @ G @ d / eps ** 2 + dim * np.log(eps ** 2) + logdet + dim * np.log(2 * np.pi))
+
+    acc_ref = np.zeros(C_, bool)
+    margin = np.full(C_, np.inf)
+    for i in range(C_):
+        if not (c0["ok"][i] and p["ok"][i] and ss_ref[i] == 0):
+            continue
+        G0 = c0["G"][:, i].reshape(dim, dim)
+        Gp = p["G"][:, i].reshape(dim, dim)
+        lr = (ls_ref[i] - l0_ref[i] + logq(x0[:, i], p["mu"][:, i], Gp, p["logdet"][i])
+              - logq(xs[:, i], c0["mu"][:, i], G0, c0["logdet"][i]))
+        acc_ref[i] = np.exp(lr) > u[i]
+        margin[i] = abs(lr - np.log(u[i]))
+    tally = IP.Tally("smala/S2 128 chains exact metric")
+    tally.add(acc_dev, acc_ref, margin, ss_dev, ss_ref, ls_dev, ls_ref)
+    rep = tally.report(chains=C_, eps=eps, alpha=1e3)
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
+    assert 0 < rep["accepted_ias15"]
