@@ -2,9 +2,11 @@
 
 Tiers:
   T1  kernel vs oracle/rvoracle.c's restatement of the SAME algorithm (Richardson-extrapolated
-      Wisdom-Holman, identical schedule):  |dlogL| <= 1e-11 sum|w| max(1, |logL|), model RV within
-      1e-14 sum|w| absolute, identical status codes.  Chaotic walkers (wide ball) are compared within
-      their own roundoff sensitivity, measured on the oracle.
+      Wisdom-Holman, identical schedule):  |dlogL| / max(1, |logL|) <= 3x the oracle's own
+      roundoff sensitivity over the batch (its response to 1e-15 relative input nudges,
+      t1_tol_sens; measured kernel error 0.2-2.2x that sensitivity), model RV within 1e-14 sum|w|
+      absolute, identical status codes.  Chaotic walkers (wide ball) are compared within their
+      own per-walker sensitivity.
   T2  kernel vs the IAS15 restatement of the reference (reference-equivalent physics):
       |dlogL| <= 5e-8 absolute at the default integrator settings (SURVEY.md §8c allows 1e-6;
       measured 1.4e-9 S2, 1.9e-9 HD155358, 1.2e-8 on the short inclined set below); golden G2/G3.
@@ -24,6 +26,12 @@ pytestmark = pytest.mark.gpu
 # 6.2 at 4 levels, 26 at 6) and by the likelihood's conditioning (dlogL/drv ~ 2 sum|r|/(N sigma^2)
 # ~ 1e4).  Tolerance: 1e-11 * sum|w| * max(1, |logL|)  (measured max 4e-11 at 4 levels).
 T1_REL_PER_W = 1e-11
+# T1 as used by the batch comparisons below: 3x the oracle's own roundoff sensitivity over the
+# batch (t1_tol_sens).  SURVEY.md §8c's 1e-12 is below that sensitivity for these walkers (the
+# oracle itself moves by up to 7.5e-11 when an input changes by 1e-15 relative), so it cannot be
+# met by any second implementation; t1_tol (the Sigma|w| form above) remains for the sampler and
+# derivative tests that compare single values.
+T1_SENS_FACTOR = 3.0
 T2_ABS = 5e-8
 # default integrator (rvmcmc.engine.IntegratorConfig): level multipliers and base steps per orbit
 LEVELS = (4, 5, 6, 7)
@@ -78,11 +86,57 @@ def _run(plan, P, hill=1.0, want_rv=False):
     return lp.cpu().numpy(), st.cpu().numpy(), (rv.cpu().numpy() if rv is not None else None)
 
 
-def _assert_t1(got, st, ref, st_ref, nl=LEVELS):
+def _t1_report(err, tol, nl, sens=None):
+    """Append the measured T1 maximum of one comparison to $RVM_T1_REPORT (JSON lines)."""
+    path = os.environ.get("RVM_T1_REPORT")
+    if path:
+        import json
+
+        d = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0],
+             "max_rel_err": float(err.max(initial=0.0)), "tol": float(tol),
+             "levels": list(np.atleast_1d(nl).tolist()), "sum_abs_w": float(np.abs(O.richardson_weights(nl)).sum())}
+        if sens is not None and len(err):
+            r = err / np.maximum(sens, 1e-300)
+            d.update(max_sens=float(sens.max()), min_sens=float(sens.min()), max_err_over_sens=float(r.max()),
+                     p99_err_over_sens=float(np.percentile(r, 99)), max_err_where_sens_zero=float(err[sens == 0].max(initial=0)),
+                     max_err_over_max_sens_1e12=float((err / np.maximum(sens, 1e-12)).max()))
+        with open(path, "a") as f:
+            f.write(json.dumps(d) + "\n")
+
+
+NUDGES = [(0, 4, 1), (-1, 4, -1), (0, 1, 1), (-1, 1, -1), (0, 2, 1), (-1, 0, 1)]
+
+
+def oracle_sensitivity(P, n_planets, obs, dt, nl, hill=1.0, has_inc=0):
+    """Per-walker roundoff sensitivity of the oracle's logL: the largest relative response to a
+    1e-15 relative nudge of one input (l, a, h, m of the first / last planet).  The kernel and the
+    oracle round differently (FMA contraction, rcp/rsq Newton math, Stumpff evaluation), so their
+    difference is a roundoff path of the same size."""
+    ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, nl, hill, 1, has_inc)
+    sens = np.zeros(len(P))
+    for pl, par, sgn in NUDGES:
+        P2 = P.copy()
+        P2[:, pl, par] *= 1 + sgn * 1e-15
+        r2, s2 = O.logl_whx_batch(P2, n_planets, obs, dt, nl, hill, 1, has_inc)
+        both = (st_ref == 0) & (s2 == 0)
+        sens[both] = np.maximum(sens[both], np.abs(r2[both] - ref[both]) / np.maximum(1.0, np.abs(ref[both])))
+    return sens
+
+
+def t1_tol_sens(sens):
+    """T1 from the batch's own roundoff conditioning: T1_SENS_FACTOR x the oracle's largest
+    response to a 1-ulp-scale input nudge (floor 1e-13).  Measured (round 2, every T1 batch of
+    this file): max kernel error / max sensitivity = 0.2 ... 2.2."""
+    return T1_SENS_FACTOR * max(float(np.max(sens, initial=0.0)), 1e-13)
+
+
+def _assert_t1(got, st, ref, st_ref, nl=LEVELS, sens=None):
     np.testing.assert_array_equal(st, st_ref)
     ok = st == 0
     err = np.abs(got[ok] - ref[ok]) / np.maximum(1.0, np.abs(ref[ok]))
-    assert err.max(initial=0.0) <= t1_tol(nl), err.max()
+    tol = t1_tol(nl) if sens is None else t1_tol_sens(sens[ok])
+    _t1_report(err, tol, nl, None if sens is None else sens[ok])
+    assert err.max(initial=0.0) <= tol, (err.max(), tol)
     assert np.all(np.isneginf(got[~ok]))
 
 
@@ -93,7 +147,7 @@ def test_t1_s2_tight_ball(W):
     P = _ball(S2_PLANETS, W, seed=W)
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, LEVELS)
-    _assert_t1(got, st, ref, st_ref)
+    _assert_t1(got, st, ref, st_ref, sens=oracle_sensitivity(P, 2, obs, dt, LEVELS))
 
 
 def test_t1_wide_ball_statuses():
@@ -145,7 +199,7 @@ def test_t1_levels(nl, spo):
     P = _ball(S2_PLANETS, 96, seed=int(np.sum(nl)))
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, nl)
-    _assert_t1(got, st, ref, st_ref, nl)
+    _assert_t1(got, st, ref, st_ref, nl, sens=oracle_sensitivity(P, 2, obs, dt, nl))
 
 
 EXTRA_PLANETS = [{"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0},
@@ -161,7 +215,7 @@ def test_t1_planet_counts(n_planets):
     P = _ball(planets, 70, seed=n_planets)
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS)
-    _assert_t1(got, st, ref, st_ref)
+    _assert_t1(got, st, ref, st_ref, sens=oracle_sensitivity(P, n_planets, obs, dt, LEVELS))
 
 
 @pytest.mark.parametrize("n_planets,hill", [(3, 4.0), (4, 3.0)])
@@ -176,7 +230,7 @@ def test_t1_planet_counts_close_encounters(n_planets, hill):
     got, st, _ = _run(plan, P, hill=hill)
     ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS, hill_factor=hill)
     assert 0 < np.count_nonzero(st_ref == 2) < len(P)  # some walkers exit, not all
-    _assert_t1(got, st, ref, st_ref)
+    _assert_t1(got, st, ref, st_ref, sens=oracle_sensitivity(P, n_planets, obs, dt, LEVELS, hill))
 
 
 def test_t2_s2_vs_ias15():
@@ -229,7 +283,7 @@ def test_epoch_edge_cases():
     P = _ball(planets, 5, seed=9)
     got, st, rv = _run(plan, P, want_rv=True)
     ref, st_ref = O.logl_whx_batch(P, 2, o, dt, LEVELS)
-    _assert_t1(got, st, ref, st_ref)
+    _assert_t1(got, st, ref, st_ref, sens=oracle_sensitivity(P, 2, o, dt, LEVELS))
     assert np.all(rv[1] == rv[2]) and np.all(rv[0] == rv[4])
 
 
@@ -304,7 +358,7 @@ def test_two_group_blocks_vs_oracle_three_planets(W):
     got, st, _ = _run(plan, P)
     idx = np.r_[0:24, 2000:2024, W - 24:W]
     ref, st_ref = O.logl_whx_batch(P[idx], 3, obs, dt, LEVELS)
-    _assert_t1(got[idx], st[idx], ref, st_ref)
+    _assert_t1(got[idx], st[idx], ref, st_ref, sens=oracle_sensitivity(P[idx], 3, obs, dt, LEVELS))
     for i in (15, 16, W - 1):
         one, st1, _ = _run(plan, P[i:i + 1])
         assert one[0] == got[i] and st1[0] == st[i]
@@ -333,7 +387,7 @@ def test_t1_inclined_vs_oracle():
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, 2, obs, dt, LEVELS, has_inc=1)
     assert st[0] == 1
-    _assert_t1(got, st, ref, st_ref)
+    _assert_t1(got, st, ref, st_ref, sens=oracle_sensitivity(P, 2, obs, dt, LEVELS, has_inc=1))
 
 
 def test_t2_inclined_vs_ias15():
@@ -389,7 +443,7 @@ def test_t1_inclined_planet_counts(n_planets):
     P[:, :, 5:7] += 1e-3 * rng.standard_normal((64, n_planets, 2))
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, n_planets, obs, dt, LEVELS, has_inc=1)
-    _assert_t1(got, st, ref, st_ref)
+    _assert_t1(got, st, ref, st_ref, sens=oracle_sensitivity(P, n_planets, obs, dt, LEVELS, has_inc=1))
 
 
 def test_empty_observation_set_and_odd_batch_sizes():
@@ -432,4 +486,4 @@ def test_maximum_epochs_per_direction():
     P = _ball(S2_PLANETS, 3, seed=2)
     got, st, _ = _run(plan, P)
     ref, st_ref = O.logl_whx_batch(P, 2, o, dt, LEVELS)
-    _assert_t1(got, st, ref, st_ref)
+    _assert_t1(got, st, ref, st_ref, sens=oracle_sensitivity(P, 2, o, dt, LEVELS))
