@@ -269,7 +269,10 @@ struct Lane {
     double dmin2, idmin2;   // (hill_factor * max r_Hill)^2 and its reciprocal
     double kA, kB, kC;      // closed-form 2-planet kick coefficients of the own lane (kick2)
     double kAh, kBh, kCh;   // the same times the current step (lane_set_step)
-    double pair_s;          // kick2: -0.0 on planet 1's lane (pair 0-2), -1.0 on planet 2's (pair 1-2)
+    double pair_s;          // kickN (3 planets): -0.0 / -1.0 selects the lane's round-0 pair
+    double oA, oB;          // kick2: own pair vector o = oA r'_own + oB r'_other
+    double kP1, kP2, kP3, kP4;      // kick2: own/other coefficients of the own velocity update
+    double kP1h, kP2h, kP3h, kP4h;  // the same times the current step
     double kP[KickPairs<NP>::n];   // NP >= 3 (kickN): own-lane coefficient of every pair but (0,1)
     double kPh[KickPairs<NP>::n];  // the same times the current step
     int p;                  // own planet index (lane % L, clamped to NP-1)
@@ -285,6 +288,12 @@ __device__ __forceinline__ void lane_set_step(Lane<NP>& s, double h) {
     s.kAh = s.kA * h;
     s.kBh = s.kB * h;
     s.kCh = s.kC * h;
+    if constexpr (NP == 2) {
+        s.kP1h = s.kP1 * h;
+        s.kP2h = s.kP2 * h;
+        s.kP3h = s.kP3 * h;
+        s.kP4h = s.kP4 * h;
+    }
     if constexpr (NP >= 3) {
 #pragma unroll
         for (int k = 0; k < KickPairs<NP>::n; k++) s.kPh[k] = s.kP[k] * h;
@@ -304,6 +313,18 @@ __device__ __forceinline__ void lane_finish(Lane<NP>& s) {
         s.kB = p1 ? -s.m[1] : -q;
         s.kC = p1 ? s.m[1] : -q * s.m[0];
         s.pair_s = p1 ? -0.0 : -1.0;
+        // kick2 in own/other form: with c = m1/M1, x2 = r'_2 + c r'_1 and d12 = x2 - r'_1,
+        //   planet 1's lane (own = r'_1): x2 = c own + oth,  d12 = (c - 1) own + oth, own pair x2
+        //   planet 2's lane (own = r'_2): x2 = own + c oth,  d12 = own + (c - 1) oth, own pair d12
+        // so v += A r' + B x2 / r02^3 + C d12 / r12^3 = (A + P1 ic_own + P2 ic_oth) own
+        //                                              + (P3 ic_own + P4 ic_oth) oth
+        const double c = s.m[0] * s.iMi[1], c1 = c - 1.0;
+        s.oA = p1 ? c : 1.0;
+        s.oB = p1 ? 1.0 : c1;
+        s.kP1 = p1 ? s.kB * c : s.kC;
+        s.kP2 = p1 ? s.kC * c1 : s.kB;
+        s.kP3 = p1 ? s.kB : s.kC * c1;
+        s.kP4 = p1 ? s.kC : s.kB * c;
     } else {
         // kickN, 3 planets: round-0 pair of group lane q is (q >> 1, 2 + (q & 1)) in body indices:
         // -0.0 for the star pairs (0,2), (0,3), -1.0 for (1,2), (1,3)
@@ -719,42 +740,47 @@ __device__ __forceinline__ void kick_generic(Lane<NP>& s, double dt) {
 //   dv'_1 = dt m_2 (d12/r12^3 - d02/r02^3)
 //   dv'_2 = dt [ M_2 r'_2/|r'_2|^3 - (M_2/M_1)(d02/r02^3 + m_1 d12/r12^3) ]
 // with heliocentric x_1 = r'_1, x_2 = r'_2 + (m_1/M_1) r'_1, d02 = x_2, d12 = x_2 - x_1.  The
-// own |r'| (= star--planet-1 distance on planet 1's lane) is carried from the drift: 2 rsq per kick.
+// own |r'| (= star--planet-1 distance on planet 1's lane) is carried from the drift.
 //
-// The two pair distances are split over the walker's two lanes: planet 1's lane takes d02 = x2,
-// planet 2's lane d12 = x2 - x1 (the same expressions, so the same bits), one inverse cube each,
-// exchanged by DPP: one v_rsq_f64 per lane and kick instead of two.  The encounter bits of both
-// lanes count (kick_enc_mask: the logl epilogue ORs a walker's lane pair).
+// Own/other form (lane_finish): each lane reads only the OTHER planet's Jacobi position and
+// the other pair's inverse cube from its partner lane (one DPP swap per 32-bit half: 6 moves per
+// kick instead of 12), forms its own pair vector o = oA own + oB oth (planet 1's lane: d02,
+// planet 2's lane: d12; one v_rsq_f64 per lane and kick), and updates its velocity as
+// v += (A + P1 ic_own + P2 ic_oth) own + (P3 ic_own + P4 ic_oth) oth (32 VALU per kick, was 40).
+// The encounter bits of both lanes count (kick_enc_bits: the logl epilogue ORs a walker's pair).
+template <int L>
+__device__ __forceinline__ double pair_swap(double v) {
+    static_assert(L == 2, "pair_swap exchanges the two lanes of a 2-planet walker");
+    constexpr int ctrl = 1 | (0 << 2) | (3 << 4) | (2 << 6);  // quad_perm [1, 0, 3, 2]
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
 template <int L, bool D3 = false>
 __device__ __forceinline__ void kick2(Lane<2>& s, double c1875 = 1.875) {
     static_assert(L == 2, "kick2 pairs the two planets' lanes");
-    const double x1 = grp_get<L, 0>(s.rx), y1 = grp_get<L, 0>(s.ry);
-    const double R2x = grp_get<L, 1>(s.rx), R2y = grp_get<L, 1>(s.ry);
-    const double c = s.m[0] * s.iMi[1];  // m_1 / M_1
-    const double x2 = fma(c, x1, R2x), y2 = fma(c, y1, R2y);
-    const double dx12 = x2 - x1, dy12 = y2 - y1;
-    // own pair: fma(-0, x1, x2) = x2 on planet 1's lane, fma(-1, x1, x2) = x2 - x1 on planet 2's
-    const double ox = fma(s.pair_s, x1, x2), oy = fma(s.pair_s, y1, y2);
+    const double ox_ = pair_swap<L>(s.rx), oy_ = pair_swap<L>(s.ry);  // the other planet's r'
+    const double ox = fma(s.oA, s.rx, s.oB * ox_), oy = fma(s.oA, s.ry, s.oB * oy_);
     double rsq = fma(ox, ox, oy * oy);
-    double z2 = 0.0, dz12 = 0.0;
+    double oz_ = 0.0;
     if constexpr (D3) {
-        const double z1 = grp_get<L, 0>(s.rz), R2z = grp_get<L, 1>(s.rz);
-        z2 = fma(c, z1, R2z);
-        dz12 = z2 - z1;
-        const double oz = fma(s.pair_s, z1, z2);
+        oz_ = pair_swap<L>(s.rz);
+        const double oz = fma(s.oA, s.rz, s.oB * oz_);
         rsq = fma(oz, oz, rsq);
     }
     // own pair on every lane; star--planet-1 from |r'_1| on planet 1's lanes only (|r'_2| is a
     // Jacobi distance, not a pair)
-    s.encm |= ballot(rsq < s.dmin2) | (ballot(s.ir * s.ir > s.idmin2) & 0x5555555555555555ull);
+    const double ir2 = s.ir * s.ir;
+    s.encm |= ballot(rsq < s.dmin2) | (ballot(ir2 > s.idmin2) & 0x5555555555555555ull);
     const double ic = rcube_nr(rsq, c1875);
-    const double i02c = grp_get<L, 0>(ic), i12c = grp_get<L, 1>(ic);
-    // coefficients carry the step (lane_set_step): v += A r' + B x2/r02^3 + C d12/r12^3
-    const double A = s.kAh * (s.ir * (s.ir * s.ir));
-    const double bx = s.kBh * i02c, cx = s.kCh * i12c;
-    s.vx = fma(A, s.rx, fma(bx, x2, fma(cx, dx12, s.vx)));
-    s.vy = fma(A, s.ry, fma(bx, y2, fma(cx, dy12, s.vy)));
-    if constexpr (D3) s.vz = fma(A, s.rz, fma(bx, z2, fma(cx, dz12, s.vz)));
+    const double ico = pair_swap<L>(ic);
+    const double A = s.kAh * (s.ir * ir2);
+    const double al = fma(s.kP2h, ico, fma(s.kP1h, ic, A));
+    const double be = fma(s.kP4h, ico, s.kP3h * ic);
+    s.vx = fma(al, s.rx, fma(be, ox_, s.vx));
+    s.vy = fma(al, s.ry, fma(be, oy_, s.vy));
+    if constexpr (D3) s.vz = fma(al, s.rz, fma(be, oz_, s.vz));
 }
 
 // Closed-form kick for NP >= 3 planets (the same interaction as kick_generic): every lane of

@@ -40,7 +40,7 @@ namespace rvm {
 // Timing build (make profile -> scripts/probe/librvmcmc_prof.so): per wave, s_memtime at kernel
 // start, after the prologue, accumulated inside segments, accumulated in epoch handling (incl.
 // the barrier), and at the end.  Read with rvm_prof_copy (scripts/probe/prof_kernel.py).
-#define RVM_PROF_SLOTS 11
+#define RVM_PROF_SLOTS 14
 #define RVM_PROF_MAX_WAVES 4096
 __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 #define PROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -183,9 +183,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     int grp, lvl, G, d, w0;
     bool idle = false;
     // (recomputed where needed, not kept live through the integration)
-    auto unit_of = [&]() { return (int)blockIdx.x < nA ? 2 * (int)blockIdx.x + (wv & 1) : 8 * ((int)blockIdx.x - nA) + wv; };
+    // the type-B blocks (level 1 of eight units, every SIMD critical) are dispatched first: the
+    // last blocks of a grid start several us after the first (measured: 450 -> 439 us per
+    // 6144-walker launch, scripts/probe/handoff_ab.sh)
+    const int nB = (int)gridDim.x - nA;
+    const int bid = (int)blockIdx.x < nB ? nA + (int)blockIdx.x : (int)blockIdx.x - nB;
+    auto unit_of = [&]() { return bid < nA ? 2 * bid + (wv & 1) : 8 * (bid - nA) + wv; };
     if (dec) {
-        const int b = blockIdx.x;
+        const int b = bid;
         const int unit = __builtin_amdgcn_readfirstlane(unit_of());  // wave-uniform (SGPRs)
         lvl = __builtin_amdgcn_readfirstlane(b < nA ? (wv < 2 ? 3 : (wv < 4 ? 2 : 0)) : 1);
         idle = b < nA && (wv == 4 || wv == 5);
@@ -456,7 +461,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
         if (dec) {
+#ifndef RVM_EXP_NO_HANDOFF_WRITES  // experiment builds only (scripts/probe): hand-off cost
             if (pl_idx == 0 && valid) *rvp = v0;
+#endif
             rvp += rv_stride;
         } else {
             if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
@@ -542,6 +549,29 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     } else {
         // level-split: publish this level's flags, count the unit's arrivals; the last level wave
         // to arrive combines all levels (their RVs went to P.lv_rv at every epoch)
+#ifdef RVM_PROFILE
+        const unsigned long long rt_integ = __builtin_amdgcn_s_memrealtime();
+        auto prof_dec = [&](unsigned long long rt_arr, int arr) {
+            const int gw = (int)blockIdx.x * (blockDim.x >> 6) + wv;
+            if (lane == 0 && gw < RVM_PROF_MAX_WAVES) {
+                unsigned long long* o = rvm_prof + (size_t)gw * RVM_PROF_SLOTS;
+                o[0] = t_start;
+                o[1] = t_pro;
+                o[2] = t_seg;
+                o[3] = t_epo;
+                o[4] = __builtin_readcyclecounter();
+                o[5] = rt_start;
+                o[6] = __builtin_amdgcn_s_memrealtime();
+                o[7] = (unsigned long long)lvl | ((unsigned long long)d << 8) | ((unsigned long long)mult << 16);
+                o[8] = (unsigned long long)redo;
+                o[9] = (unsigned long long)E;
+                o[10] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+                o[11] = rt_integ;
+                o[12] = rt_arr;
+                o[13] = (unsigned long long)arr | ((unsigned long long)unit_of() << 8);
+            }
+        };
+#endif
         if (pl_idx == 0 && valid) P.lv_enc[(size_t)(d * nl + lvl) * P.lv_stride + w] = encflag;
         __threadfence();  // release this wave's RVs and flags (agent scope: the units span XCDs)
         // the write-back must complete before the counter add (MI355X_MICROARCH.md, compiler
@@ -551,50 +581,77 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const int unit = unit_of();
         if (lane == 0) arrived = atomicAdd(P.lv_cnt + unit, 1);
         arrived = __builtin_amdgcn_readfirstlane(arrived);
+#ifdef RVM_PROFILE
+        const unsigned long long rt_arr = __builtin_amdgcn_s_memrealtime();
+        if (arrived != nl - 1) {
+            prof_dec(rt_arr, arrived);
+            return;
+        }
+#endif
         if (arrived != nl - 1) return;
         if (lane == 0) P.lv_cnt[unit] = 0;  // all nl arrived: ready for the next launch
+#ifdef RVM_EXP_NO_COMBINE  // experiment builds only (scripts/probe): hand-off cost
+        return;
+#endif
         __threadfence();  // acquire the other levels' stores (invalidates this CU's L1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (pl_idx == 0 && valid) {
+        if (valid) {  // both lanes of the walker's pair take part in the loads
             int enc = 0;
-            for (int k = 0; k < nl; k++) enc |= __builtin_nontemporal_load(P.lv_enc + (size_t)(d * nl + k) * P.lv_stride + w);
-            // (nl = 4 here) epochs in chunks of CH, software-pipelined: the next chunk's 4 CH loads
-            // are in flight while this chunk is combined (the other levels' values come from other
-            // XCDs' stores, an HBM round trip each)
-            constexpr int CH = 8;
+            if (pl_idx == 0)
+                for (int k = 0; k < nl; k++) enc |= __builtin_nontemporal_load(P.lv_enc + (size_t)(d * nl + k) * P.lv_stride + w);
+            // (nl = 4 here) epochs in chunks of CH, software-pipelined: the next chunk's loads are in
+            // flight while this chunk is combined (the other levels' values come from other XCDs'
+            // stores, an HBM round trip each).  Lane pl of the walker's pair loads and combines
+            // epochs [e0 + pl HC, e0 + (pl + 1) HC) of a chunk; the pair's first lane then sums the
+            // chi^2 terms in epoch order (same bits as the LDS-coupled path).
+            constexpr int NLP = L >= 2 ? 2 : 1;  // lanes sharing a walker's loads (one planet: one lane)
+            constexpr int CH = 16, HC = CH / NLP;
             const size_t ls = (size_t)P.lv_emax * P.lv_stride;
             const double* rvb = P.lv_rv + (size_t)(d * 4) * ls + w;
-            auto load_chunk = [&](int e0, double (&v)[CH][4]) {
+            const int eh = (pl_idx < NLP ? pl_idx : 0) * HC;
+            auto load_half = [&](int e0, double (&v)[HC][4]) {
 #pragma unroll
-                for (int i = 0; i < CH; i++) {
-                    const int e = e0 + i < E ? e0 + i : E - 1;
+                for (int i = 0; i < HC; i++) {
+                    const int e = e0 + eh + i < E ? e0 + eh + i : E - 1;
 #pragma unroll
                     for (int k = 0; k < 4; k++) v[i][k] = __builtin_nontemporal_load(rvb + k * ls + (size_t)e * P.lv_stride);
                 }
             };
             double chi2w = 0.0;
-            double va[CH][4], vb[CH][4];
-            if (E > 0) load_chunk(0, va);
+            double va[HC][4], vb[HC][4];
+            if (E > 0) load_half(0, va);
             for (int e0 = 0; e0 < E; e0 += CH) {
-                if (e0 + CH < E) load_chunk(e0 + CH, vb);
+                if (e0 + CH < E) load_half(e0 + CH, vb);
+                double term[HC];
 #pragma unroll
-                for (int i = 0; i < CH; i++) {
-                    const int e = e0 + i;
-                    if (e < E) {
-                        double rvx = 0.0;
+                for (int i = 0; i < HC; i++) {
+                    const int e = e0 + eh + i;
+                    const int ec = e < E ? e : E - 1;
+                    double rvx = 0.0;
 #pragma unroll
-                        for (int k = 0; k < 4; k++) rvx += P.lw[k] * va[i][k];
-                        const double r = rvx - l_rv[e];
-                        chi2w += (r * r) / l_s2[e];
-                        if (rv_out != nullptr) rv_out[(size_t)l_idx[e] * W + w] = rvx;
+                    for (int k = 0; k < 4; k++) rvx += P.lw[k] * va[i][k];
+                    const double r = rvx - l_rv[ec];
+                    term[i] = (r * r) / l_s2[ec];
+                    if (rv_out != nullptr && e < E && pl_idx < NLP) rv_out[(size_t)l_idx[e] * W + w] = rvx;
+                }
+#pragma unroll
+                for (int i = 0; i < HC; i++)
+                    if (e0 + i < E) chi2w += term[i];
+                if constexpr (NLP == 2) {
+#pragma unroll
+                    for (int i = 0; i < HC; i++) {
+                        const double t1 = grp_get<L, 1>(term[i]);
+                        if (e0 + HC + i < E) chi2w += t1;
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < CH; i++)
+                for (int i = 0; i < HC; i++)
 #pragma unroll
                     for (int k = 0; k < 4; k++) va[i][k] = vb[i][k];
             }
-            if (stretch) {
+            if (pl_idx != 0) {
+                // (the pair's second lane only helped with the loads)
+            } else if (stretch) {
                 // the slot's draws again (recomputed from an opaque index rather than kept live
                 // through the integration)
                 int wo = w, k2, wk2, j2, jp2;
@@ -610,6 +667,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 finish(w, chi2w, enc, row, 0.0, 0.0, 0.0);
             }
         }
+#ifdef RVM_PROFILE
+        prof_dec(rt_arr, nl - 1);
+        return;
+#endif
     }
 #ifdef RVM_PROFILE
     PROF_T(t_end);

@@ -125,9 +125,10 @@ def oracle_sensitivity(P, n_planets, obs, dt, nl, hill=1.0, has_inc=0):
 
 def t1_tol_sens(sens):
     """T1 from the batch's own roundoff conditioning: T1_SENS_FACTOR x the oracle's largest
-    response to a 1-ulp-scale input nudge (floor 1e-13).  Measured (round 2, every T1 batch of
-    this file): max kernel error / max sensitivity = 0.2 ... 2.2."""
-    return T1_SENS_FACTOR * max(float(np.max(sens, initial=0.0)), 1e-13)
+    response to a 1-ulp-scale input nudge, floored at SURVEY.md §8c's 1e-12 (a few-walker batch
+    samples the sensitivity poorly).  Measured (round 2, every T1 batch of this file): max kernel
+    error / max(sensitivity, 1e-12) = 0.2 ... 2.2."""
+    return T1_SENS_FACTOR * max(float(np.max(sens, initial=0.0)), 1e-12)
 
 
 def _assert_t1(got, st, ref, st_ref, nl=LEVELS, sens=None):
