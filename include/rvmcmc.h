@@ -15,7 +15,8 @@
  *     errorf,errorb,Npoints}
  *   mcmc.py:57-65 Ensemble.step -> emcee 2.2.1 stretch     rvm_stretch_propose / rvm_stretch_accept,
  *     move (EnsembleSampler._propose_stretch)                or fused: rvm_stretch_half_step
- *   mcmc.py:89-121 Mh.generate_proposal / Mh.step          rvm_mh_propose / rvm_mh_accept
+ *   mcmc.py:89-121 Mh.generate_proposal / Mh.step          rvm_mh_propose / rvm_mh_accept, or fused:
+ *                                                            rvm_mh_step
  *   state.py:218-294 get_chi2_d_dd / get_logp_d_dd         rvm_logl_derivs (exact gradient + Hessian,
  *     (REBOUND 1st/2nd-order variational equations)         hyper-dual forward mode)
  *   mcmc.py:144-187 Smala.generate_proposal/step           rvm_fd_params (finite-difference stencil)
@@ -51,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 7
+#define RVM_ABI_VERSION 8
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -185,6 +186,16 @@ int rvm_mh_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, cons
 int rvm_mh_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, double* lnp, const double* q,
                   const double* lnp_new, uint64_t seed, uint64_t iteration, const double* draws, int32_t* accepted,
                   void* stream);
+/* One whole MH step of n_chains chains (mcmc.py:107-121 for every chain) in ONE likelihood launch:
+ * the proposal (as rvm_mh_propose, Philox draws), the walker log-likelihood of map(q) (as
+ * rvm_logl_batch) and the accept (as rvm_mh_accept), bit-identical to the three-call sequence.
+ * x [n_params][n_chains] and lnp [n_chains] in place; scales [n_params]; n_chains <= the plan's
+ * max_walkers.  lnp_new_out / status_out (nullable): the proposals' logl and status; accepted
+ * (nullable): int32 counters += 1.  Prior / encounter proposals are rejected through -inf. */
+int rvm_mh_step(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_chains,
+                int64_t chain_begin, double* x, double* lnp, const double* scales, double step_size, uint64_t seed,
+                uint64_t iteration, double hill_factor, double* lnp_new_out, int32_t* status_out, int32_t* accepted,
+                void* stream);
 
 /* Central finite-difference stencil for SMALA's gradient/metric (x: [n_params][n_chains]).
  * out: SoA [n_params][(2P+1) * n_chains]; stencil point s of chain c is walker s*n_chains + c with
@@ -236,6 +247,31 @@ int rvm_smala_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, c
 int rvm_smala_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const rvm_smala_cache* cur,
                      const double* x_prop, const rvm_smala_cache* prop, double eps, uint64_t seed,
                      uint64_t iteration, const double* draws, int32_t* accepted, int32_t* failures, void* stream);
+
+/* Fused SMALA step, three launches instead of five (mcmc.py:167-187 for every chain):
+ *   rvm_smala_propose                       x* (unchanged)
+ *   rvm_smala_stencil_logl                  rvm_fd_params' stencil of x* formed inside ONE likelihood
+ *                                           launch (walker s * n_chains + c, as rvm_fd_params; map:
+ *                                           free parameters -> kernel rows, as rvm_stretch_half_step)
+ *                                           -> logl / status [(2P+1) C], rv_out [n_obs][(2P+1) C]
+ *   rvm_smala_derive_accept                 rvm_smala_derive of x* into prop, then rvm_smala_accept,
+ *                                           in one kernel (one wave per chain)
+ * bit-identical to rvm_fd_params + rvm_logl_batch + rvm_smala_derive + rvm_smala_accept.
+ * rvm_smala_metric_accept is the exact-Hessian counterpart (rvm_smala_metric + rvm_smala_accept). */
+int rvm_smala_stencil_logl(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_chains,
+                           const double* x, double rel_step, const double* floor_, double hill_factor,
+                           double* logl_out, int32_t* status_out, double* rv_out, void* stream);
+int rvm_smala_derive_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, int32_t n_obs, double* x,
+                            const double* x_prop, double rel_step, const double* floor_, const double* lp_stencil,
+                            const int32_t* status_stencil, const double* rv_stencil, const double* inv_sigma2,
+                            double npoints_norm, double alpha, double eps, const rvm_smala_cache* cur,
+                            const rvm_smala_cache* prop, uint64_t seed, uint64_t iteration, const double* draws,
+                            int32_t* accepted, int32_t* failures, void* stream);
+int rvm_smala_metric_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const double* x_prop,
+                            const double* lp, const int32_t* status, const double* grad, const double* hess,
+                            double alpha, double eps, const rvm_smala_cache* cur, const rvm_smala_cache* prop,
+                            uint64_t seed, uint64_t iteration, const double* draws, int32_t* accepted,
+                            int32_t* failures, void* stream);
 
 /* ---- exact derivatives (state.py:218-294) ----------------------------------------------------
  * logp, its gradient and its Hessian for n_chains parameter vectors (params: kernel rows

@@ -41,6 +41,16 @@ hipError_t launch_smala_propose(int P, int C, int64_t begin, const double* x, co
 hipError_t launch_smala_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
                                const SmalaCache& prop, double eps, uint64_t seed, uint64_t it, const double* draws,
                                int32_t* accepted, int32_t* failures, hipStream_t st);
+hipError_t launch_smala_derive_accept(int P, int C, int E, const double* xs, double rel, const double* fl,
+                                      const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
+                                      double npoints, double alpha, double eps, const SmalaCache& prop,
+                                      int64_t begin, double* x, const SmalaCache& cur, uint64_t seed, uint64_t it,
+                                      const double* draws, int32_t* accepted, int32_t* failures, hipStream_t st);
+hipError_t launch_smala_metric_accept(int P, int C, const double* xs, const double* lp, const int32_t* status,
+                                      const double* grad, const double* hess, double alpha, double eps,
+                                      const SmalaCache& prop, int64_t begin, double* x, const SmalaCache& cur,
+                                      uint64_t seed, uint64_t it, const double* draws, int32_t* accepted,
+                                      int32_t* failures, hipStream_t st);
 hipError_t launch_derivs(const DevPlan& P, int C, const double* params, int n_dirs, const int32_t* dir_rows,
                          double hill_factor, double* ws, int32_t* wst, double* logl, double* grad, double* hess,
                          int32_t* status, hipStream_t stream);
@@ -465,6 +475,69 @@ int rvm_mh_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, doubl
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_mh_accept");
 }
 
+int rvm_mh_step(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_chains,
+                int64_t chain_begin, double* x, double* lnp, const double* scales, double step_size, uint64_t seed,
+                uint64_t iteration, double hill_factor, double* lnp_new_out, int32_t* status_out, int32_t* accepted,
+                void* stream) {
+    if (!plan || !map) return fail(-1, "rvm_mh_step: null plan or map");
+    if (n_chains == 0) return 0;
+    if (n_chains < 0 || n_chains > plan->max_walkers)
+        return fail(-1, "rvm_mh_step: n_chains exceeds the plan's max_walkers");
+    if (n_params < 1 || !x || !lnp || !scales) return fail(-1, "rvm_mh_step: bad arguments");
+    if (!(hill_factor >= 0.0)) return fail(-1, "rvm_mh_step: hill_factor must be >= 0");
+    const int rows = (plan->dev.inclined ? 7 : 5) * plan->dev.n_planets;
+    if (map->n_rows != rows) return fail(-1, "rvm_mh_step: map rows do not match the plan");
+    rvm::StretchArgs sa{};
+    sa.x = x;
+    sa.lnp = lnp;
+    sa.accepted = accepted;
+    sa.s0_begin = chain_begin;
+    sa.seed = seed;
+    sa.iteration = iteration;
+    sa.dim = n_params;
+    sa.xstride = n_chains;
+    sa.mh_scale = scales;
+    sa.mh_step = step_size;
+    for (int r = 0; r < RVM_MAX_PARAM_ROWS; r++) {
+        const int k = r < rows ? map->src[r] : -1;
+        if (k >= n_params) return fail(-1, "rvm_mh_step: map source index out of range");
+        sa.src[r] = k < 0 ? -1 : k;
+        sa.base[r] = r < rows ? map->base[r] : 0.0;
+    }
+    hipError_t e = rvm::launch_logl(plan->dev, n_chains, nullptr, hill_factor, plan->slots, lnp_new_out, status_out,
+                                    nullptr, sa, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_mh_step");
+}
+
+int rvm_smala_stencil_logl(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_chains,
+                           const double* x, double rel_step, const double* floor_, double hill_factor,
+                           double* logl_out, int32_t* status_out, double* rv_out, void* stream) {
+    if (!plan || !map) return fail(-1, "rvm_smala_stencil_logl: null plan or map");
+    if (n_chains == 0) return 0;
+    const int64_t W = (int64_t)(2 * n_params + 1) * n_chains;
+    if (n_params < 1 || n_chains < 0 || !x || !floor_ || !logl_out || !status_out || !(rel_step > 0.0))
+        return fail(-1, "rvm_smala_stencil_logl: bad arguments");
+    if (W > plan->max_walkers) return fail(-1, "rvm_smala_stencil_logl: (2 n_params + 1) n_chains exceeds max_walkers");
+    if (!(hill_factor >= 0.0)) return fail(-1, "rvm_smala_stencil_logl: hill_factor must be >= 0");
+    const int rows = (plan->dev.inclined ? 7 : 5) * plan->dev.n_planets;
+    if (map->n_rows != rows) return fail(-1, "rvm_smala_stencil_logl: map rows do not match the plan");
+    rvm::StretchArgs sa{};
+    sa.dim = n_params;
+    sa.fd_x = x;
+    sa.fd_floor = floor_;
+    sa.fd_rel = rel_step;
+    sa.fd_n = n_chains;
+    for (int r = 0; r < RVM_MAX_PARAM_ROWS; r++) {
+        const int k = r < rows ? map->src[r] : -1;
+        if (k >= n_params) return fail(-1, "rvm_smala_stencil_logl: map source index out of range");
+        sa.src[r] = k < 0 ? -1 : k;
+        sa.base[r] = r < rows ? map->base[r] : 0.0;
+    }
+    hipError_t e = rvm::launch_logl(plan->dev, (int)W, nullptr, hill_factor, plan->slots, logl_out, status_out, rv_out,
+                                    sa, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_stencil_logl");
+}
+
 int rvm_fd_params(int32_t n_params, int32_t n_chains, const double* x, double rel_step, const double* floor_,
                   double* out, void* stream) {
     if (n_chains == 0) return 0;
@@ -537,6 +610,39 @@ int rvm_smala_metric(int32_t n_params, int32_t n_chains, const double* x, const 
     hipError_t e = rvm::launch_smala_metric(n_params, n_chains, x, lp, status, grad, hess, alpha, eps, smala_cache(out),
                                             (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_metric");
+}
+
+int rvm_smala_derive_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, int32_t n_obs, double* x,
+                            const double* x_prop, double rel_step, const double* floor_, const double* lp_stencil,
+                            const int32_t* status_stencil, const double* rv_stencil, const double* inv_sigma2,
+                            double npoints_norm, double alpha, double eps, const rvm_smala_cache* cur,
+                            const rvm_smala_cache* prop, uint64_t seed, uint64_t iteration, const double* draws,
+                            int32_t* accepted, int32_t* failures, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || n_obs < 0 || !x || !x_prop || !floor_ ||
+        !lp_stencil || !status_stencil || (n_obs > 0 && (!rv_stencil || !inv_sigma2)) || !smala_cache_ok(cur) ||
+        !smala_cache_ok(prop) || !(rel_step > 0.0) || !(npoints_norm != 0.0) || !(alpha > 0.0))
+        return fail(-1, "rvm_smala_derive_accept: bad arguments");
+    hipError_t e = rvm::launch_smala_derive_accept(n_params, n_chains, n_obs, x_prop, rel_step, floor_, lp_stencil,
+                                                   status_stencil, rv_stencil, inv_sigma2, npoints_norm, alpha, eps,
+                                                   smala_cache(prop), chain_begin, x, smala_cache(cur), seed,
+                                                   iteration, draws, accepted, failures, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_derive_accept");
+}
+
+int rvm_smala_metric_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const double* x_prop,
+                            const double* lp, const int32_t* status, const double* grad, const double* hess,
+                            double alpha, double eps, const rvm_smala_cache* cur, const rvm_smala_cache* prop,
+                            uint64_t seed, uint64_t iteration, const double* draws, int32_t* accepted,
+                            int32_t* failures, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || !x || !x_prop || !lp || !status || !grad ||
+        !hess || !smala_cache_ok(cur) || !smala_cache_ok(prop) || !(alpha > 0.0))
+        return fail(-1, "rvm_smala_metric_accept: bad arguments");
+    hipError_t e = rvm::launch_smala_metric_accept(n_params, n_chains, x_prop, lp, status, grad, hess, alpha, eps,
+                                                   smala_cache(prop), chain_begin, x, smala_cache(cur), seed,
+                                                   iteration, draws, accepted, failures, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_metric_accept");
 }
 
 int rvm_smala_propose(int32_t n_params, int32_t n_chains, int64_t chain_begin, const double* x,

@@ -38,8 +38,9 @@ struct DevPlan {
     DirSched fwd, bwd;
 };
 
-// Fused stretch half-step (rvm_stretch_half_step) by value as a kernel argument; c == nullptr
-// for a plain likelihood launch.
+// Fused sampler step by value as a kernel argument: a stretch half-step (rvm_stretch_half_step,
+// c != nullptr) or an MH step (rvm_mh_step, mh_scale != nullptr); both null for a plain
+// likelihood launch.
 //
 // Speculative whole iteration (rvm_stretch_iteration_begin, n_spec > 0): the launch has 3 n_spec
 // walker slots.  Slots [0, n) are half 0's walkers (proposal against c = half 1, accept at the
@@ -66,6 +67,18 @@ struct StretchArgs {
     const double* x1;   // half 1's free parameters [dim][n_spec]
     int64_t s1_begin;   // global index of half 1's walker 0 (Philox key)
     int32_t* dec;       // [n_spec] half 0's accept decisions (1 accepted)
+    // fused MH step (rvm_mh_step; c == nullptr, mh_scale != nullptr): walker w is chain w with
+    // free parameters x [dim][xstride], proposal q = x + mh_step * mh_scale[p] * N(0,1) formed in the
+    // prologue (Philox keyed by s0_begin + w), MH accept at the end against lnp
+    const double* mh_scale;  // [dim]
+    double mh_step;
+    // fused SMALA stencil (rvm_smala_stencil_logl; fd_x != nullptr, no accept in the launch):
+    // walker w = s * fd_n + c is point s of chain c's central-difference stencil around
+    // fd_x [dim][fd_n], formed as rvm_fd_params does (fd_point)
+    const double* fd_x;
+    const double* fd_floor;  // [dim]
+    double fd_rel;
+    int32_t fd_n;
     int32_t src[RVM_MAX_PARAM_ROWS];  // rvm_param_map
     double base[RVM_MAX_PARAM_ROWS];
 };

@@ -105,16 +105,20 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, double h, int ns, int& redo
     return false;
 }
 
-// kernel parameter row r of walker w: from the SoA input, or (fused stretch half-step) the row's
-// fixed value or the walker's proposal of the free parameter feeding it
+// kernel parameter row r of walker w: from the SoA input, or (fused sampler step) the row's fixed
+// value or the walker's proposal of the free parameter feeding it: MH (sa.mh_scale), or stretch
 // (kind 1 / 2: half 1's walker of a speculative iteration against its partner's rejected /
 // accepted position, StretchArgs)
-__device__ __forceinline__ double walker_param(bool stretch, const double* __restrict__ params, int W, int w,
+__device__ __forceinline__ double walker_param(bool mapped, const double* __restrict__ params, int W, int w,
                                                const StretchArgs& sa, int r, double z, int j, int kind, double zp,
                                                int jp) {
-    if (!stretch) return params[(size_t)r * W + w];
+    if (!mapped) return params[(size_t)r * W + w];
     const int k = sa.src[r];
     if (k < 0) return sa.base[r];
+    if (sa.fd_x) return fd_point(sa.fd_x, sa.fd_floor, sa.fd_rel, sa.fd_n, k, w);
+    if (sa.mh_scale)
+        return mh_q(sa.x[(size_t)k * sa.xstride + w], sa.mh_step, sa.mh_scale[k],
+                    mh_normal(sa.seed, (uint64_t)(sa.s0_begin + w), sa.iteration, k));
     if (kind == 0) return stretch_q(sa.c[(size_t)j * sa.dim + k], z, sa.x[(size_t)k * sa.xstride + w]);
     double c = sa.c0[(size_t)j * sa.dim + k];
     if (kind == 2) c = stretch_q(sa.c[(size_t)jp * sa.dim + k], zp, c);  // q0(j): bit-identical to slot j's
@@ -259,22 +263,24 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // q = c_j - z (c_j - x) mapped onto the kernel rows (rvm_stretch.h, rvm_param_map).
     constexpr int PR = D3 ? 7 : 5;  // parameter rows per planet
     const bool stretch = sa.c != nullptr;
+    const bool mh = sa.mh_scale != nullptr;  // fused MH step (rvm_mh_step)
+    const bool fused = stretch || mh;        // accepts at the end
+    const bool mapped = fused || sa.fd_x != nullptr;  // parameters formed from StretchArgs
     double zst = 0.0, zp = 0.0;
     int jst = 0, jp = 0, kind = 0, wk = wl;
     // slot kind (speculative iteration, StretchArgs): see stretch_slot
     if (stretch) stretch_slot(sa, wl, kind, wk, zst, jst, zp, jp);
     // one lane per walker stages the accept inputs; only kind-0 slots accept in this launch, and
     // sa.lnp holds just their n_spec (or W) entries -- half 1's slots must not read it
-    const bool stager = !dec && stretch && lvl == 0 && pl_idx == 0 && kind == 0;
-    if (stretch) {
-        if (stager) {
-            constexpr int R = PR * NP;
-            l_q[R * GW + gi] = zst;
-            l_q[(R + 1) * GW + gi] = stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wl), sa.iteration, sa.half);
-            l_q[(R + 2) * GW + gi] = sa.lnp[wl];
-        }
+    const bool stager = !dec && fused && lvl == 0 && pl_idx == 0 && kind == 0;
+    if (stager) {
+        constexpr int R = PR * NP;
+        l_q[R * GW + gi] = zst;
+        l_q[(R + 1) * GW + gi] = mh ? mh_u(sa.seed, (uint64_t)(sa.s0_begin + wl), sa.iteration)
+                                    : stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wl), sa.iteration, sa.half);
+        l_q[(R + 2) * GW + gi] = sa.lnp[wl];
     }
-#define prm(r) stage_row(stager, l_q, GW, gi, (r), walker_param(stretch, params, W, wk, sa, (r), zst, jst, kind, zp, jp))
+#define prm(r) stage_row(stager, l_q, GW, gi, (r), walker_param(mapped, params, W, wk, sa, (r), zst, jst, kind, zp, jp))
     Lane<NP> s;
     double pa[NP], ph[NP], pk[NP], pl[NP], pix[NP], piy[NP];
     int status = RVM_STATUS_OK;
@@ -511,10 +517,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const double lp = stw == RVM_STATUS_OK ? lp0 : -INFINITY;
         if (logl_out) logl_out[wo] = lp;
         if (status_out) status_out[wo] = stw;
-        if (stretch && (sa.n_spec == 0 || wo < sa.n_spec)) {
-            // emcee accept (half 1's slots of a speculative iteration only deliver their logl:
-            // rvm_stretch_iteration_end)
-            const bool acc = stretch_accepts(sa.dim, z, lp, lnp0, u3);
+        if (fused && (sa.n_spec == 0 || wo < sa.n_spec)) {
+            // emcee / MH accept (half 1's slots of a speculative iteration only deliver their
+            // logl: rvm_stretch_iteration_end)
+            const bool acc = mh ? mh_accepts(lp, lnp0, u3) : stretch_accepts(sa.dim, z, lp, lnp0, u3);
             if (acc) {
 #pragma unroll
                 for (int r = 0; r < R; r++) {
@@ -540,7 +546,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
                 const int gl = grp * WPB + lane;
                 auto row = [&](int r) { return l_q[r * GW + gl]; };
-                if (stretch)
+                if (fused)
                     finish(wo, chi2, enc, row, l_q[R * GW + gl], l_q[(R + 1) * GW + gl], l_q[(R + 2) * GW + gl]);
                 else
                     finish(wo, chi2, enc, row, 0.0, 0.0, 0.0);
@@ -662,6 +668,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 // (lnp0 exists for the accepting kind-0 slots only: sa.lnp is n_spec long)
                 finish(w, chi2w, enc, row, z2, stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half),
                        k2 == 0 ? sa.lnp[wo] : 0.0);
+            } else if (mh) {
+                auto row = [&](int r) { return walker_param(true, params, W, w, sa, r, 0.0, 0, 0, 0.0, 0); };
+                finish(w, chi2w, enc, row, 0.0, mh_u(sa.seed, (uint64_t)(sa.s0_begin + w), sa.iteration), sa.lnp[w]);
             } else {
                 auto row = [&](int) { return 0.0; };
                 finish(w, chi2w, enc, row, 0.0, 0.0, 0.0);
@@ -705,7 +714,8 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
     dim3 block(64 * P.n_levels * G);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t rows = (size_t)(P.inclined ? 7 : 5) * P.n_planets;
-    size_t smem = (size_t)emax * 4 * sizeof(double) + (sa.c ? (rows + 3) * G * wpb * sizeof(double) : 0);
+    const bool fused = sa.c != nullptr || sa.mh_scale != nullptr;
+    size_t smem = (size_t)emax * 4 * sizeof(double) + (fused ? (rows + 3) * G * wpb * sizeof(double) : 0);
     // level-split layout (logl_kernel) when it lowers the heaviest SIMD's load: in steps per base
     // step, max(m3, m2 + m0, 2 m1) for one round of <= n_cu blocks, against m3 per round of
     // single-group blocks or max_i(m_i + m_{n-1-i}) per round of two-group blocks

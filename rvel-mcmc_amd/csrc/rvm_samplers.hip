@@ -97,26 +97,14 @@ __global__ void stretch_iteration_end_kernel(const IterEndArgs g) {
     }
 }
 
-__device__ __forceinline__ double box_muller(double u0, double u1) {
-    return sqrt(-2.0 * log(u0)) * cospi(2.0 * u1);
-}
-
 __global__ void mh_propose_kernel(int P, int n, int64_t begin, const double* __restrict__ x,
                                   const double* __restrict__ scales, double step, uint64_t seed, uint64_t iteration,
                                   const double* __restrict__ draws, double* __restrict__ q) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     for (int p = 0; p < P; p++) {
-        double g;
-        if (draws) {
-            g = draws[(size_t)p * n + i];
-        } else {
-            double u0, u1;
-            uniform2(seed, (uint64_t)(begin + i), iteration, RNG_MH_PROPOSE | ((uint32_t)p << 8), u0, u1);
-            g = box_muller(u0, u1);
-        }
-        // mcmc.py:91-92: shift = step_size * scales * N(0,1); prop.shift_params(shift)
-        q[(size_t)p * n + i] = x[(size_t)p * n + i] + (step * scales[p]) * g;
+        const double g = draws ? draws[(size_t)p * n + i] : mh_normal(seed, (uint64_t)(begin + i), iteration, p);
+        q[(size_t)p * n + i] = mh_q(x[(size_t)p * n + i], step, scales[p], g);
     }
 }
 
@@ -126,14 +114,8 @@ __global__ void mh_accept_kernel(int P, int n, int64_t begin, double* __restrict
                                  int32_t* __restrict__ accepted) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    double u, unused;
-    if (draws) {
-        u = draws[i];
-    } else {
-        uniform2(seed, (uint64_t)(begin + i), iteration, RNG_MH_ACCEPT, u, unused);
-    }
-    // mcmc.py:115: if np.exp(logp_proposal - logp) > np.random.uniform(): accept
-    if (exp(lnp_new[i] - lnp[i]) > u) {
+    const double u = draws ? draws[i] : mh_u(seed, (uint64_t)(begin + i), iteration);
+    if (mh_accepts(lnp_new[i], lnp[i], u)) {
         for (int p = 0; p < P; p++) x[(size_t)p * n + i] = q[(size_t)p * n + i];
         lnp[i] = lnp_new[i];
         if (accepted) accepted[i] += 1;
@@ -147,17 +129,8 @@ __global__ void fd_params_kernel(int P, int n, const double* __restrict__ x, dou
     if (c >= n) return;
     const int S = 2 * P + 1;
     const size_t WW = (size_t)S * n;
-    for (int p = 0; p < P; p++) {
-        const double xp = x[(size_t)p * n + c];
-        for (int s = 0; s < S; s++) out[(size_t)p * WW + (size_t)s * n + c] = xp;
-    }
-    for (int p = 0; p < P; p++) {
-        const double xp = x[(size_t)p * n + c];
-        const double ax = fabs(xp) > fl[p] ? fabs(xp) : fl[p];
-        const double eps = rel * ax;
-        out[(size_t)p * WW + (size_t)(1 + 2 * p) * n + c] = xp + eps;
-        out[(size_t)p * WW + (size_t)(2 + 2 * p) * n + c] = xp - eps;
-    }
+    for (int p = 0; p < P; p++)
+        for (int s = 0; s < S; s++) out[(size_t)p * WW + (size_t)s * n + c] = fd_point(x, fl, rel, n, p, s * n + c);
 }
 
 static inline dim3 grid1(int n) { return dim3((n + 255) / 256); }

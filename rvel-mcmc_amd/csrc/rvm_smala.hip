@@ -209,13 +209,11 @@ __device__ __forceinline__ void smala_metric_stage(int P, int C, int c, int lane
 
 // One wave per chain: the P x P matrices live in LDS, lanes own matrix rows / entries, and the
 // sequential parts (Jacobi rotations, Cholesky columns) run lock-step across the wave.
-__global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, const double* __restrict__ x,
-                                                          double rel, const double* __restrict__ fl,
-                                                          const double* __restrict__ lp_st,
-                                                          const int32_t* __restrict__ st_st,
-                                                          const double* __restrict__ rv,
-                                                          const double* __restrict__ w, double npoints,
-                                                          double alpha, double eps, SmalaCache out) {
+__device__ __forceinline__ void smala_derive_chain(int P, int C, int E, const double* __restrict__ x, double rel,
+                                                   const double* __restrict__ fl, const double* __restrict__ lp_st,
+                                                   const int32_t* __restrict__ st_st, const double* __restrict__ rv,
+                                                   const double* __restrict__ w, double npoints, double alpha,
+                                                   double eps, const SmalaCache& out) {
     constexpr int PM = RVM_SMALA_MAX_PARAMS;
     constexpr int NTRI = PM * (PM + 1) / 2;        // upper-triangle entries
     constexpr int PER_LANE = (NTRI + 63) / 64;     // accumulators per lane
@@ -299,13 +297,21 @@ __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, c
     smala_metric_stage(P, C, c, lane, A, Qm, gr, xv, lt, inv, ra, rb, dn, rp, okflag, lp_st[c], alpha, eps, out);
 }
 
+__global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, const double* __restrict__ x,
+                                                          double rel, const double* __restrict__ fl,
+                                                          const double* __restrict__ lp_st,
+                                                          const int32_t* __restrict__ st_st,
+                                                          const double* __restrict__ rv,
+                                                          const double* __restrict__ w, double npoints,
+                                                          double alpha, double eps, SmalaCache out) {
+    smala_derive_chain(P, C, E, x, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, out);
+}
+
 // rvm_smala_metric: the same metric pipeline from exact derivatives (rvm_logl_derivs)
-__global__ __launch_bounds__(64) void smala_metric_kernel(int P, int C, const double* __restrict__ x,
-                                                          const double* __restrict__ lp,
-                                                          const int32_t* __restrict__ status,
-                                                          const double* __restrict__ grad,
-                                                          const double* __restrict__ hess, double alpha, double eps,
-                                                          SmalaCache out) {
+__device__ __forceinline__ void smala_metric_chain(int P, int C, const double* __restrict__ x,
+                                                   const double* __restrict__ lp, const int32_t* __restrict__ status,
+                                                   const double* __restrict__ grad, const double* __restrict__ hess,
+                                                   double alpha, double eps, const SmalaCache& out) {
     constexpr int PM = RVM_SMALA_MAX_PARAMS;
     __shared__ double A[PM * PM], Qm[PM * PM];
     __shared__ double gr[PM], lt[PM], inv[PM], xv[PM];
@@ -339,6 +345,15 @@ __global__ __launch_bounds__(64) void smala_metric_kernel(int P, int C, const do
     const int ok0 = okflag;
     smala_metric_stage(P, C, c, lane, A, Qm, gr, xv, lt, inv, ra, rb, dn, rp, okflag, lp[c], alpha, eps, out);
     if (lane == 0 && !ok0) out.ok[c] = 0;
+}
+
+__global__ __launch_bounds__(64) void smala_metric_kernel(int P, int C, const double* __restrict__ x,
+                                                          const double* __restrict__ lp,
+                                                          const int32_t* __restrict__ status,
+                                                          const double* __restrict__ grad,
+                                                          const double* __restrict__ hess, double alpha, double eps,
+                                                          SmalaCache out) {
+    smala_metric_chain(P, C, x, lp, status, grad, hess, alpha, eps, out);
 }
 
 __device__ __forceinline__ double box_muller_s(double u0, double u1) {
@@ -384,12 +399,11 @@ __device__ __forceinline__ double mvn_logpdf(int P, double maha, double logdet, 
 
 // One wave per chain: both Mahalanobis forms with the matrix entries spread over the lanes, then
 // the accept (mcmc.py:167-187) and, on accept, the proposal's cached derivatives copied in parallel.
-__global__ __launch_bounds__(64) void smala_accept_kernel(int P, int C, int64_t begin, double* __restrict__ x,
-                                                          SmalaCache cur, const double* __restrict__ xs,
-                                                          SmalaCache prop, double eps, uint64_t seed,
-                                                          uint64_t iteration, const double* __restrict__ draws,
-                                                          int32_t* __restrict__ accepted,
-                                                          int32_t* __restrict__ failures) {
+__device__ __forceinline__ void smala_accept_chain(int P, int C, int64_t begin, double* __restrict__ x,
+                                                   const SmalaCache& cur, const double* __restrict__ xs,
+                                                   const SmalaCache& prop, double eps, uint64_t seed,
+                                                   uint64_t iteration, const double* __restrict__ draws,
+                                                   int32_t* __restrict__ accepted, int32_t* __restrict__ failures) {
     const int c = blockIdx.x;
     const int lane = threadIdx.x;
     __shared__ double d1[RVM_SMALA_MAX_PARAMS], d2[RVM_SMALA_MAX_PARAMS];
@@ -437,6 +451,59 @@ __global__ __launch_bounds__(64) void smala_accept_kernel(int P, int C, int64_t 
         cur.ok[c] = 1;
         if (accepted) accepted[c] += 1;
     }
+}
+
+__global__ __launch_bounds__(64) void smala_accept_kernel(int P, int C, int64_t begin, double* __restrict__ x,
+                                                          SmalaCache cur, const double* __restrict__ xs,
+                                                          SmalaCache prop, double eps, uint64_t seed,
+                                                          uint64_t iteration, const double* __restrict__ draws,
+                                                          int32_t* __restrict__ accepted,
+                                                          int32_t* __restrict__ failures) {
+    smala_accept_chain(P, C, begin, x, cur, xs, prop, eps, seed, iteration, draws, accepted, failures);
+}
+
+// Fused second half of a SMALA step (rvm_smala_derive_accept / rvm_smala_metric_accept): the
+// proposal's cache from its stencil (or exact derivatives), then, in the same wave, the accept.
+// The barrier makes the cache entries this block just wrote visible to every lane of it.
+__global__ __launch_bounds__(64) void smala_derive_accept_kernel(
+    int P, int C, int E, const double* __restrict__ xs, double rel, const double* __restrict__ fl,
+    const double* __restrict__ lp_st, const int32_t* __restrict__ st_st, const double* __restrict__ rv,
+    const double* __restrict__ w, double npoints, double alpha, double eps, SmalaCache prop, int64_t begin,
+    double* __restrict__ x, SmalaCache cur, uint64_t seed, uint64_t iteration, const double* __restrict__ draws,
+    int32_t* __restrict__ accepted, int32_t* __restrict__ failures) {
+    smala_derive_chain(P, C, E, xs, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, prop);
+    __syncthreads();
+    smala_accept_chain(P, C, begin, x, cur, xs, prop, eps, seed, iteration, draws, accepted, failures);
+}
+
+__global__ __launch_bounds__(64) void smala_metric_accept_kernel(
+    int P, int C, const double* __restrict__ xs, const double* __restrict__ lp, const int32_t* __restrict__ status,
+    const double* __restrict__ grad, const double* __restrict__ hess, double alpha, double eps, SmalaCache prop,
+    int64_t begin, double* __restrict__ x, SmalaCache cur, uint64_t seed, uint64_t iteration,
+    const double* __restrict__ draws, int32_t* __restrict__ accepted, int32_t* __restrict__ failures) {
+    smala_metric_chain(P, C, xs, lp, status, grad, hess, alpha, eps, prop);
+    __syncthreads();
+    smala_accept_chain(P, C, begin, x, cur, xs, prop, eps, seed, iteration, draws, accepted, failures);
+}
+
+hipError_t launch_smala_derive_accept(int P, int C, int E, const double* xs, double rel, const double* fl,
+                                      const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
+                                      double npoints, double alpha, double eps, const SmalaCache& prop,
+                                      int64_t begin, double* x, const SmalaCache& cur, uint64_t seed, uint64_t it,
+                                      const double* draws, int32_t* accepted, int32_t* failures, hipStream_t st) {
+    smala_derive_accept_kernel<<<C, 64, 0, st>>>(P, C, E, xs, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, prop,
+                                                 begin, x, cur, seed, it, draws, accepted, failures);
+    return hipGetLastError();
+}
+
+hipError_t launch_smala_metric_accept(int P, int C, const double* xs, const double* lp, const int32_t* status,
+                                      const double* grad, const double* hess, double alpha, double eps,
+                                      const SmalaCache& prop, int64_t begin, double* x, const SmalaCache& cur,
+                                      uint64_t seed, uint64_t it, const double* draws, int32_t* accepted,
+                                      int32_t* failures, hipStream_t st) {
+    smala_metric_accept_kernel<<<C, 64, 0, st>>>(P, C, xs, lp, status, grad, hess, alpha, eps, prop, begin, x, cur,
+                                                 seed, it, draws, accepted, failures);
+    return hipGetLastError();
 }
 
 hipError_t launch_smala_metric(int P, int C, const double* x, const double* lp, const int32_t* status,

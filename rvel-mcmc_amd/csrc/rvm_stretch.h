@@ -49,4 +49,51 @@ __device__ __forceinline__ bool stretch_accepts(int dim, double z, double lnp_ne
     return lnpdiff > log(u3);
 }
 
+// ---- Gaussian random-walk MH (mcmc.py:89-121), shared by rvm_mh_propose / rvm_mh_accept and the
+// fused rvm_mh_step (the likelihood kernel forms the proposal in its prologue, accepts at the end)
+
+__device__ __forceinline__ double box_muller(double u0, double u1) {
+#pragma clang fp contract(off)
+    return sqrt(-2.0 * log(u0)) * cospi(2.0 * u1);
+}
+
+// N(0,1) draw of free parameter p of chain `gidx` (global index)
+__device__ __forceinline__ double mh_normal(uint64_t seed, uint64_t gidx, uint64_t iteration, int p) {
+    double u0, u1;
+    uniform2(seed, gidx, iteration, RNG_MH_PROPOSE | ((uint32_t)p << 8), u0, u1);
+    return box_muller(u0, u1);
+}
+
+// mcmc.py:91-92: shift = step_size * scales * N(0,1); prop.shift_params(shift)
+__device__ __forceinline__ double mh_q(double x, double step, double scale, double g) {
+#pragma clang fp contract(off)
+    return x + (step * scale) * g;
+}
+
+__device__ __forceinline__ double mh_u(uint64_t seed, uint64_t gidx, uint64_t iteration) {
+    double u, unused;
+    uniform2(seed, gidx, iteration, RNG_MH_ACCEPT, u, unused);
+    return u;
+}
+
+// mcmc.py:115: if np.exp(logp_proposal - logp) > np.random.uniform(): accept
+__device__ __forceinline__ bool mh_accepts(double lnp_new, double lnp_old, double u) {
+#pragma clang fp contract(off)
+    return exp(lnp_new - lnp_old) > u;
+}
+
+// ---- SMALA's central-difference stencil (rvm_fd_params and the fused rvm_smala_stencil_logl):
+// parameter p of stencil walker w = s * n + c around x [P][n]:  s = 1 + 2p: x_p + eps_p,
+// s = 2 + 2p: x_p - eps_p, otherwise x_p; eps_p = rel * max(|x_p|, floor_p)
+__device__ __forceinline__ double fd_point(const double* __restrict__ x, const double* __restrict__ fl, double rel,
+                                           int n, int p, int w) {
+#pragma clang fp contract(off)
+    const int s = w / n, c = w - s * n;
+    const double xp = x[(size_t)p * n + c];
+    if (s != 1 + 2 * p && s != 2 + 2 * p) return xp;
+    const double ax = fabs(xp) > fl[p] ? fabs(xp) : fl[p];
+    const double eps = rel * ax;
+    return s == 1 + 2 * p ? xp + eps : xp - eps;
+}
+
 }  // namespace rvm

@@ -17,7 +17,7 @@ RVM_STATUS_ENCOUNTER = 2
 RVM_STATUS_NONFINITE = 3
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
-ABI_VERSION = 7  # include/rvmcmc.h RVM_ABI_VERSION
+ABI_VERSION = 8  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):
@@ -64,6 +64,14 @@ SIGNATURES = {
                                     C.c_uint64, C.c_uint64, _dp, _dp, _dp]),
     "rvm_smala_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, C.POINTER(SmalaCache), _dp,
                                    C.POINTER(SmalaCache), C.c_double, C.c_uint64, C.c_uint64, _dp, _dp, _dp, _dp]),
+    "rvm_smala_stencil_logl": (C.c_int, [C.c_void_p, C.POINTER(ParamMapC), C.c_int32, C.c_int32, _dp, C.c_double,
+                                         _dp, C.c_double, _dp, _dp, _dp, _dp]),
+    "rvm_smala_derive_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int32, _dp, _dp, C.c_double, _dp, _dp,
+                                          _dp, _dp, _dp, C.c_double, C.c_double, C.c_double, C.POINTER(SmalaCache),
+                                          C.POINTER(SmalaCache), C.c_uint64, C.c_uint64, _dp, _dp, _dp, _dp]),
+    "rvm_smala_metric_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, _dp, _dp, _dp, _dp, _dp, C.c_double,
+                                          C.c_double, C.POINTER(SmalaCache), C.POINTER(SmalaCache), C.c_uint64,
+                                          C.c_uint64, _dp, _dp, _dp, _dp]),
     "rvm_last_error": (C.c_char_p, []),
     "rvm_plan_create": (C.c_int, [C.POINTER(RvmConfig), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
@@ -88,6 +96,8 @@ SIGNATURES = {
                                  _dp, _dp]),
     "rvm_mh_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, _dp, _dp, _dp, C.c_uint64, C.c_uint64, _dp, _dp,
                                 _dp]),
+    "rvm_mh_step": (C.c_int, [C.c_void_p, C.POINTER(ParamMapC), C.c_int32, C.c_int32, C.c_int64, _dp, _dp, _dp,
+                              C.c_double, C.c_uint64, C.c_uint64, C.c_double, _dp, _dp, _dp, _dp]),
     "rvm_fd_params": (C.c_int, [C.c_int32, C.c_int32, _dp, C.c_double, _dp, _dp, _dp]),
     "rvm_logl_derivs_workspace_bytes": (C.c_size_t, [C.c_int32, C.c_int32]),
     "rvm_logl_derivs": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_int32, C.POINTER(C.c_int32), C.c_double, _dp, _dp,

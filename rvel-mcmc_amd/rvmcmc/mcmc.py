@@ -13,6 +13,8 @@
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
 from . import _lib, engine
@@ -205,9 +207,10 @@ class Mh(Mcmc):
 class MhChains:
     """n_chains independent Gaussian random-walk MH chains, all resident on the device.
 
-    Per step: one proposal kernel, one likelihood launch for all chains, one accept kernel
-    (mcmc.py:89-121 semantics per chain; priorHard / Encounter proposals are rejected through
-    logp = -inf)."""
+    Per step ONE launch for all chains (rvm_mh_step: the likelihood kernel forms each chain's
+    proposal in its prologue and runs the accept on the lane that finishes the chain), or with
+    injected draws a proposal kernel, one likelihood launch and an accept kernel (mcmc.py:89-121
+    semantics per chain; priorHard / Encounter proposals are rejected through logp = -inf)."""
 
     def __init__(self, initial_state, obs, scales, step_size, n_chains, X0=None, seed=0, device=None):
         import torch
@@ -251,8 +254,22 @@ class MhChains:
         self.iteration, self.seed, self.step_size = int(d["iteration"]), int(d["seed"]), float(d["step_size"])
         self.Q = torch.empty_like(self.X)
 
-    def step(self, draws_propose=None, draws_accept=None):
+    def step(self, draws_propose=None, draws_accept=None, fused=True):
+        """One MH step of every chain.  Philox draws: ONE launch (rvm_mh_step: proposal, likelihood
+        and accept fused); injected draws, or fused=False: propose / likelihood / accept launches
+        (bit-identical for the same draws)."""
+        import torch
+
         st = _lib.stream_handle()
+        if fused and draws_propose is None and draws_accept is None:
+            with torch.cuda.device(self.device):
+                _lib.check(self.lib.rvm_mh_step(self.plan._h, C.byref(self.pmap.c_map()), self.dim, self.n, 0,
+                                                self.X.data_ptr(), self.lnp.data_ptr(), self.scales.data_ptr(),
+                                                self.step_size, self.seed, self.iteration,
+                                                float(self.state.hillRadiusFactor), 0, 0, self.accepted.data_ptr(),
+                                                st), "rvm_mh_step")
+            self.iteration += 1
+            return
         _lib.check(self.lib.rvm_mh_propose(self.dim, self.n, 0, self.X.data_ptr(), self.scales.data_ptr(),
                                            self.step_size, self.seed, self.iteration,
                                            draws_propose.data_ptr() if draws_propose is not None else 0,

@@ -132,7 +132,31 @@ class SmalaChains:
         d["_c"] = _lib.SmalaCache(*[d[k].data_ptr() for k in ("lp", "grad", "mu", "L", "G", "logdet", "ok")])
         return d
 
-    def _derive_into(self, X, cache):
+    def _stencil_logl(self, X, fused=True):
+        """logp, status [(2P+1) C] and model RVs [n_obs][(2P+1) C] over the central-difference
+        stencil of X: one launch that forms the stencil in the likelihood kernel's prologue
+        (rvm_smala_stencil_logl), or rvm_fd_params + rvm_logl_batch (fused=False; same bits)."""
+        torch = _torch()
+        if not fused:
+            _lib.check(self.lib.rvm_fd_params(self.P, self.n, X.data_ptr(), self.rel_step, self.floor.data_ptr(),
+                                              self.stencil.data_ptr(), _lib.stream_handle()), "rvm_fd_params")
+            return self.state.get_logp_batch(self.obs, self.stencil, hill_factor=1.0, want_rv=True, pmap=self.pmap)
+        S = 2 * self.P + 1
+        plan = self.state._plan(self.obs, max_walkers=S * self.n, device=self.device)
+        if getattr(self, "_st_bufs", None) is None:
+            self._st_bufs = (torch.empty(S * self.n, dtype=torch.float64, device=self.device),
+                             torch.empty(S * self.n, dtype=torch.int32, device=self.device),
+                             torch.empty((self.n_obs, S * self.n), dtype=torch.float64, device=self.device))
+        lp, st, rv = self._st_bufs
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.rvm_smala_stencil_logl(plan._h, C.byref(self.pmap.c_map()), self.P, self.n,
+                                                       X.data_ptr(), self.rel_step, self.floor.data_ptr(), 1.0,
+                                                       lp.data_ptr(), st.data_ptr(), rv.data_ptr(),
+                                                       _lib.stream_handle()), "rvm_smala_stencil_logl")
+        self._plan_keep = plan  # the launch's plan stays alive with the sampler
+        return lp, st, rv
+
+    def _derive_into(self, X, cache, fused=True):
         st_h = _lib.stream_handle()
         if self.hessian == "exact":
             lp, g, H, st = self.state.get_logp_d_dd_batch(self.obs, X, hill_factor=1.0, pmap=self.pmap)
@@ -141,9 +165,7 @@ class SmalaChains:
                                                  C.byref(cache["_c"]), st_h), "rvm_smala_metric")
             self._keep = (lp, g, H, st)  # alive until the stream has consumed them
             return
-        _lib.check(self.lib.rvm_fd_params(self.P, self.n, X.data_ptr(), self.rel_step, self.floor.data_ptr(),
-                                          self.stencil.data_ptr(), st_h), "rvm_fd_params")
-        lp, st, rv = self.state.get_logp_batch(self.obs, self.stencil, hill_factor=1.0, want_rv=True, pmap=self.pmap)
+        lp, st, rv = self._stencil_logl(X, fused)
         _lib.check(self.lib.rvm_smala_derive(self.P, self.n, self.n_obs, X.data_ptr(), self.rel_step,
                                              self.floor.data_ptr(), lp.data_ptr(), st.data_ptr(), rv.data_ptr(),
                                              self.inv_sigma2.data_ptr(), float(self.obs.Npoints), self.alpha,
@@ -172,8 +194,13 @@ class SmalaChains:
     def linalg_failures(self):
         return int(self.failures.sum().item())
 
-    def step(self, z=None, u=None):
-        """One SMALA step of every chain; z [C][P] / u [C] inject the normals / uniforms."""
+    def step(self, z=None, u=None, fused=True):
+        """One SMALA step of every chain; z [C][P] / u [C] inject the normals / uniforms.
+
+        fused (default): three launches -- rvm_smala_propose, the stencil likelihood launch
+        (rvm_smala_stencil_logl; exact: rvm_logl_derivs) and rvm_smala_derive_accept
+        (rvm_smala_metric_accept); fused=False runs the separate fd / logl / derive / accept
+        launches (bit-identical)."""
         st_h = _lib.stream_handle()
         zp = 0
         if z is not None:
@@ -186,7 +213,27 @@ class SmalaChains:
         _lib.check(self.lib.rvm_smala_propose(self.P, self.n, 0, self.X.data_ptr(), C.byref(self.cache["_c"]),
                                               self.eps, self.seed, self.iteration, zp, self.Xs.data_ptr(), st_h),
                    "rvm_smala_propose")
-        self._derive_into(self.Xs, self.prop)
+        cur, prop = C.byref(self.cache["_c"]), C.byref(self.prop["_c"])
+        if fused and self.hessian == "exact":
+            lp, g, H, st = self.state.get_logp_d_dd_batch(self.obs, self.Xs, hill_factor=1.0, pmap=self.pmap)
+            _lib.check(self.lib.rvm_smala_metric_accept(self.P, self.n, 0, self.X.data_ptr(), self.Xs.data_ptr(),
+                                                        lp.data_ptr(), st.data_ptr(), g.data_ptr(), H.data_ptr(),
+                                                        self.alpha, self.eps, cur, prop, self.seed, self.iteration,
+                                                        up, self.accepted.data_ptr(), self.failures.data_ptr(),
+                                                        st_h), "rvm_smala_metric_accept")
+            self._keep = (lp, g, H, st)
+            self.iteration += 1
+            return
+        if fused:
+            lp, st, rv = self._stencil_logl(self.Xs)
+            _lib.check(self.lib.rvm_smala_derive_accept(
+                self.P, self.n, 0, self.n_obs, self.X.data_ptr(), self.Xs.data_ptr(), self.rel_step,
+                self.floor.data_ptr(), lp.data_ptr(), st.data_ptr(), rv.data_ptr(), self.inv_sigma2.data_ptr(),
+                float(self.obs.Npoints), self.alpha, self.eps, cur, prop, self.seed, self.iteration, up,
+                self.accepted.data_ptr(), self.failures.data_ptr(), st_h), "rvm_smala_derive_accept")
+            self.iteration += 1
+            return
+        self._derive_into(self.Xs, self.prop, fused=False)
         _lib.check(self.lib.rvm_smala_accept(self.P, self.n, 0, self.X.data_ptr(), C.byref(self.cache["_c"]),
                                              self.Xs.data_ptr(), C.byref(self.prop["_c"]), self.eps, self.seed,
                                              self.iteration, up, self.accepted.data_ptr(), self.failures.data_ptr(),
