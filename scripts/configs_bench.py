@@ -7,6 +7,8 @@
   config 5: affine stretch, 3-planet synthetic, 8192 walkers per GPU (= 65536 over 8 GPUs);
             the third planet is named here (not in the reference): {m 1e-3, a 2.6, h 0.05, k 0, l 1}
   config 1: the reference-API single-chain Mh (mcmc_benchmark_mh.py), steps/s
+  config 1b: batched MH chains (MhChains, fused rvm_mh_step), 4096 chains; 1bu / 4u: the same
+            with the separate propose / logL / accept launches (before the fusion)
 
 Prints one JSON line per config.  Usage: python scripts/configs_bench.py [config ...]
 """
@@ -78,20 +80,22 @@ def config3():
     return {"config": "3: affine, 4096 walkers, HD155358.vels", **_affine(s, obs, 4096)}
 
 
-def config4(chains=256, steps=10):
+def config4(chains=256, steps=10, fused=True):
     np.random.seed(2017)
     s = State(planets=[dict(p) for p in S2])
     obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
     sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=chains, seed=0)
-    sm.step()
+    sm.step(fused=fused)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        sm.step()
+        sm.step(fused=fused)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     P = s.Nvars
-    return {"config": "4: SMALA, 256 chains, 10-dim, FD (2P+1 = 21 logL per chain-step)",
+    how = ("fused: propose + stencil logL launch + derive/accept kernel" if fused else
+           "separate propose / fd / logL / derive / accept launches")
+    return {"config": f"4: SMALA, 256 chains, 10-dim, FD (2P+1 = 21 logL per chain-step), {how}",
             "chain_steps_per_s": chains * steps / dt, "walker_logl_evals_per_s": chains * steps * (2 * P + 1) / dt,
             "ms_per_step": 1e3 * dt / steps, "acceptance": float(sm.accepted.double().mean().item() / sm.iteration)}
 
@@ -113,6 +117,35 @@ def config4x(chains=256, steps=5):
     return {"config": "4x: SMALA, 256 chains, 10-dim, exact gradient + Hessian (hyper-dual, 55 pair integrations)",
             "chain_steps_per_s": chains * steps / dt, "ms_per_step": 1e3 * dt / steps,
             "acceptance": float(sm.accepted.double().mean().item() / sm.iteration)}
+
+
+def config4u():
+    return config4(fused=False)
+
+
+def config1b(chains=4096, steps=20, fused=True):
+    """Batched MH (MhChains: mcmc.py:107-121 for every chain at once), 4096 chains on the
+    2-planet synthetic config, mcmc_benchmark_mh.py:52 scales, step 1e-3."""
+    np.random.seed(2017)
+    s = State(planets=[dict(p) for p in S2])
+    obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    mh = mcmc.MhChains(s, obs, {"m": 1.e-3, "a": 0.3, "h": 0.5, "k": 0.5, "l": np.pi / 2.}, 1e-3, chains, seed=0)
+    for _ in range(3):
+        mh.step(fused=fused)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        mh.step(fused=fused)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    how = "fused (rvm_mh_step, one launch)" if fused else "propose / logL / accept launches"
+    return {"config": f"1b: batched MH, {chains} chains, 2-planet synthetic, {how}",
+            "chain_steps_per_s": chains * steps / dt, "ms_per_step": 1e3 * dt / steps,
+            "acceptance": float(mh.accepted.double().mean().item() / mh.iteration)}
+
+
+def config1bu():
+    return config1b(fused=False)
 
 
 def config5(W=8192):
@@ -144,9 +177,11 @@ def config1s():
 
 
 def main():
-    which = sys.argv[1:] or ["2", "2w", "3", "4", "4x", "5", "1", "1s"]
+    which = sys.argv[1:] or ["2", "2w", "3", "4", "4u", "4x", "5", "1", "1s", "1b", "1bu"]
+    table = {"1": config1, "2": config2, "2w": config2w, "3": config3, "4": config4, "4u": config4u, "4x": config4x,
+             "5": config5, "1s": config1s, "1b": config1b, "1bu": config1bu}
     for c in which:
-        out = {"1": config1, "2": config2, "2w": config2w, "3": config3, "4": config4, "4x": config4x, "5": config5, "1s": config1s}[c]()
+        out = table[c]()
         print(json.dumps(out), flush=True)
 
 

@@ -38,12 +38,29 @@ RNG_MH_PROPOSE = 3
 RNG_MH_ACCEPT = 4
 
 
+def uniform2_vec(seed, items, iteration, stream):
+    """uniform2 for an array of items at once (numpy uint64 lanes; same bits as uniform2)."""
+    u64 = np.uint64
+    items = np.asarray(items, dtype=np.uint64)
+    m = u64(MASK)
+    x, y = items & m, (items >> u64(32)) & m
+    z = np.full_like(items, iteration & MASK)
+    w = np.full_like(items, (((iteration >> 32) & 0xFFFF) | (stream << 16)) & MASK)
+    k0, k1 = u64(seed & MASK), u64((seed >> 32) & MASK)
+    for _ in range(10):
+        p0 = u64(M0) * x
+        p1 = u64(M1) * z
+        x, y, z, w = ((p1 >> u64(32)) ^ y ^ k0) & m, p1 & m, ((p0 >> u64(32)) ^ w ^ k1) & m, p0 & m
+        k0 = (k0 + u64(W0)) & m
+        k1 = (k1 + u64(W1)) & m
+    a = ((x >> u64(5)) << u64(26)) | (y >> u64(6))
+    b = ((z >> u64(5)) << u64(26)) | (w >> u64(6))
+    return (a.astype(np.float64) + 0.5) / 9007199254740992.0, (b.astype(np.float64) + 0.5) / 9007199254740992.0
+
+
 def stretch_uniforms(seed, begin, n, iteration, half):
     """(u1, u2, u3) arrays for walkers begin..begin+n-1 as the device draws them."""
-    u1 = np.empty(n)
-    u2 = np.empty(n)
-    u3 = np.empty(n)
-    for i in range(n):
-        u1[i], u2[i] = uniform2(seed, begin + i, iteration, RNG_STRETCH_PROPOSE | (half << 8))
-        u3[i], _ = uniform2(seed, begin + i, iteration, RNG_STRETCH_ACCEPT | (half << 8))
+    items = np.arange(begin, begin + n, dtype=np.uint64)
+    u1, u2 = uniform2_vec(seed, items, iteration, RNG_STRETCH_PROPOSE | (half << 8))
+    u3, _ = uniform2_vec(seed, items, iteration, RNG_STRETCH_ACCEPT | (half << 8))
     return u1, u2, u3

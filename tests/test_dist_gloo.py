@@ -151,44 +151,52 @@ class SpecNumpyOps(FusedNumpyOps):
             s.pos_aos[h].copy_(s.pos[h].t())
 
 
-def _initial_positions(state):
+THIRD = {"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}  # scripts/configs_bench.py config 5
+DEFAULT = dict(W=W, planets=S2_PLANETS, iters=ITERS)
+# BASELINE config 5: 65536 walkers, 3 planets, sharded 8 ways (8192 walkers = 4096 per half per rank)
+CONFIG5 = dict(W=65536, planets=S2_PLANETS + [THIRD], iters=2)
+
+
+def _initial_positions(state, W):
     rng = np.random.default_rng(3)
     scales = np.array([S2_SCALES[k] for k in state.get_rawkeys()])
     return state.get_params()[None] + 1e-3 * scales * rng.standard_normal((W, state.Nvars))
 
 
-def _run_sampler(fused=False, ckpt=None):
+def _run_sampler(fused=False, ckpt=None, cfg=DEFAULT):
     from rvmcmc.ensemble import EnsembleSampler
     from rvmcmc.state import State
 
-    state = State(planets=[dict(p) for p in S2_PLANETS])
+    W_, iters = cfg["W"], cfg["iters"]
+    state = State(planets=[dict(p) for p in cfg["planets"]])
     ops = {False: NumpyOps, True: FusedNumpyOps, "spec": SpecNumpyOps}
-    ens = EnsembleSampler(W, state, obs=None, seed=SEED, device="cpu", ops=ops[fused])
+    ens = EnsembleSampler(W_, state, obs=None, seed=SEED, device="cpu", ops=ops[fused])
     assert ens.fused == bool(fused) and ens.speculating() == (fused == "spec")
-    ens.set_positions(_initial_positions(state))
+    ens.set_positions(_initial_positions(state, W_))
     ens.compute_lnprob()
     if ckpt is None:
-        for _ in range(ITERS):
+        for _ in range(iters):
             ens.step()
     else:  # half the iterations, checkpoint, continue in a fresh sampler from the file
-        for _ in range(ITERS // 2):
+        for _ in range(iters // 2):
             ens.step()
         ens.checkpoint(ckpt)
         if dist.is_initialized():
             dist.barrier()
-        ens = EnsembleSampler(W, state, obs=None, seed=0, device="cpu", ops=ops[fused])
+        ens = EnsembleSampler(W_, state, obs=None, seed=0, device="cpu", ops=ops[fused])
         ens.restore(ckpt)
-        for _ in range(ITERS - ITERS // 2):
+        for _ in range(iters - iters // 2):
             ens.step()
     return ens.gather_positions(), ens.gather_lnprob(), ens.naccepted.clone()
 
 
-def _worker(rank, world, port, out_dir, fused=False, ckpt=False):
+def _worker(rank, world, port, out_dir, fused=False, ckpt=False, cfg=DEFAULT):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        pos, lnp, acc = _run_sampler(fused, os.path.join(out_dir, "ckpt.npz") if ckpt else None)
+        pos, lnp, acc = _run_sampler(fused, os.path.join(out_dir, "ckpt.npz") if ckpt else None, cfg)
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), pos=pos, lnp=lnp, acc=acc.numpy())
     finally:
         dist.destroy_process_group()
@@ -245,6 +253,30 @@ def test_checkpoint_resume_is_bit_identical(tmp_path, world):
         pos, lnp = d["pos"], d["lnp"]
     np.testing.assert_array_equal(pos, pos1)
     np.testing.assert_array_equal(lnp, lnp1)
+
+
+@pytest.mark.parametrize("fused", [True, "spec"])
+def test_config5_layout_world8(tmp_path, fused):
+    """BASELINE config 5's sharded layout: 65536 walkers of the 3-planet system over 8 ranks
+    (rank r owns walkers [4096 r, 4096 (r + 1)) of each 32768-walker half; Philox keys = global
+    indices; complements all-gathered in global order).  Every rank's gathered ensemble, lnprob
+    and its slices of the accept counters equal the single-process run (the RCCL path itself is
+    unmeasured on hardware: the driver's 8-GPU node runs it)."""
+    world = 8
+    pos1, lnp1, acc1 = _run_sampler(fused=fused, cfg=CONFIG5)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), fused, False, CONFIG5), nprocs=world, join=True)
+    W_ = CONFIG5["W"]
+    n = W_ // 2 // world
+    accs = []
+    for r in range(world):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        np.testing.assert_array_equal(d["pos"], pos1)
+        np.testing.assert_array_equal(d["lnp"], lnp1)
+        assert d["acc"].shape == (2 * n,)
+        accs.append(d["acc"])
+    got = np.concatenate([np.concatenate([a[:n] for a in accs]), np.concatenate([a[n:] for a in accs])])
+    np.testing.assert_array_equal(got, acc1.numpy())
+    assert 0 < acc1.sum() < W_ * CONFIG5["iters"]
 
 
 def test_sampler_rejects_bad_sizes():
