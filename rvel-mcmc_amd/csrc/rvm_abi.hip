@@ -160,6 +160,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const Dir& D = dir[dd];
         const size_t n = D.idx.size();
         S[dd]->n_epochs = (int32_t)n;
+        S[dd]->n_steps = (int32_t)total_steps[dd];
         std::memcpy(hd + od, D.seg_len.data(), n * sizeof(double));
         S[dd]->seg_h1 = dd_base + od;
         od += n;

@@ -163,11 +163,17 @@ __device__ __forceinline__ void stumpff_full(double z, double& c0, double& c1, d
 }
 
 // ---- Pal (2009) -> heliocentric Cartesian (coplanar); REBOUND reb_tools_pal_to_particle -------
-__device__ __forceinline__ void pal_to_cart(double mu, double a, double lam, double k, double h, double& X,
-                                            double& Y, double& VX, double& VY) {
-    // Newton from F = lam; a lane stops updating at its own convergence (as a scalar loop would),
-    // so the result never depends on the other lanes of the wave.
-    double F = lam;
+// Eccentric longitude F from lam = F - k sin F + h cos F: Newton from F = lam, at most 100 steps,
+// stop once |step| <= 1e-16 max(|F|, 1) (the reference's loop).  A lane stops updating at its own
+// convergence (as a scalar loop would), so the result never depends on the other lanes of the wave.
+// Many walkers never meet that test: at roundoff the iteration settles into a 2-cycle between two
+// neighbouring doubles whose steps both exceed the bound, and the scalar loop runs all 100
+// iterations (~1000 cycles each; one such lane held its whole workgroup at the schedule barrier
+// for up to 50 us, timing build).  The map is deterministic, so once F_{i+1} == F_{i-1} with
+// neither step converged the sequence alternates for good, and the lane takes at once the iterate
+// the 100-step loop ends on: the same bits, without the remaining iterations.
+__device__ __forceinline__ double pal_solve_F(double lam, double k, double h) {
+    double F = lam, Fp = __builtin_nan("");  // Fp: the iterate before F
     bool done = false;
     for (int it = 0; it < 100; it++) {
         double sF, cF;
@@ -177,10 +183,21 @@ __device__ __forceinline__ void pal_to_cart(double mu, double a, double lam, dou
         const double step = fF / dF;
         const double Fn = F - step;
         const bool conv = !(fabs(step) > 1e-16 * (fabs(Fn) > 1.0 ? fabs(Fn) : 1.0));
-        F = done ? F : Fn;
-        done = done || conv;
+        const bool cyc = !conv && Fn == Fp;
+        const double Fc = ((99 - it) & 1) == 0 ? Fn : F;  // iterate 100 of the 2-cycle
+        if (!done) {
+            Fp = F;
+            F = cyc ? Fc : Fn;
+        }
+        done = done || conv || cyc;
         if (__all(done)) break;
     }
+    return F;
+}
+
+__device__ __forceinline__ void pal_to_cart(double mu, double a, double lam, double k, double h, double& X,
+                                            double& Y, double& VX, double& VY) {
+    const double F = pal_solve_F(lam, k, h);
     double sF, cF;
     sincos(F, &sF, &cF);
     const double beta = 1.0 / (1.0 + sqrt(1.0 - h * h - k * k));

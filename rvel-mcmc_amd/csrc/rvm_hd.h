@@ -379,21 +379,7 @@ __device__ __forceinline__ HD star_vx_hd(const LaneHD<NP>& s) {
 // eccentric-longitude equation F - k sin F + h cos F = lambda is solved on the primal, then two
 // hyper-dual Newton steps give F's derivatives.
 __device__ __forceinline__ void pal_to_cart_hd(HD mu, HD a, HD lam, HD k, HD h, HD& X, HD& Y, HD& VX, HD& VY) {
-    double F0 = lam.v;
-    bool done = false;
-    for (int it = 0; it < 100; it++) {
-        double sF, cF;
-        sincos(F0, &sF, &cF);
-        const double fF = F0 - k.v * sF + h.v * cF - lam.v;
-        const double dF = 1.0 - k.v * cF - h.v * sF;
-        const double step = fF / dF;
-        const double Fn = F0 - step;
-        const bool conv = !(fabs(step) > 1e-16 * (fabs(Fn) > 1.0 ? fabs(Fn) : 1.0));
-        F0 = done ? F0 : Fn;
-        done = done || conv;
-        if (__all(done)) break;
-    }
-    HD F = hd_c(F0);
+    HD F = hd_c(pal_solve_F(lam.v, k.v, h.v));
 #pragma unroll
     for (int it = 0; it < 2; it++) {
         const HD sF = hd_sin(F), cF = hd_cos(F);

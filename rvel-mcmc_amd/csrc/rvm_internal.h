@@ -9,6 +9,7 @@ namespace rvm {
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
     int32_t n_epochs;
+    int32_t n_steps;          // sum of seg_n: base steps of the whole direction
     const int32_t* seg_n;     // level-1 steps in the segment ending at this epoch (0: same time)
     const double* seg_h1;     // signed base step of the segment: length / seg_n (0 if seg_n = 0)
     const double* obs_rv;     // observed RV

@@ -40,7 +40,7 @@ namespace rvm {
 // Timing build (make profile -> scripts/probe/librvmcmc_prof.so): per wave, s_memtime at kernel
 // start, after the prologue, accumulated inside segments, accumulated in epoch handling (incl.
 // the barrier), and at the end.  Read with rvm_prof_copy (scripts/probe/prof_kernel.py).
-#define RVM_PROF_SLOTS 14
+#define RVM_PROF_SLOTS 18
 #define RVM_PROF_MAX_WAVES 4096
 __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 #define PROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -298,6 +298,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         if constexpr (D3) bad = bad || !(pix[p] * pix[p] + piy[p] * piy[p] < 4.0);  // state.py:311-313
         if (bad) status = RVM_STATUS_PRIOR;
     }
+    PROF_T(t_p1);  // parameters read, prior checked
     if (status != RVM_STATUS_OK) {  // keep the lane numerically benign; its result is discarded
 #pragma unroll
         for (int p = 0; p < NP; p++) {
@@ -383,6 +384,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         s.rz = D3 ? jz : 0.0;
         s.vz = D3 ? jvz : 0.0;
     }
+    PROF_T(t_p2);  // Pal -> Jacobi done
     s.r = D3 ? sqrt(s.rx * s.rx + s.ry * s.ry + s.rz * s.rz) : sqrt(s.rx * s.rx + s.ry * s.ry);
     s.ir = 1.0 / s.r;
     s.encm = 0;
@@ -393,6 +395,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         s.encm = t0.encm;
     }
 
+    PROF_T(t_p3);  // lane constants, encounter check at t = 0
     if (!dec) {
         if (i0 < E) {
             l_len[i0] = st_h;
@@ -424,6 +427,18 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         }
     }
 
+    // Level-split layout: waves wv and wv ^ 4 share a SIMD and run free (no epoch barrier couples
+    // them).  Equal-priority waves issue oldest first, so one of the pair ran at its lone-wave rate
+    // and the other crawled until it was alone (the SIMD's two instruction streams overlapped for
+    // a fraction of the time only).  Each wave publishes its remaining work (steps weighted by the
+    // level's step cost) in LDS at every epoch and takes the higher issue priority while it has
+    // more left than its SIMD partner: the pair finishes together, overlapped throughout.
+    PROF_T(t_p4);  // schedule staged (before the barrier)
+    __shared__ int s_rem[8];
+    const int wcost = spec ? 10 : 12;  // gated steps (ballot per drift) cost ~20 % more (timing build)
+    int rem = live ? mult * S.n_steps * wcost : 0;
+    if (dec && lane == 0) s_rem[wv] = rem;
+
     // ---- integrate outward from t = 0 through this direction's epochs -------------------------
     __syncthreads();  // schedule staged
     if (dec && !live) return;  // (no block barrier follows in the level-split layout)
@@ -444,6 +459,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const int n1_next = e + 1 < E ? l_n[e + 1] : 0;
         const double len_next = e + 1 < E ? l_len[e + 1] : 0.0;
         const int ns = n1 * mult;
+        // the partner's remaining work, read now and used after the segment (latency hidden)
+        int rem_oth = 0;
+        if (dec) rem_oth = __hip_atomic_load(s_rem + (wv ^ 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         PROF_T(ta);
         if (ns > 0) {
             const double h = len * inv_mult;  // len holds the segment's base step
@@ -467,6 +485,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
         if (dec) {
+            rem -= ns * wcost;
+            if (lane == 0) __hip_atomic_store(s_rem + wv, rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // (both operands through readfirstlane: a provably wave-uniform branch around each
+            // s_setprio, which ignores EXEC -- cdna_hip_programming.md §5.5 T5)
+            if (__builtin_amdgcn_readfirstlane(rem_oth) < __builtin_amdgcn_readfirstlane(rem))
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(1);
 #ifndef RVM_EXP_NO_HANDOFF_WRITES  // experiment builds only (scripts/probe): hand-off cost
             if (pl_idx == 0 && valid) *rvp = v0;
 #endif
@@ -575,6 +601,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 o[11] = rt_integ;
                 o[12] = rt_arr;
                 o[13] = (unsigned long long)arr | ((unsigned long long)unit_of() << 8);
+                o[14] = t_p1;
+                o[15] = t_p2;
+                o[16] = t_p3;
+                o[17] = t_p4;
             }
         };
 #endif
@@ -697,6 +727,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         o[8] = (unsigned long long)redo;
         o[9] = (unsigned long long)E;
         o[10] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
+        o[14] = t_p1;
+        o[15] = t_p2;
+        o[16] = t_p3;
+        o[17] = t_p4;
     }
 #endif
 }

@@ -17,7 +17,7 @@ import oracle as O  # noqa: E402
 from conftest import S2_PLANETS, s2_obs_oracle  # noqa: E402
 from rvmcmc import _lib, engine  # noqa: E402
 
-SLOTS, MAXW = 14, 4096
+SLOTS, MAXW = 18, 4096
 
 
 def main():
