@@ -31,7 +31,7 @@
  *     into a hipGraph.  rvm_plan_create is the only call that allocates (device buffers owned by
  *     the plan) and it synchronises once.
  *   - A plan is single-stream: it owns per-launch workspace (the direction-exchange slots and the
- *     level-split hand-off buffers and arrival counters), so launches that use one plan must be
+ *     level-split hand-off slots, left empty by every completed launch), so launches that use one plan must be
  *     serialised on one stream at a time.  Concurrent launches on two streams need two plans (the
  *     Python layer keys its plan cache by stream, rvmcmc/engine.py).
  *   - Walker parameters are SoA, [n_params][n_walkers] float64, n_params = 5*n_planets with the
@@ -88,7 +88,7 @@ typedef struct rvm_plan rvm_plan;
  * sign; t = 0 is the initial condition).  Allocates device memory and workspace for up to
  * max_walkers walkers per launch -- with four increasing levels and max_walkers large enough for
  * the level-split launch layout (more walker groups than half the CUs) also its hand-off
- * workspace, 64 * max(epochs per direction) * max_walkers bytes.
+ * workspace, 16 * max(epochs per direction) * max_walkers + 8 * max_walkers bytes.
  * observations.py:6-69 (tf/tb/rvf/rvb/errorf/errorb). */
 int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, const double* sigma, int32_t n_obs,
                     int32_t max_walkers, rvm_plan** out);

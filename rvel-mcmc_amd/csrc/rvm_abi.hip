@@ -234,7 +234,6 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     // big enough that the plan's largest launch would need two-group blocks
     P.lv_rv = nullptr;
     P.lv_enc = nullptr;
-    P.lv_cnt = nullptr;
     P.lv_emax = 0;
     P.lv_stride = 0;
     {
@@ -247,26 +246,23 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         if (nols && nols[0] == '1') inc = false;
         if (inc && P.n_cu > 0 && 2 * groups > P.n_cu) {
             const int64_t emax = (int64_t)(nf > nb ? nf : nb) > 0 ? (int64_t)(nf > nb ? nf : nb) : 1;
-            const int64_t units = 2 * groups + 8;
-            const size_t b_rv = (size_t)(2 * 4 * emax * max_walkers) * sizeof(double);
-            const size_t b_enc = (size_t)(2 * 4 * (int64_t)max_walkers) * sizeof(int32_t);
-            const size_t b_cnt = (size_t)units * sizeof(int32_t);
-            if (hipMalloc(&plan->lvmem, b_rv + b_enc + b_cnt) != hipSuccess) {
+            const size_t b_rv = (size_t)(2 * emax * max_walkers) * sizeof(double);
+            const size_t b_enc = (size_t)(2 * (int64_t)max_walkers) * sizeof(int32_t);
+            if (hipMalloc(&plan->lvmem, b_rv + b_enc) != hipSuccess) {
                 plan->lvmem = nullptr;
                 (void)hipGetLastError();  // the fallback is not an error: clear the runtime's sticky status
             } else {
                 unsigned char* base = reinterpret_cast<unsigned char*>(plan->lvmem);
                 P.lv_rv = reinterpret_cast<double*>(base);
                 P.lv_enc = reinterpret_cast<int32_t*>(base + b_rv);
-                P.lv_cnt = reinterpret_cast<int32_t*>(base + b_rv + b_enc);
                 P.lv_emax = (int32_t)emax;
                 P.lv_stride = max_walkers;
-                if (hipMemset(P.lv_cnt, 0, b_cnt) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+                // every slot empty (all-ones: the NaN sentinel / -1); the combiners restore this
+                if (hipMemset(plan->lvmem, 0xFF, b_rv + b_enc) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                     (void)hipFree(plan->lvmem);
                     plan->lvmem = nullptr;
                     P.lv_rv = nullptr;
                     P.lv_enc = nullptr;
-                    P.lv_cnt = nullptr;
                     (void)hipGetLastError();
                 }
             }

@@ -6,6 +6,11 @@
 
 namespace rvm {
 
+// level-split layout: the LDS ring of a type-A block holds at most this many epochs per level
+// (levels wait for the combiner beyond it), and the whole dynamic LDS request stays within
+constexpr int RVM_LS_RING = 64;
+constexpr int RVM_LS_MAX_LDS = 160 * 1024 - 16 * 1024;  // (the kernel's static LDS is < 16 KB)
+
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
     int32_t n_epochs;
@@ -30,11 +35,11 @@ struct DevPlan {
     int32_t n_obs;
     int32_t inclined;  // 1: 7 parameter rows per planet (ix, iy), 3-D integration
     int32_t n_cu;      // compute units of the plan's device (launch shape, launch_logl)
-    // level-split layout (launch_logl, rvm_logl.hip): each level wave of a walker group may run in
-    // its own workgroup; the waves meet through HBM instead of LDS.  Null when the plan cannot use it.
-    double* lv_rv;     // [2][n_levels][lv_emax][lv_stride] star vx per direction, level, epoch, walker
-    int32_t* lv_enc;   // [2][n_levels][lv_stride] encounter / prior flags per level
-    int32_t* lv_cnt;   // [units] level waves arrived per (walker group, direction); 0 between launches
+    // level-split layout (launch_logl, rvm_logl.hip): level 1 of a walker group runs in another
+    // workgroup than its levels 3, 2, 0 and the unit's combiner, and hands its star velocities over
+    // through HBM.  Null when the plan cannot use it.  All-ones / -1 between launches.
+    double* lv_rv;     // [2][lv_emax][lv_stride] level 1's star vx per direction, epoch, walker
+    int32_t* lv_enc;   // [2][lv_stride] level 1's encounter / prior flags
     int32_t lv_emax, lv_stride;
     DirSched fwd, bwd;
 };

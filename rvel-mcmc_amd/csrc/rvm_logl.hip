@@ -153,6 +153,19 @@ __device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, in
 // launches): chi2 >= 0 for an OK direction, -status otherwise.
 #define RVM_SLOT_EMPTY 0x7FF4DEADBEEF0001ULL  // a NaN pattern no direction result can take
 
+// Level-split hand-off of level 1 (type-B block -> the unit's combiner): the star vx of walker w at
+// epoch e of direction d sits in P.lv_rv[(d lv_emax + e) lv_stride + w]; all-ones (a NaN no
+// computed value takes: v0 is canonicalised) marks an empty slot.  The producer's agent-scope
+// relaxed store is write-through (sc1), the consumer polls with agent-scope relaxed loads (L1
+// bypassed) and puts the sentinel back: the value is the flag (cdna_hip_programming.md §6
+// Guideline 16, R2), no fence on either side.  Encounter / prior flags likewise in P.lv_enc (-1).
+#define RVM_LV_EMPTY 0xFFFFFFFFFFFFFFFFULL
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+// bounded spins (a hand-off that never completes gives up instead of hanging the GPU; blocks are
+// all resident by construction: launch_logl uses the layout only when its grid fits the CUs)
+#define RVM_LS_SPIN_MAX (1u << 20)
+
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
 template <int NP, bool D3, bool DEC>
 __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
@@ -177,10 +190,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // Level-split layout (nA > 0; four levels m0 < m1 < m2 < m3, 1-D grid of 8-wave blocks, wave i
     // on SIMD i % 4): a unit = (walker group, direction), u = 2 group + direction.  Blocks b < nA
     // carry levels (3, 3, 2, 2, -, -, 0, 0) of units 2b and 2b + 1 -- SIMD loads m3, m3, m2 + m0,
-    // m2 + m0; waves 4 and 5 only help stage the schedule -- and the others level 1 of eight
-    // units (2 m1 on every SIMD).  (136 VGPRs per lane: one such block per CU.)  A unit's level waves then sit in
-    // different workgroups: they hand their star velocities over through HBM (P.lv_*), and the
-    // last one to arrive forms the Richardson RVs and chi^2 (same arithmetic as the LDS path).
+    // m2 + m0; waves 4 and 5 are the two units' combiners -- and the others level 1 of eight
+    // units (2 m1 on every SIMD).  (136 VGPRs per lane: one such block per CU.)  Levels 3, 2, 0 of
+    // a unit hand their star velocities to the combiner through an LDS ring (with per-level epoch
+    // counters), level 1 -- in a type-B block on another CU, usually another XCD -- through HBM, one
+    // agent-scope 8-byte store per walker and epoch whose arrival is the value itself (the slot holds
+    // a NaN sentinel in between).  The combiner forms the Richardson RVs and chi^2 (same arithmetic
+    // as the LDS-coupled path) epoch by epoch while the levels still integrate, then finishes the
+    // walkers: when the last level ends, only its last epoch is left to combine.
     const int nl = P.n_levels;
     const int wv = threadIdx.x >> 6;
     constexpr bool dec = DEC;  // (nA > 0)
@@ -197,7 +214,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const int b = bid;
         const int unit = __builtin_amdgcn_readfirstlane(unit_of());  // wave-uniform (SGPRs)
         lvl = __builtin_amdgcn_readfirstlane(b < nA ? (wv < 2 ? 3 : (wv < 4 ? 2 : 0)) : 1);
-        idle = b < nA && (wv == 4 || wv == 5);
+        idle = b < nA && (wv == 4 || wv == 5);  // the combiners (no integration)
         grp = 0;
         G = 1;
         d = unit & 1;
@@ -210,6 +227,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         w0 = (blockIdx.x * G + grp) * WPB;  // first walker of the group
     }
     const bool live = w0 < W && !idle;  // level-split: waves past the last unit only help stage the schedule
+    const bool comb = dec && idle;       // level-split: this unit's combiner (type-A waves 4, 5)
     const int lane = threadIdx.x & 63;
     const int slot = lane / L;                     // walker slot within the group
     const int pl_idx = lane % L;
@@ -218,6 +236,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const int wl = valid ? w : (W - 1);
 
     __shared__ double s_rv_all[2][2][RVM_MAX_LEVELS][64];
+    // level-split hand-off inside a type-A block (unit ul = wv & 1; local level slot ks = 0, 1, 2
+    // for levels 3, 2, 0): epochs published per level, epochs consumed by the combiner, the levels'
+    // encounter / prior flags; the RVs themselves sit in the ring after the schedule (s_sched)
+    __shared__ int s_lvp[2][3];
+    __shared__ int s_cprog[2];
+    __shared__ int s_encl[2][3][64];
     __shared__ int s_enc_all[2][RVM_MAX_LEVELS][64];
     double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
@@ -412,6 +436,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             l_idx[i] = S.obs_idx[i];
         }
     } else {
+        if (threadIdx.x < 6) (&s_lvp[0][0])[threadIdx.x] = 0;
+        if (threadIdx.x < 2) s_cprog[threadIdx.x] = 0;
         for (int dd = 0; dd < 2; dd++) {
             const DirSched& SD = dd ? P.bwd : P.fwd;
             double* b = s_sched + (size_t)dd * 4 * emax2;
@@ -441,7 +467,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 
     // ---- integrate outward from t = 0 through this direction's epochs -------------------------
     __syncthreads();  // schedule staged
-    if (dec && !live) return;  // (no block barrier follows in the level-split layout)
+    if (dec && !live && !comb) return;  // (no block barrier follows in the level-split layout)
     PROF_T(t_pro);
 #ifdef RVM_PROFILE
     unsigned long long t_seg = 0, t_epo = 0;
@@ -449,12 +475,18 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     int redo = 0;      // speculative segments redone gated (counted in the timing build only)
     int spec_off = 0;  // wave-uniform: segments left to run gated after a redo
     double chi2 = 0.0;
-    // level-split: this lane's column of P.lv_rv (advanced by one epoch row per epoch)
-    double* rvp = dec ? P.lv_rv + (size_t)(d * nl + lvl) * P.lv_emax * P.lv_stride + wl : nullptr;
-    const int rv_stride = dec ? P.lv_stride : 0;
+    // level-split hand-off: level 1's column of P.lv_rv (one epoch row per epoch); the other levels'
+    // slot in the block's LDS ring ([unit ul][local level ks][RING][WPB] doubles after the schedule)
+    const int ul = wv & 1;
+    const int ks = lvl == 3 ? 0 : (lvl == 2 ? 1 : 2);
+    const int RING = emax2 < RVM_LS_RING ? emax2 : RVM_LS_RING;
+    double* ring = s_sched + (size_t)8 * emax2;
+    gu64* lv1p = dec ? (gu64*)(P.lv_rv + (size_t)d * P.lv_emax * P.lv_stride + wl) : nullptr;
+    int rslot = 0;
+    const int E_int = comb ? 0 : E;  // the combiners integrate nothing
     int n1 = E > 0 ? l_n[0] : 0;
     double len = E > 0 ? l_len[0] : 0.0;
-    for (int e = 0; e < E; e++) {
+    for (int e = 0; e < E_int; e++) {
         // prefetch the next segment while this one integrates
         const int n1_next = e + 1 < E ? l_n[e + 1] : 0;
         const double len_next = e + 1 < E ? l_len[e + 1] : 0.0;
@@ -493,10 +525,26 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 __builtin_amdgcn_s_setprio(2);
             else
                 __builtin_amdgcn_s_setprio(1);
-#ifndef RVM_EXP_NO_HANDOFF_WRITES  // experiment builds only (scripts/probe): hand-off cost
-            if (pl_idx == 0 && valid) *rvp = v0;
-#endif
-            rvp += rv_stride;
+            if (lvl == 1) {
+                if (pl_idx == 0 && valid) {
+                    unsigned long long bits = (unsigned long long)__double_as_longlong(v0);
+                    if (bits == RVM_LV_EMPTY) bits = 0x7FF8000000000000ULL;  // (still a NaN)
+                    __hip_atomic_store(lv1p, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                lv1p += P.lv_stride;
+            } else {
+                // wait while the combiner is a whole ring behind (only when E > RING)
+                if (E > RING) {
+                    unsigned spins = 0;
+                    while (e - __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                   s_cprog + ul, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >= RING &&
+                           ++spins < RVM_LS_SPIN_MAX)
+                        __builtin_amdgcn_s_sleep(4);
+                }
+                if (pl_idx == 0) ring[((ul * 3 + ks) * RING + rslot) * WPB + slot] = v0;
+                if (lane == 0) __hip_atomic_store(&s_lvp[ul][ks], e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                rslot = rslot + 1 == RING ? 0 : rslot + 1;
+            }
         } else {
             if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
             __syncthreads();
@@ -579,8 +627,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             }
         }
     } else {
-        // level-split: publish this level's flags, count the unit's arrivals; the last level wave
-        // to arrive combines all levels (their RVs went to P.lv_rv at every epoch)
+        // level-split: level waves publish their flags and leave; the combiner finishes the unit
 #ifdef RVM_PROFILE
         const unsigned long long rt_integ = __builtin_amdgcn_s_memrealtime();
         auto prof_dec = [&](unsigned long long rt_arr, int arr) {
@@ -594,7 +641,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 o[4] = __builtin_readcyclecounter();
                 o[5] = rt_start;
                 o[6] = __builtin_amdgcn_s_memrealtime();
-                o[7] = (unsigned long long)lvl | ((unsigned long long)d << 8) | ((unsigned long long)mult << 16);
+                // (level field 7: a combiner)
+                o[7] = (unsigned long long)(comb ? 7 : lvl) | ((unsigned long long)d << 8) | ((unsigned long long)mult << 16);
                 o[8] = (unsigned long long)redo;
                 o[9] = (unsigned long long)E;
                 o[10] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -608,83 +656,86 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             }
         };
 #endif
-        if (pl_idx == 0 && valid) P.lv_enc[(size_t)(d * nl + lvl) * P.lv_stride + w] = encflag;
-        __threadfence();  // release this wave's RVs and flags (agent scope: the units span XCDs)
-        // the write-back must complete before the counter add (MI355X_MICROARCH.md, compiler
-        // hazard: the wait after buffer_wbl2 can be dropped; inline asm is invisible to that pass)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        int arrived = 0;
-        const int unit = unit_of();
-        if (lane == 0) arrived = atomicAdd(P.lv_cnt + unit, 1);
-        arrived = __builtin_amdgcn_readfirstlane(arrived);
+        if (!comb) {
+            // a level wave: publish this level's encounter / prior flags and leave
+            if (lvl == 1) {
+                if (pl_idx == 0 && valid)
+                    __hip_atomic_store((gi32*)(P.lv_enc + (size_t)d * P.lv_stride + w), encflag, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                if (pl_idx == 0) s_encl[ul][ks][slot] = encflag;
+                if (lane == 0) __hip_atomic_store(&s_lvp[ul][ks], E + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
 #ifdef RVM_PROFILE
-        const unsigned long long rt_arr = __builtin_amdgcn_s_memrealtime();
-        if (arrived != nl - 1) {
-            prof_dec(rt_arr, arrived);
+            prof_dec(__builtin_amdgcn_s_memrealtime(), lvl);
+#endif
             return;
         }
-#endif
-        if (arrived != nl - 1) return;
-        if (lane == 0) P.lv_cnt[unit] = 0;  // all nl arrived: ready for the next launch
-#ifdef RVM_EXP_NO_COMBINE  // experiment builds only (scripts/probe): hand-off cost
-        return;
-#endif
-        __threadfence();  // acquire the other levels' stores (invalidates this CU's L1)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (valid) {  // both lanes of the walker's pair take part in the loads
-            int enc = 0;
-            if (pl_idx == 0)
-                for (int k = 0; k < nl; k++) enc |= __builtin_nontemporal_load(P.lv_enc + (size_t)(d * nl + k) * P.lv_stride + w);
-            // (nl = 4 here) epochs in chunks of CH, software-pipelined: the next chunk's loads are in
-            // flight while this chunk is combined (the other levels' values come from other XCDs'
-            // stores, an HBM round trip each).  Lane pl of the walker's pair loads and combines
-            // epochs [e0 + pl HC, e0 + (pl + 1) HC) of a chunk; the pair's first lane then sums the
-            // chi^2 terms in epoch order (same bits as the LDS-coupled path).
-            constexpr int NLP = L >= 2 ? 2 : 1;  // lanes sharing a walker's loads (one planet: one lane)
-            constexpr int CH = 16, HC = CH / NLP;
-            const size_t ls = (size_t)P.lv_emax * P.lv_stride;
-            const double* rvb = P.lv_rv + (size_t)(d * 4) * ls + w;
-            const int eh = (pl_idx < NLP ? pl_idx : 0) * HC;
-            auto load_half = [&](int e0, double (&v)[HC][4]) {
-#pragma unroll
-                for (int i = 0; i < HC; i++) {
-                    const int e = e0 + eh + i < E ? e0 + eh + i : E - 1;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) v[i][k] = __builtin_nontemporal_load(rvb + k * ls + (size_t)e * P.lv_stride);
-                }
-            };
-            double chi2w = 0.0;
-            double va[HC][4], vb[HC][4];
-            if (E > 0) load_half(0, va);
-            for (int e0 = 0; e0 < E; e0 += CH) {
-                if (e0 + CH < E) load_half(e0 + CH, vb);
-                double term[HC];
-#pragma unroll
-                for (int i = 0; i < HC; i++) {
-                    const int e = e0 + eh + i;
-                    const int ec = e < E ? e : E - 1;
-                    double rvx = 0.0;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) rvx += P.lw[k] * va[i][k];
-                    const double r = rvx - l_rv[ec];
-                    term[i] = (r * r) / l_s2[ec];
-                    if (rv_out != nullptr && e < E && pl_idx < NLP) rv_out[(size_t)l_idx[e] * W + w] = rvx;
-                }
-#pragma unroll
-                for (int i = 0; i < HC; i++)
-                    if (e0 + i < E) chi2w += term[i];
-                if constexpr (NLP == 2) {
-#pragma unroll
-                    for (int i = 0; i < HC; i++) {
-                        const double t1 = grp_get<L, 1>(term[i]);
-                        if (e0 + HC + i < E) chi2w += t1;
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < HC; i++)
-#pragma unroll
-                    for (int k = 0; k < 4; k++) va[i][k] = vb[i][k];
+        // the unit's combiner: consume epoch e once the three local levels have published it
+        // (LDS counters) and level 1's values have landed (every lane's slot off the sentinel);
+        // lowest issue priority (it shares SIMD 0 / 1 with a level-3 wave)
+        __builtin_amdgcn_s_setprio(0);
+        unsigned spins = 0;
+        bool hung = false;
+        auto local_published = [&]() {
+            const int p0 = __hip_atomic_load(&s_lvp[ul][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int p1 = __hip_atomic_load(&s_lvp[ul][1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int p2 = __hip_atomic_load(&s_lvp[ul][2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return __builtin_amdgcn_readfirstlane(p0 < p1 ? (p0 < p2 ? p0 : p2) : (p1 < p2 ? p1 : p2));
+        };
+        gu64* l1 = (gu64*)(P.lv_rv + (size_t)d * P.lv_emax * P.lv_stride + wl);
+        double chi2w = 0.0;
+        int rr = 0;
+        for (int e = 0; e < E; e++) {
+            while (!hung && local_published() <= e) {
+                __builtin_amdgcn_s_sleep(2);
+                hung = ++spins >= RVM_LS_SPIN_MAX;
             }
+            unsigned long long b1;
+            for (;;) {
+                b1 = valid ? __hip_atomic_load(l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ULL;
+                if (ballot(b1 == RVM_LV_EMPTY) == 0 || hung) break;
+                __builtin_amdgcn_s_sleep(2);
+                hung = ++spins >= RVM_LS_SPIN_MAX;
+            }
+            if (valid && pl_idx == 0) __hip_atomic_store(l1, RVM_LV_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            l1 += P.lv_stride;
+            // levels in order 0..3 (same arithmetic as the LDS-coupled path)
+            const double* rg = ring + (size_t)rr * WPB + slot;
+            const double v[4] = {rg[(ul * 3 + 2) * RING * WPB], __longlong_as_double((long long)b1),
+                                 rg[(ul * 3 + 1) * RING * WPB], rg[(ul * 3 + 0) * RING * WPB]};
+            double rvx = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) rvx += P.lw[k] * v[k];
+            const double r = rvx - l_rv[e];
+            chi2w += (r * r) / l_s2[e];
+            if (rv_out != nullptr && valid && pl_idx == 0) rv_out[(size_t)l_idx[e] * W + w] = rvx;
+            if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            rr = rr + 1 == RING ? 0 : rr + 1;
+        }
+        // the levels' flags: local ones after their last counter step (E + 1), level 1's from HBM
+        while (!hung && local_published() <= E) {
+            __builtin_amdgcn_s_sleep(2);
+            hung = ++spins >= RVM_LS_SPIN_MAX;
+        }
+        int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];
+        {
+            gi32* e1p = (gi32*)(P.lv_enc + (size_t)d * P.lv_stride + wl);
+            int f1;
+            for (;;) {
+                f1 = valid ? __hip_atomic_load(e1p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                if (ballot(f1 < 0) == 0 || hung) break;
+                __builtin_amdgcn_s_sleep(2);
+                hung = ++spins >= RVM_LS_SPIN_MAX;
+            }
+            if (valid && pl_idx == 0) __hip_atomic_store(e1p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            enc |= f1 > 0 ? f1 : 0;
+        }
+        if (hung) chi2w = __builtin_nan("");  // never completed: reported as RVM_STATUS_NONFINITE
+#ifdef RVM_PROFILE
+        const unsigned long long rt_arr = __builtin_amdgcn_s_memrealtime();
+#endif
+        if (valid) {
             if (pl_idx != 0) {
                 // (the pair's second lane only helped with the loads)
             } else if (stretch) {
@@ -761,19 +812,27 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
         const int c_dec = std::max(m[3], std::max(m[2] + m[0], 2 * m[1]));
         const int c_cpl = G == 1 ? m[3] * ((2 * groups + P.n_cu - 1) / P.n_cu)
                                  : std::max(m[0] + m[3], m[1] + m[2]) * ((groups + P.n_cu - 1) / P.n_cu);
-        if (na + nb <= P.n_cu && c_dec < c_cpl) {
+        const int ring = emax < RVM_LS_RING ? emax : RVM_LS_RING;
+        const size_t smem_ls = (size_t)emax * 8 * sizeof(double) + (size_t)6 * ring * wpb * sizeof(double);
+        if (na + nb <= P.n_cu && c_dec < c_cpl && smem_ls <= (size_t)RVM_LS_MAX_LDS) {
             nA = na;
             grid = dim3(na + nb, 1);
             block = dim3(8 * 64);
-            smem = (size_t)emax * 8 * sizeof(double);
+            smem = smem_ls;
         }
     }
 #define RVM_LAUNCH(NPV, D3V)                                                                                \
     do {                                                                                                 \
-        if (nA > 0)                                                                                      \
+        if (nA > 0) {                                                                                    \
+            static bool lds_set = false; /* dynamic LDS beyond 64 KB: once per instantiation */         \
+            if (!lds_set) {                                                                              \
+                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logl_kernel<NPV, D3V, true>),   \
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, RVM_LS_MAX_LDS);   \
+                lds_set = true;                                                                          \
+            }                                                                                            \
             logl_kernel<NPV, D3V, true><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, \
                                                                        logl, status, sa, nA);            \
-        else                                                                                             \
+        } else                                                                                           \
             logl_kernel<NPV, D3V, false><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots,  \
                                                                         rv_out, logl, status, sa, nA);   \
     } while (0)
