@@ -346,6 +346,37 @@ def test_large_batch_size_independent_results(W):
     assert np.isfinite(big).all()
 
 
+@pytest.mark.parametrize("one_sided", [False, True])
+def test_level_split_ring_wrap_and_empty_direction(one_sided):
+    """Level-split hand-off (rvm_logl.hip): levels 3, 2, 0 pass their per-epoch RVs to the unit's
+    combiner through an LDS ring of RVM_LS_RING = 64 epochs and wait when a whole ring ahead;
+    level 1 through HBM granules.  301 epochs (151 forward) wrap the ring and exercise that wait;
+    the one-sided set (all epochs at t >= 0) leaves the backward units with no epoch at all.  Every
+    walker gives the bits (logL, status, model RVs) of its LDS-coupled single launch, and T1
+    against the oracle on a subset."""
+    np.random.seed(13)
+    obs = O.fake_obs(S2_PLANETS, Npoints=300, error=1.5e-4, errorVar=2.5e-5, tmax=150.)
+    if one_sided:
+        e = np.zeros(0)
+        obs = O.OracleObs(tf=obs.tf, rvf=obs.rvf, errorf=obs.errorf, tb=e, rvb=e, errorb=e, Npoints=obs.Npoints)
+    W = 6000  # 376 (group, direction) units: the level-split layout
+    plan, dt = _plan(obs, S2_PLANETS, max_walkers=W)
+    P = _ball(S2_PLANETS, W, seed=31)
+    big, st_big, rv_big = _run(plan, P, want_rv=True)
+    assert np.isfinite(big).all()
+    for i in (0, 31, 2999, W - 1):
+        one, st1, rv1 = _run(plan, P[i:i + 1], want_rv=True)
+        assert one[0] == big[i] and st1[0] == st_big[i]
+        np.testing.assert_array_equal(rv1[:, 0], rv_big[:, i])
+    idx = np.r_[0:12, W - 12:W]
+    ref, st_ref = O.logl_whx_batch(P[idx], 2, obs, dt, LEVELS)
+    _assert_t1(big[idx], st_big[idx], ref, st_ref, sens=oracle_sensitivity(P[idx], 2, obs, dt, LEVELS))
+    # a second launch finds every hand-off slot empty again (the combiners restore the sentinel)
+    again, st2, _ = _run(plan, P)
+    np.testing.assert_array_equal(again, big)
+    np.testing.assert_array_equal(st2, st_big)
+
+
 @pytest.mark.parametrize("W", [4160, 2900])
 def test_two_group_blocks_vs_oracle_three_planets(W):
     """3 planets: 16 walkers per wave; 4160 walkers run two mirrored groups per block, 2900 the
