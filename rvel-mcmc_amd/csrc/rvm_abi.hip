@@ -161,6 +161,36 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const size_t n = D.idx.size();
         S[dd]->n_epochs = (int32_t)n;
         S[dd]->n_steps = (int32_t)total_steps[dd];
+        // head / tail split points (rvm_logl.hip level-split roles): level 0 at the share f0 of the
+        // steps that balances SIMD loads m2 + f0 m0 = m3 + (1 - f0) m0, level 1 at one half
+        {
+            const int nlv = cfg->n_levels;
+            double f0 = 0.5;
+            if (nlv == 4) f0 = std::min(1.0, std::max(0.0, (double)(mult[3] + mult[0] - mult[2]) / (2.0 * mult[0])));
+            const double fr[2] = {f0, 0.5};
+            int32_t sp[2] = {0, 0}, pr[2] = {0, 0};
+            for (int q = 0; q < 2; q++) {
+                const double target = fr[q] * (double)total_steps[dd];
+                long long cum = 0, best_cum = 0;
+                int best = 0;
+                double best_d = target;  // split at 0
+                for (size_t i = 0; i < n; i++) {
+                    cum += D.seg_n[i];
+                    const double dist = std::fabs((double)cum - target);
+                    if (dist < best_d) {
+                        best_d = dist;
+                        best = (int)i + 1;
+                        best_cum = cum;
+                    }
+                }
+                sp[q] = best;
+                pr[q] = (int32_t)best_cum;
+            }
+            S[dd]->split0 = sp[0];
+            S[dd]->pre0 = pr[0];
+            S[dd]->split1 = sp[1];
+            S[dd]->pre1 = pr[1];
+        }
         std::memcpy(hd + od, D.seg_len.data(), n * sizeof(double));
         S[dd]->seg_h1 = dd_base + od;
         od += n;

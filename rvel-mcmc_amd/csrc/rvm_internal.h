@@ -15,6 +15,9 @@ constexpr int RVM_LS_MAX_LDS = 160 * 1024 - 16 * 1024;  // (the kernel's static 
 struct DirSched {
     int32_t n_epochs;
     int32_t n_steps;          // sum of seg_n: base steps of the whole direction
+    // level-split layout: levels 0 (type-A blocks) and 1 (type-B, tB = 6) may run as a head over
+    // epochs [0, split) and a tail over [split, n_epochs) in two waves; pre = base steps before split
+    int32_t split0, pre0, split1, pre1;
     const int32_t* seg_n;     // level-1 steps in the segment ending at this epoch (0: same time)
     const double* seg_h1;     // signed base step of the segment: length / seg_n (0 if seg_n = 0)
     const double* obs_rv;     // observed RV

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                                                                    double* __restrict__ rv_out,
                                                                    double* __restrict__ logl_out,
                                                                    int32_t* __restrict__ status_out,
-                                                                   const StretchArgs sa, const int nA) {
+                                                                   const StretchArgs sa, const int nA, const int lsm) {
     constexpr int L = LanesPerWalker<NP>::value;  // lanes per walker (one per planet)
     constexpr int WPB = 64 / L;                    // walkers per block (= per wave)
     PROF_T(t_start);
@@ -209,12 +209,32 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // 6144-walker launch, scripts/probe/handoff_ab.sh)
     const int nB = (int)gridDim.x - nA;
     const int bid = (int)blockIdx.x < nB ? nA + (int)blockIdx.x : (int)blockIdx.x - nB;
-    auto unit_of = [&]() { return bid < nA ? 2 * bid + (wv & 1) : 8 * (bid - nA) + wv; };
+    // level-split roles (8-wave blocks, wave i on SIMD i % 4; part: 0 whole level, 1 / 2 the head /
+    // tail of a level split at an epoch, the state handed over through LDS in slot hs):
+    //   type A, units 2b + (wv & 1): waves 0, 1 level 3; 2, 3 level 2; and either (splitA) 6, 7 the
+    //     heads of level 0 (epochs [0, split0)), then the units' combiners, with 4, 5 its tails on
+    //     SIMDs 0, 1 -- SIMD loads m3 + m0 (1 - f), m2 + m0 f with f = split0's share of the steps
+    //     (0.625 at 4..7: 8.5, 8.5); or 6, 7 level 0 whole and 4, 5 the combiners (10, 7)
+    //   type B, tB = 8 units of level 1 per block: waves 0..7 one each (2 m1 per SIMD); or tB = 6
+    //     (all CUs in use): waves 0..3 whole, 4 / 5 head / tail of unit 4, 6 / 7 of unit 5 (1.5 m1)
+    const int tB = lsm & 0xFF;
+    const bool splitA = (lsm >> 8) != 0;  // (needs the whole direction in the ring: E <= RVM_LS_RING)
+    const int tsk = wv < 4 || tB == 8 ? wv : (wv < 6 ? 4 : 5);  // type-B task of this wave
+    auto unit_of = [&]() { return bid < nA ? 2 * bid + (wv & 1) : tB * (bid - nA) + tsk; };
+    int part = 0, hs = 0;
+    bool skip = false;  // no role (the blocks' last waves)
     if (dec) {
         const int b = bid;
         const int unit = __builtin_amdgcn_readfirstlane(unit_of());  // wave-uniform (SGPRs)
         lvl = __builtin_amdgcn_readfirstlane(b < nA ? (wv < 2 ? 3 : (wv < 4 ? 2 : 0)) : 1);
-        idle = b < nA && (wv == 4 || wv == 5);  // the combiners (no integration)
+        idle = b < nA && !splitA && (wv == 4 || wv == 5);  // the combiners (no integration)
+        if (b < nA) {
+            part = splitA ? (wv >= 6 ? 1 : (wv >= 4 ? 2 : 0)) : 0;
+            hs = wv & 1;
+        } else {
+            part = tB == 8 || wv < 4 ? 0 : ((wv & 1) ? 2 : 1);
+            hs = (wv - 4) >> 1;
+        }
         grp = 0;
         G = 1;
         d = unit & 1;
@@ -226,8 +246,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         d = blockIdx.y;
         w0 = (blockIdx.x * G + grp) * WPB;  // first walker of the group
     }
-    const bool live = w0 < W && !idle;  // level-split: waves past the last unit only help stage the schedule
-    const bool comb = dec && idle;       // level-split: this unit's combiner (type-A waves 4, 5)
+    const bool live = w0 < W && !idle && !skip;  // level-split: waves past the last unit only help stage the schedule
+    const bool comb = dec && idle;       // level-split: this unit's combiner from the start
     const int lane = threadIdx.x & 63;
     const int slot = lane / L;                     // walker slot within the group
     const int pl_idx = lane % L;
@@ -242,6 +262,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     __shared__ int s_lvp[2][3];
     __shared__ int s_cprog[2];
     __shared__ int s_encl[2][3][64];
+    // head -> tail hand-off of a split level (slot hs): the lanes' dynamic state, the wave's
+    // encounter mask and speculation state, and the ready flag
+    __shared__ double s_hos[2][8][64];
+    __shared__ unsigned long long s_hoe[2];
+    __shared__ int s_hosp[2], s_hof[2];
     __shared__ int s_enc_all[2][RVM_MAX_LEVELS][64];
     double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
@@ -438,6 +463,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     } else {
         if (threadIdx.x < 6) (&s_lvp[0][0])[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_cprog[threadIdx.x] = 0;
+        if (threadIdx.x < 2) s_hof[threadIdx.x] = 0;
         for (int dd = 0; dd < 2; dd++) {
             const DirSched& SD = dd ? P.bwd : P.fwd;
             double* b = s_sched + (size_t)dd * 4 * emax2;
@@ -454,16 +480,30 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     }
 
     // Level-split layout: waves wv and wv ^ 4 share a SIMD and run free (no epoch barrier couples
-    // them).  Equal-priority waves issue oldest first, so one of the pair ran at its lone-wave rate
-    // and the other crawled until it was alone (the SIMD's two instruction streams overlapped for
-    // a fraction of the time only).  Each wave publishes its remaining work (steps weighted by the
-    // level's step cost) in LDS at every epoch and takes the higher issue priority while it has
-    // more left than its SIMD partner: the pair finishes together, overlapped throughout.
+    // them).  Equal-priority waves issue oldest first, so one ran at its lone-wave rate and
+    // the others crawled until it was done (the SIMD's instruction streams overlapped for a fraction
+    // of the time only).  Each wave publishes its remaining work (steps weighted by the level's
+    // step cost) in LDS at
+    // every epoch and takes the higher issue priority while it has more left than its SIMD partner:
+    // the pair finishes together, overlapped throughout.  A head and its partner instead keep equal
+    // pace (weighted steps done): the head ends about when its tail can best share the other SIMD
+    // (measured: head-first priority serialised its SIMD, remaining-work priority started the
+    // tail too late).
     PROF_T(t_p4);  // schedule staged (before the barrier)
-    __shared__ int s_rem[8];
+    __shared__ int s_rem[8], s_done[8];
     const int wcost = spec ? 10 : 12;  // gated steps (ballot per drift) cost ~20 % more (timing build)
-    int rem = live ? mult * S.n_steps * wcost : 0;
-    if (dec && lane == 0) s_rem[wv] = rem;
+    const int esplit = lvl == 0 ? S.split0 : S.split1;  // head / tail boundary of a split level
+    const int e_lo = part == 2 ? esplit : 0, e_hi = part == 1 ? esplit : E;
+    int rem = live ? mult * (S.n_steps - (part == 2 ? (lvl == 0 ? S.pre0 : S.pre1) : 0)) * wcost : 0;
+    // a head runs first (its tail, on another SIMD, cannot start before it ends): it publishes more
+    // remaining work than any whole level has
+    int done = 0;
+    if (dec && lane == 0) {
+        s_rem[wv] = rem;
+        s_done[wv] = 0;
+    }
+    // the SIMD partner (wv ^ 4) heads a split level: type A waves 6, 7 (splitA), type B 4, 6 (tB = 6)
+    const bool oth_head = bid < nA ? (splitA && (wv == 2 || wv == 3)) : (tB == 6 && (wv == 0 || wv == 2));
 
     // ---- integrate outward from t = 0 through this direction's epochs -------------------------
     __syncthreads();  // schedule staged
@@ -481,19 +521,41 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const int ks = lvl == 3 ? 0 : (lvl == 2 ? 1 : 2);
     const int RING = emax2 < RVM_LS_RING ? emax2 : RVM_LS_RING;
     double* ring = s_sched + (size_t)8 * emax2;
-    gu64* lv1p = dec ? (gu64*)(P.lv_rv + (size_t)d * P.lv_emax * P.lv_stride + wl) : nullptr;
-    int rslot = 0;
-    const int E_int = comb ? 0 : E;  // the combiners integrate nothing
-    int n1 = E > 0 ? l_n[0] : 0;
-    double len = E > 0 ? l_len[0] : 0.0;
-    for (int e = 0; e < E_int; e++) {
+    gu64* lv1p = dec ? (gu64*)(P.lv_rv + ((size_t)d * P.lv_emax + e_lo) * P.lv_stride + wl) : nullptr;
+    int rslot = RING > 0 ? e_lo % RING : 0;
+    const int E_int = comb ? 0 : e_hi;  // the combiners integrate nothing
+    if (dec && part == 2) {
+        // a tail: wait for the head's state at epoch e_lo (same block, LDS)
+        unsigned spins = 0;
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_hof[hs], __ATOMIC_ACQUIRE,
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) == 0 &&
+               ++spins < RVM_LS_SPIN_MAX)
+            __builtin_amdgcn_s_sleep(8);
+        s.rx = s_hos[hs][0][lane];
+        s.ry = s_hos[hs][1][lane];
+        s.vx = s_hos[hs][2][lane];
+        s.vy = s_hos[hs][3][lane];
+        s.rz = s_hos[hs][4][lane];
+        s.vz = s_hos[hs][5][lane];
+        s.r = s_hos[hs][6][lane];
+        s.ir = s_hos[hs][7][lane];
+        s.encm = __builtin_amdgcn_readfirstlane(s_hoe[hs] & 0xFFFFFFFFull) |
+                 ((unsigned long long)__builtin_amdgcn_readfirstlane(s_hoe[hs] >> 32) << 32);
+        spec_off = __builtin_amdgcn_readfirstlane(s_hosp[hs]);
+    }
+    int n1 = e_lo < E ? l_n[e_lo] : 0;
+    double len = e_lo < E ? l_len[e_lo] : 0.0;
+    for (int e = e_lo; e < E_int; e++) {
         // prefetch the next segment while this one integrates
         const int n1_next = e + 1 < E ? l_n[e + 1] : 0;
         const double len_next = e + 1 < E ? l_len[e + 1] : 0.0;
         const int ns = n1 * mult;
         // the partner's remaining work, read now and used after the segment (latency hidden)
-        int rem_oth = 0;
-        if (dec) rem_oth = __hip_atomic_load(s_rem + (wv ^ 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        int rem_oth = 0, done_oth = 0;
+        if (dec) {
+            rem_oth = __hip_atomic_load(s_rem + (wv ^ 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            done_oth = __hip_atomic_load(s_done + (wv ^ 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         PROF_T(ta);
         if (ns > 0) {
             const double h = len * inv_mult;  // len holds the segment's base step
@@ -518,10 +580,17 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const double v0 = star_vx<NP, L>(s);
         if (dec) {
             rem -= ns * wcost;
-            if (lane == 0) __hip_atomic_store(s_rem + wv, rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            // (both operands through readfirstlane: a provably wave-uniform branch around each
+            done += ns * wcost;
+            if (lane == 0) {
+                __hip_atomic_store(s_rem + wv, rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(s_done + wv, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            // (operands through readfirstlane: a provably wave-uniform branch around each
             // s_setprio, which ignores EXEC -- cdna_hip_programming.md §5.5 T5)
-            if (__builtin_amdgcn_readfirstlane(rem_oth) < __builtin_amdgcn_readfirstlane(rem))
+            const int ro = __builtin_amdgcn_readfirstlane(rem_oth), rm = __builtin_amdgcn_readfirstlane(rem);
+            const int dn = __builtin_amdgcn_readfirstlane(done), dno = __builtin_amdgcn_readfirstlane(done_oth);
+            const bool high = part == 1 ? dn <= dno : (oth_head ? dn < dno : ro < rm);
+            if (__builtin_amdgcn_readfirstlane((int)high))
                 __builtin_amdgcn_s_setprio(2);
             else
                 __builtin_amdgcn_s_setprio(1);
@@ -642,7 +711,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 o[5] = rt_start;
                 o[6] = __builtin_amdgcn_s_memrealtime();
                 // (level field 7: a combiner)
-                o[7] = (unsigned long long)(comb ? 7 : lvl) | ((unsigned long long)d << 8) | ((unsigned long long)mult << 16);
+                o[7] = (unsigned long long)(comb || (part == 1 && bid < nA) ? 7 : lvl) | ((unsigned long long)d << 8) |
+                       ((unsigned long long)mult << 16) |
+                       ((unsigned long long)part << 24);
                 o[8] = (unsigned long long)redo;
                 o[9] = (unsigned long long)E;
                 o[10] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -656,7 +727,34 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             }
         };
 #endif
-        if (!comb) {
+        if (part == 1) {
+            // a head: hand the state over to the tail and leave
+            s_hos[hs][0][lane] = s.rx;
+            s_hos[hs][1][lane] = s.ry;
+            s_hos[hs][2][lane] = s.vx;
+            s_hos[hs][3][lane] = s.vy;
+            s_hos[hs][4][lane] = s.rz;
+            s_hos[hs][5][lane] = s.vz;
+            s_hos[hs][6][lane] = s.r;
+            s_hos[hs][7][lane] = s.ir;
+            if (lane == 0) {
+                s_hoe[hs] = s.encm;
+                s_hosp[hs] = spec_off;
+                __hip_atomic_store(&s_hof[hs], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (bid >= nA) {  // (type-B heads have no combiner role)
+#ifdef RVM_PROFILE
+                prof_dec(__builtin_amdgcn_s_memrealtime(), lvl);
+#endif
+                return;
+            }
+            // type A: this wave now combines its unit
+            if (lane == 0) {  // (its partner no longer keeps pace with it)
+                __hip_atomic_store(s_rem + wv, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(s_done + wv, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        if (!comb && part != 1) {
             // a level wave: publish this level's encounter / prior flags and leave
             if (lvl == 1) {
                 if (pl_idx == 0 && valid)
@@ -673,7 +771,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         }
         // the unit's combiner: consume epoch e once the three local levels have published it
         // (LDS counters) and level 1's values have landed (every lane's slot off the sentinel);
-        // lowest issue priority (it shares SIMD 0 / 1 with a level-3 wave)
+        // lowest issue priority (it shares a SIMD with a level-3 or level-2 wave)
         __builtin_amdgcn_s_setprio(0);
         unsigned spins = 0;
         bool hung = false;
@@ -804,11 +902,15 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
     // level-split layout (logl_kernel) when it lowers the heaviest SIMD's load: in steps per base
     // step, max(m3, m2 + m0, 2 m1) for one round of <= n_cu blocks, against m3 per round of
     // single-group blocks or max_i(m_i + m_{n-1-i}) per round of two-group blocks
-    int nA = 0;
+    int nA = 0, tB = 8, splitA = 0;
     if (P.lv_rv != nullptr && W <= P.lv_stride && P.n_levels == 4 && P.n_cu > 0) {
         const int* m = P.mult;
         const int units = 2 * groups;
-        const int na = groups, nb = (units + 7) / 8;
+        // type-B blocks carry 6 units' level 1 (two of them split head / tail) when the CUs allow,
+        // else 8
+        const int na = groups;
+        tB = na + (units + 5) / 6 <= P.n_cu ? 6 : 8;
+        const int nb = (units + tB - 1) / tB;
         const int c_dec = std::max(m[3], std::max(m[2] + m[0], 2 * m[1]));
         const int c_cpl = G == 1 ? m[3] * ((2 * groups + P.n_cu - 1) / P.n_cu)
                                  : std::max(m[0] + m[3], m[1] + m[2]) * ((groups + P.n_cu - 1) / P.n_cu);
@@ -818,6 +920,9 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
             nA = na;
             grid = dim3(na + nb, 1);
             block = dim3(8 * 64);
+            // level 0 split head / tail in the type-A blocks: the combiner starts with the head's
+            // hand-off, so the ring must hold every epoch of a direction
+            splitA = emax <= RVM_LS_RING ? 1 : 0;
             smem = smem_ls;
         }
     }
@@ -831,10 +936,10 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
                 lds_set = true;                                                                          \
             }                                                                                            \
             logl_kernel<NPV, D3V, true><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, \
-                                                                       logl, status, sa, nA);            \
+                                                                       logl, status, sa, nA, tB | (splitA << 8)); \
         } else                                                                                           \
             logl_kernel<NPV, D3V, false><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots,  \
-                                                                        rv_out, logl, status, sa, nA);   \
+                                                                        rv_out, logl, status, sa, nA, 8);  \
     } while (0)
     const bool inc = P.inclined != 0;
     switch (P.n_planets) {

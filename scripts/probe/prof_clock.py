@@ -56,7 +56,7 @@ def run(lib, W):
     b = b[used]
     lvl = b[:, 7] & 0xFF
     d = (b[:, 7] >> 8) & 0xFF
-    m = b[:, 7] >> 16
+    m = (b[:, 7] >> 16) & 0xFF
     cyc = b[:, 4] - b[:, 0]
     rt_us = (b[:, 6] - b[:, 5]) / 100.0
     ok = rt_us > 1.0
