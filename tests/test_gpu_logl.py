@@ -327,14 +327,15 @@ def test_fake_observation_matches_oracle():
     np.testing.assert_allclose(o.rvb, r2.rvb, rtol=0, atol=1e-10)
 
 
-@pytest.mark.parametrize("W", [4096, 4128, 6000, 8192])
+@pytest.mark.parametrize("W", [4096, 4128, 6000, 6400, 8192])
 def test_large_batch_size_independent_results(W):
     """A walker's logL does not depend on the batch it is launched in (W vs 1).  4096 runs one
     walker group per block; 4128 and 8192 exceed one block per CU and run two groups per block
-    with mirrored level order (4128: the last block's second group is partly empty); 6000 runs
-    the level-split layout (each level wave in its own block, levels meeting through HBM; the
-    last type-B block partly empty) and must give the same bits as the LDS-coupled single
-    launches."""
+    with mirrored level order (4128: the last block's second group is partly empty); 6000 and
+    6400 run the level-split layout (level 1 in type-B blocks meeting the unit's combiner through
+    HBM, level 0 split into a head and a tail; type-B blocks of 6 units with split pairs at 6000,
+    of 8 whole units at 6400, where 6-unit blocks would not fit the CUs; the last type-B block
+    partly empty) and must give the same bits as the LDS-coupled single launches."""
     obs = s2_obs_oracle()
     plan, _ = _plan(obs, S2_PLANETS, max_walkers=W)
     P = _ball(S2_PLANETS, W, seed=21)
