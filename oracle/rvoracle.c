@@ -25,7 +25,7 @@
  *   G1 (Pal + COM vectors), G2 (logp of HD155358 `sol`), G3 (1000-point RV curve), G4.
  *
  * It also holds `rvo_wh_*`: a plain-C restatement of the SAME Wisdom-Holman algorithm the HIP
- * kernel runs (Jacobi coordinates, DKD, epoch-aligned segments), used for the T1 parity tier
+ * kernel runs (Jacobi coordinates, KDK, epoch-aligned segments), used for the T1 parity tier
  * (GPU vs CPU, same algorithm) and as the "port" CPU baseline.  It is written independently of
  * the kernel source (no shared headers).
  */
@@ -570,9 +570,11 @@ void rvo_logl_ias15_batch(int W, int np, const double* pl, int has_hk, int has_i
 /* ------------------------------------------------------------------------------------------ */
 /* Wisdom-Holman (WHFast-style) restatement of the HIP kernel's algorithm (T1 tier).           */
 /*   Jacobi coordinates, Kepler drift (universal variables, Danby Stumpff functions),          */
-/*   interaction kick, DKD, epoch-aligned segments: the segment between consecutive epochs     */
+/*   interaction kick, KDK, epoch-aligned segments: the segment between consecutive epochs     */
 /*   (outward from t=0) of length D is cut into n = max(1, ceil(D/h - 1e-9)) equal steps,     */
-/*   each step D(h/2) K(h) D(h/2) with interior half-drifts merged.                            */
+/*   each step K(h/2) D(h) K(h/2) with interior half-kicks merged (the kernel evaluates the    */
+/*   interaction at a segment's last positions once for the closing and the next segment's      */
+/*   opening half kick; here both are evaluated: the same positions give the same values).      */
 /*   Epochs with t>=0 are visited ascending from 0, t<0 descending from 0.                     */
 /* ------------------------------------------------------------------------------------------ */
 static void stumpff(double z, double* c0, double* c1, double* c2, double* c3) {
@@ -813,10 +815,10 @@ static int wh_direction(int np, const double* pl, double hill_factor, const doub
         if (ns > 0) {
             /* the segment's base step, then the level's: (sign D / n1) * (1/sub) */
             const double h = (sign * D / n1) * (1.0 / sub);
-            wh_drift(&s, 0.5 * h);
+            wh_kick(&s, 0.5 * h);
             for (int j = 0; j < ns; j++) {
-                wh_kick(&s, h);
-                wh_drift(&s, (j == ns - 1) ? 0.5 * h : h);
+                wh_drift(&s, h);
+                wh_kick(&s, (j == ns - 1) ? 0.5 * h : h);
             }
         }
         if (s.enc) return RVO_ENCOUNTER;

@@ -173,17 +173,18 @@ __global__ __launch_bounds__(MAXT) void derivs_kernel(const DevPlan P, const Der
         s.encm = t0.encm;
     }
 
-    // ---- epochs outward from t = 0: DKD segments, Richardson-combined rv and its variations -----
+    // ---- epochs outward from t = 0: KDK segments, Richardson-combined rv and its variations -----
     double chi2 = 0.0, gi = 0.0, gj = 0.0, hij = 0.0;
     const int E = S.n_epochs;
     for (int e = 0; e < E; e++) {
         const int ns = S.seg_n[e] * mult;
         if (ns > 0) {
             const double h = S.seg_h1[e] * inv_mult;
-            drift_hd<D3>(s, 0.5 * h);
+            // kick-drift-kick (the likelihood kernel's segments, rvm_logl.hip segment_steps)
+            kick_hd_any<NP, L, D3>(s, 0.5 * h);
             for (int j = 0; j < ns; j++) {
-                kick_hd_any<NP, L, D3>(s, h);
-                drift_hd<D3>(s, j == ns - 1 ? 0.5 * h : h);
+                drift_hd<D3>(s, h);
+                kick_hd_any<NP, L, D3>(s, j == ns - 1 ? 0.5 * h : h);
             }
         }
         const HD v0 = star_vx_hd<NP, L>(s);

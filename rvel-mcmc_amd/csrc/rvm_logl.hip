@@ -7,7 +7,7 @@
 // Work decomposition:
 //   workgroup = 64/L walkers x one direction (blockIdx.y: 0 = epochs t >= 0, 1 = t < 0)
 //               x n_levels waves; wave L integrates the same walkers with mult[L]x the base steps
-//               (Wisdom-Holman DKD, epoch-aligned segments).  At every epoch each wave drops its
+//               (Wisdom-Holman KDK, epoch-aligned segments).  At every epoch each wave drops its
 //               64 model RVs into LDS, one barrier, and wave 0 forms the Richardson-extrapolated
 //               RV (sum_L w_L rv_L, the h^2 -> 0 limit) and accumulates chi2 in registers.
 //   lanes     = the planets of one walker sit on L = 1/2/4 adjacent lanes (one Kepler drift per
@@ -50,27 +50,34 @@ __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 #define PROF_COUNT(var)
 #endif
 
-// One epoch-to-epoch segment of ns Wisdom-Holman DKD steps of size h (ns is wave-uniform; the
-// step loop is unrolled by hand because the compiler will not unroll a runtime trip count around
-// the convergent DPP / ballot operations).
+// One epoch-to-epoch segment of ns Wisdom-Holman kick-drift-kick steps of size h (ns >= 1,
+// wave-uniform): K(h/2) [D(h) K(h)]^(ns-1) D(h) K(h/2).  kp holds the interaction at the current
+// positions (rvm_device.h kick_prep): evaluated at the end of the previous segment, it serves this
+// segment's opening half kick, and leaves holding the one at the next epoch.  (The step loop is
+// unrolled by hand: the compiler will not unroll a runtime trip count around the convergent DPP /
+// ballot operations.)
 template <int NT, bool GATED, bool D3, int NP, int L>
-__device__ __forceinline__ void segment_steps(Lane<NP>& s, double h, int ns, bool& bad) {
+__device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, bool& bad) {
     lane_set_step(s, h);
     const VConsts vk = vconsts_for<NT>();  // loop-invariant VGPR constants
-    drift<NT, GATED, D3>(s, 0.5 * h, bad, vk);
+    kick_apply<NP, true, D3>(s, kp);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
-        kick<NP, L, D3>(s, h, vk.c1875);
         drift<NT, GATED, D3>(s, h, bad, vk);
-        kick<NP, L, D3>(s, h, vk.c1875);
+        kp = kick_prep<NP, L, D3>(s, vk.c1875);
+        kick_apply<NP, false, D3>(s, kp);
         drift<NT, GATED, D3>(s, h, bad, vk);
+        kp = kick_prep<NP, L, D3>(s, vk.c1875);
+        kick_apply<NP, false, D3>(s, kp);
     }
     if (j < ns - 1) {
-        kick<NP, L, D3>(s, h, vk.c1875);
         drift<NT, GATED, D3>(s, h, bad, vk);
+        kp = kick_prep<NP, L, D3>(s, vk.c1875);
+        kick_apply<NP, false, D3>(s, kp);
     }
-    kick<NP, L, D3>(s, h, vk.c1875);
-    drift<NT, GATED, D3>(s, 0.5 * h, bad, vk);
+    drift<NT, GATED, D3>(s, h, bad, vk);
+    kp = kick_prep<NP, L, D3>(s, vk.c1875);
+    kick_apply<NP, true, D3>(s, kp);
 }
 
 // SPEC: run the segment with ungated drifts (rvm_device.h) and vote once at its end; if any lane
@@ -78,13 +85,14 @@ __device__ __forceinline__ void segment_steps(Lane<NP>& s, double h, int ns, boo
 // redo it gated.  Used on the fine levels, where such steps are rare.  Returns whether the
 // segment was redone (wave-uniform).  Either way every lane ends bit-identical to a gated run.
 template <int NT, bool SPEC, bool D3, int NP, int L>
-__device__ __forceinline__ bool segment(Lane<NP>& s, double h, int ns, int& redo) {
+__device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int& redo) {
     bool bad = false;
     if constexpr (SPEC) {
         const double rx = s.rx, ry = s.ry, vx = s.vx, vy = s.vy, r = s.r, ir = s.ir;
         const double rz = s.rz, vz = s.vz;
         const uint64_t encm = s.encm;
-        segment_steps<NT, false, D3, NP, L>(s, h, ns, bad);
+        const KickPrep<NP> kp0 = kp;
+        segment_steps<NT, false, D3, NP, L>(s, kp, h, ns, bad);
         if (__builtin_expect(ballot(bad) != 0, 0)) {
             PROF_COUNT(redo);
             s.rx = rx;
@@ -96,11 +104,12 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, double h, int ns, int& redo
             s.r = r;
             s.ir = ir;
             s.encm = encm;
-            segment_steps<NT, true, D3, NP, L>(s, h, ns, bad);
+            kp = kp0;
+            segment_steps<NT, true, D3, NP, L>(s, kp, h, ns, bad);
             return true;
         }
     } else {
-        segment_steps<NT, true, D3, NP, L>(s, h, ns, bad);
+        segment_steps<NT, true, D3, NP, L>(s, kp, h, ns, bad);
     }
     return false;
 }
@@ -438,11 +447,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     s.ir = 1.0 / s.r;
     s.encm = 0;
     lane_finish(s);
-    if (S.n_epochs > 0) {  // REBOUND checks exit_min_distance before the first step too -- when
-        Lane<NP> t0 = s;   // it integrates at all: get_rv of an empty epoch list never does
-        kick<NP, L, D3>(t0, 0.0);
-        s.encm = t0.encm;
-    }
+    // the interaction at t = 0 (the first segment's opening half kick) and REBOUND's check of
+    // exit_min_distance before the first step -- when it integrates at all: get_rv of an empty
+    // epoch list never does
+    KickPrep<NP> kp{};
+    if (S.n_epochs > 0) kp = kick_prep<NP, L, D3>(s, 1.875);
 
     PROF_T(t_p3);  // lane constants, encounter check at t = 0
     if (!dec) {
@@ -542,6 +551,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         s.encm = __builtin_amdgcn_readfirstlane(s_hoe[hs] & 0xFFFFFFFFull) |
                  ((unsigned long long)__builtin_amdgcn_readfirstlane(s_hoe[hs] >> 32) << 32);
         spec_off = __builtin_amdgcn_readfirstlane(s_hosp[hs]);
+        // the interaction at the hand-off epoch, from the same positions: the head's bits (its
+        // encounter test repeats on positions the head already tested)
+        kp = kick_prep<NP, L, D3>(s, 1.875);
     }
     int n1 = e_lo < E ? l_n[e_lo] : 0;
     double len = e_lo < E ? l_len[e_lo] : 0.0;
@@ -564,17 +576,17 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 // orbits keep needing the general solver (short periods, high eccentricity in a
                 // wide ensemble) then run gated for a while instead of paying for redos
                 if (spec_off == 0) {
-                    if (segment<6, true, D3, NP, L>(s, h, ns, redo)) spec_off = 4;
+                    if (segment<6, true, D3, NP, L>(s, kp, h, ns, redo)) spec_off = 4;
                 } else {
-                    segment<6, false, D3, NP, L>(s, h, ns, redo);
+                    segment<6, false, D3, NP, L>(s, kp, h, ns, redo);
                     spec_off--;
                 }
             } else if (nt <= 6)
-                segment<6, false, D3, NP, L>(s, h, ns, redo);
+                segment<6, false, D3, NP, L>(s, kp, h, ns, redo);
             else if (nt == 7)
-                segment<7, false, D3, NP, L>(s, h, ns, redo);
+                segment<7, false, D3, NP, L>(s, kp, h, ns, redo);
             else
-                segment<8, false, D3, NP, L>(s, h, ns, redo);
+                segment<8, false, D3, NP, L>(s, kp, h, ns, redo);
         }
         PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
