@@ -244,6 +244,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             part = tB == 8 || wv < 4 ? 0 : ((wv & 1) ? 2 : 1);
             hs = (wv - 4) >> 1;
         }
+        // wave-uniform in the compiler's eyes (SGPRs): branches on them stay scalar and the state
+        // they select (the encounter mask) stays in SGPRs
+        part = __builtin_amdgcn_readfirstlane(part);
+        hs = __builtin_amdgcn_readfirstlane(hs);
+        idle = __builtin_amdgcn_readfirstlane((int)idle) != 0;
         grp = 0;
         G = 1;
         d = unit & 1;
@@ -502,7 +507,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     __shared__ int s_rem[8], s_done[8];
     const int wcost = spec ? 10 : 12;  // gated steps (ballot per drift) cost ~20 % more (timing build)
     const int esplit = lvl == 0 ? S.split0 : S.split1;  // head / tail boundary of a split level
-    const int e_lo = part == 2 ? esplit : 0, e_hi = part == 1 ? esplit : E;
+    // (readfirstlane: wave-uniform in the compiler's eyes too -- a per-lane epoch range turns the
+    // step loops into exec-masked loops with a VGPR trip counter)
+    const int e_lo = __builtin_amdgcn_readfirstlane(part == 2 ? esplit : 0);
+    const int e_hi = __builtin_amdgcn_readfirstlane(part == 1 ? esplit : E);
     int rem = live ? mult * (S.n_steps - (part == 2 ? (lvl == 0 ? S.pre0 : S.pre1) : 0)) * wcost : 0;
     // a head runs first (its tail, on another SIMD, cannot start before it ends): it publishes more
     // remaining work than any whole level has

@@ -347,16 +347,18 @@ def test_large_batch_size_independent_results(W):
     assert np.isfinite(big).all()
 
 
-@pytest.mark.parametrize("one_sided", [False, True])
-def test_level_split_ring_wrap_and_empty_direction(one_sided):
+@pytest.mark.parametrize("one_sided,npoints", [(False, 300), (True, 300), (True, 100)])
+def test_level_split_ring_wrap_and_empty_direction(one_sided, npoints):
     """Level-split hand-off (rvm_logl.hip): levels 3, 2, 0 pass their per-epoch RVs to the unit's
     combiner through an LDS ring of RVM_LS_RING = 64 epochs and wait when a whole ring ahead;
     level 1 through HBM granules.  301 epochs (151 forward) wrap the ring and exercise that wait;
-    the one-sided set (all epochs at t >= 0) leaves the backward units with no epoch at all.  Every
-    walker gives the bits (logL, status, model RVs) of its LDS-coupled single launch, and T1
-    against the oracle on a subset."""
+    the one-sided sets (all epochs at t >= 0) leave the backward units with no epoch at all (with
+    51 forward epochs the ring holds a whole direction, so level 0 runs split into a head that
+    then combines and a tail: the empty direction's head hands over at once).  Every walker gives
+    the bits (logL, status, model RVs) of its LDS-coupled single launch, and T1 against the
+    oracle on a subset."""
     np.random.seed(13)
-    obs = O.fake_obs(S2_PLANETS, Npoints=300, error=1.5e-4, errorVar=2.5e-5, tmax=150.)
+    obs = O.fake_obs(S2_PLANETS, Npoints=npoints, error=1.5e-4, errorVar=2.5e-5, tmax=150. * npoints / 300)
     if one_sided:
         e = np.zeros(0)
         obs = O.OracleObs(tf=obs.tf, rvf=obs.rvf, errorf=obs.errorf, tb=e, rvb=e, errorb=e, Npoints=obs.Npoints)
