@@ -166,7 +166,12 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         {
             const int nlv = cfg->n_levels;
             double f0 = 0.5;
-            if (nlv == 4) f0 = std::min(1.0, std::max(0.0, (double)(mult[3] + mult[0] - mult[2]) / (2.0 * mult[0])));
+            // (+0.11: the tail's SIMD runs level 3 alone until the head ends, at the lone-wave rate;
+            // measured at 6144 slots, scripts/probe/prof_clock.py with RVM_LS_F0: 0.625 -> SIMD 0/1
+            // end 6 % after SIMD 2/3, 0.74 -> within 1 %)
+            if (nlv == 4) f0 = (double)(mult[3] + mult[0] - mult[2]) / (2.0 * mult[0]) + 0.11;
+            if (const char* ef = getenv("RVM_LS_F0")) f0 = atof(ef);  // (experiments: scripts/probe)
+            f0 = std::min(1.0, std::max(0.0, f0));
             const double fr[2] = {f0, 0.5};
             int32_t sp[2] = {0, 0}, pr[2] = {0, 0};
             for (int q = 0; q < 2; q++) {

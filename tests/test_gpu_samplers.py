@@ -328,6 +328,35 @@ def test_reference_api_ensemble_and_mh_step():
     assert tries >= 1 and np.isfinite(mh.state.logp)
 
 
+def test_reference_lnprob_shim():
+    """mcmc.lnprob (mcmc.py:28-35), the emcee callback: the State's logp for a valid vector,
+    -inf through priorHard (state.py:299-315), and -inf when get_logp raises -- here the
+    Encounter of a near-coorbital pair (rebound.Encounter in the reference, any exception there)."""
+    from rvmcmc import mcmc
+
+    s, obs = _state_and_obs()
+    e = mcmc.Mcmc(s, obs)
+    x = e.state.get_params().copy()
+    lp = mcmc.lnprob(x, e)
+    ref = s.deepcopy()
+    ref.set_params(x)
+    assert np.isfinite(lp) and lp == ref.get_logp(obs)
+    keys = e.state.get_rawkeys()
+    a_idx = [i for i, k in enumerate(keys) if k == "a"]
+    bad = x.copy()
+    bad[a_idx[0]] = 0.01  # a <= 0.02
+    assert mcmc.lnprob(bad, e) == -np.inf
+    enc = x.copy()
+    for k in ("h", "k", "l"):  # planet 2 on planet 1's orbit, 1 % wider: inside the exit distance at t = 0
+        ki = [i for i, kk in enumerate(keys) if kk == k]
+        enc[ki[1]] = enc[ki[0]]
+    enc[a_idx[1]] = enc[a_idx[0]] * 1.01
+    assert mcmc.lnprob(enc, e) == -np.inf
+    with pytest.raises(Exception):
+        e.state.get_logp(obs)  # (the State itself raises; the shim maps it to -inf)
+    assert mcmc.lnprob(x, e) == lp  # and recovers
+
+
 def test_smala_chains_run():
     from rvmcmc.smala import SmalaChains
 
