@@ -196,11 +196,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // so wave i of group 1 shares a SIMD with wave i of group 0 and every SIMD carries
     // mult[i] + mult[nl-1-i] steps per base step instead of up to 2 mult[nl-1].
     //
-    // Level-split layout (nA > 0; four levels m0 < m1 < m2 < m3, 1-D grid of 8-wave blocks, wave i
-    // on SIMD i % 4): a unit = (walker group, direction), u = 2 group + direction.  Blocks b < nA
-    // carry levels (3, 3, 2, 2, -, -, 0, 0) of units 2b and 2b + 1 -- SIMD loads m3, m3, m2 + m0,
-    // m2 + m0; waves 4 and 5 are the two units' combiners -- and the others level 1 of eight
-    // units (2 m1 on every SIMD).  (136 VGPRs per lane: one such block per CU.)  Levels 3, 2, 0 of
+    // Level-split layout (nA > 0; four levels m0 < m1 < m2 < m3, 1-D grid of 8-wave blocks, one
+    // per CU, wave i on SIMD i % 4): a unit = (walker group, direction), u = 2 group + direction.
+    // Type-A blocks (b < nA) carry levels 3, 2, 0 of units 2b, 2b + 1 and their combiners, type-B
+    // blocks level 1 (the roles below).  Levels 3, 2, 0 of
     // a unit hand their star velocities to the combiner through an LDS ring (with per-level epoch
     // counters), level 1 -- in a type-B block on another CU, usually another XCD -- through HBM, one
     // agent-scope 8-byte store per walker and epoch whose arrival is the value itself (the slot holds
@@ -223,7 +222,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     //   type A, units 2b + (wv & 1): waves 0, 1 level 3; 2, 3 level 2; and either (splitA) 6, 7 the
     //     heads of level 0 (epochs [0, split0)), then the units' combiners, with 4, 5 its tails on
     //     SIMDs 0, 1 -- SIMD loads m3 + m0 (1 - f), m2 + m0 f with f = split0's share of the steps
-    //     (0.625 at 4..7: 8.5, 8.5); or 6, 7 level 0 whole and 4, 5 the combiners (10, 7)
+    //     (rvm_plan_create: 0.735 at 4..7, 0.11 above the 8.5 / 8.5 balance because the tail's SIMD
+    //     runs level 3 alone until the head ends); or 6, 7 level 0 whole and 4, 5 the combiners
+    //     from the start (10, 7) when a direction has more epochs than the ring holds
     //   type B, tB = 8 units of level 1 per block: waves 0..7 one each (2 m1 per SIMD); or tB = 6
     //     (all CUs in use): waves 0..3 whole, 4 / 5 head / tail of unit 4, 6 / 7 of unit 5 (1.5 m1)
     const int tB = lsm & 0xFF;
@@ -231,7 +232,6 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const int tsk = wv < 4 || tB == 8 ? wv : (wv < 6 ? 4 : 5);  // type-B task of this wave
     auto unit_of = [&]() { return bid < nA ? 2 * bid + (wv & 1) : tB * (bid - nA) + tsk; };
     int part = 0, hs = 0;
-    bool skip = false;  // no role (the blocks' last waves)
     if (dec) {
         const int b = bid;
         const int unit = __builtin_amdgcn_readfirstlane(unit_of());  // wave-uniform (SGPRs)
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         d = blockIdx.y;
         w0 = (blockIdx.x * G + grp) * WPB;  // first walker of the group
     }
-    const bool live = w0 < W && !idle && !skip;  // level-split: waves past the last unit only help stage the schedule
+    const bool live = w0 < W && !idle;  // level-split: waves past the last unit only help stage the schedule
     const bool comb = dec && idle;       // level-split: this unit's combiner from the start
     const int lane = threadIdx.x & 63;
     const int slot = lane / L;                     // walker slot within the group
