@@ -254,10 +254,13 @@ class MhChains:
         self.iteration, self.seed, self.step_size = int(d["iteration"]), int(d["seed"]), float(d["step_size"])
         self.Q = torch.empty_like(self.X)
 
-    def step(self, draws_propose=None, draws_accept=None, fused=True):
-        """One MH step of every chain.  Philox draws: ONE launch (rvm_mh_step: proposal, likelihood
-        and accept fused); injected draws, or fused=False: propose / likelihood / accept launches
-        (bit-identical for the same draws)."""
+    def step(self, draws_propose=None, draws_accept=None, fused=False):
+        """One MH step of every chain: propose / likelihood / accept launches, or (fused=True,
+        Philox draws) ONE launch, rvm_mh_step: proposal, likelihood and accept fused; bit-identical
+        for the same draws.  The separate launches are the default: in the level-split layout every
+        level wave of a walker forms its proposal (Philox + Box-Muller per parameter) in its
+        prologue, which costs more than the two launches it saves (4096 chains: 14.6M vs 14.2M
+        chain-steps/s, profiles/r02f_configs.jsonl)."""
         import torch
 
         st = _lib.stream_handle()
