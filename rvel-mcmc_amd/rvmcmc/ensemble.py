@@ -200,6 +200,12 @@ class EnsembleSampler:
         self._c_full = torch.empty((dim, self.halfk), **f64)
         self._gather = torch.empty(self.world * dim * n, **f64) if self.world > 1 else None
         self._gather_aos = torch.empty((self.halfk, dim), **f64) if self.world > 1 else None
+        # both halves' walker-major mirrors in one buffer (pos_aos[h] are views of it): at N > 1 a
+        # speculative iteration gathers both with ONE all-gather
+        self._aos_pair = torch.empty((2, n, dim), **f64)
+        self.pos_aos = [self._aos_pair[0], self._aos_pair[1]]
+        self._gather_pair = torch.empty(self.world * 2 * n * dim, **f64) if self.world > 1 else None
+        self._c01 = torch.empty((2, self.halfk, dim), **f64) if self.world > 1 else None
         self._aos_stale = True  # pos_aos (walker-major mirrors for the fused path) out of date
         self.naccepted = torch.zeros(2 * n, dtype=torch.int32, device=self.device)
         self.nevals = 0
@@ -211,7 +217,6 @@ class EnsembleSampler:
         self._st_spec = torch.empty(3 * n, dtype=torch.int32, device=self.device)
         self._dec = torch.zeros(n, dtype=torch.int32, device=self.device)
         self._dec_all = torch.empty(self.halfk, dtype=torch.int32, device=self.device) if self.world > 1 else None
-        self._gather_aos0 = torch.empty((self.halfk, dim), **f64) if self.world > 1 else None
         self._spec_pays = None
         # one launch per half-step (rvm_stretch_half_step) unless draws are injected or the ops
         # (e.g. the CPU restatements of the distributed tests) provide only the three-step path
@@ -259,8 +264,13 @@ class EnsembleSampler:
         torch.distributed.all_gather_into_tensor(self._gather_aos, self.pos_aos[other], group=self.group)
         return self._gather_aos
 
+    def _set_aos(self, a0, a1):
+        self._aos_pair[0].copy_(a0)
+        self._aos_pair[1].copy_(a1)
+        self.pos_aos = [self._aos_pair[0], self._aos_pair[1]]
+
     def _refresh_aos(self):
-        self.pos_aos = [p.t().contiguous() for p in self.pos]
+        self._set_aos(self.pos[0].t(), self.pos[1].t())
         self._aos_stale = False
 
     def half_step(self, X0, lnp0, Xc, half, draws_propose=None, draws_accept=None):
@@ -294,7 +304,7 @@ class EnsembleSampler:
             raise ValueError(f"positions must be [{self.k}][{self.dim}]")
         s0, s1 = self.local_slices()
         self.pos = [Xg[s0].t().contiguous(), Xg[s1].t().contiguous()]
-        self.pos_aos = [Xg[s0].contiguous(), Xg[s1].contiguous()]
+        self._set_aos(Xg[s0], Xg[s1])
         self._aos_stale = False
         self.lnp = [None, None]
 
@@ -325,22 +335,28 @@ class EnsembleSampler:
             self.half_step(B, self.lnp[1], A, 1)
         self.iteration += 1
 
-    def _speculative_iteration(self):
-        """Both half-steps as one launch over 3 nloc walker slots (half 0, and half 1 against both
-        possible positions of each partner) plus a small accept launch; bit-identical to two
-        half_step calls.  Collectives (N > 1): the two halves' walker-major mirrors before the
-        launch, half 0's decisions between the two launches."""
+    def gather_mirrors(self):
+        """Both halves' walker-major mirrors [W/2][dim] in global order: this rank's own at N = 1,
+        else one all-gather of the pair buffer re-laid out by one copy."""
         torch = _torch()
         if self._aos_stale:
             self._refresh_aos()
         if self.world == 1:
-            c0, c1 = self.pos_aos
-            dec_all = self._dec
-        else:
-            torch.distributed.all_gather_into_tensor(self._gather_aos0, self.pos_aos[0], group=self.group)
-            torch.distributed.all_gather_into_tensor(self._gather_aos, self.pos_aos[1], group=self.group)
-            c0, c1 = self._gather_aos0, self._gather_aos
-            dec_all = self._dec_all
+            return self.pos_aos[0], self.pos_aos[1]
+        torch.distributed.all_gather_into_tensor(self._gather_pair, self._aos_pair.view(-1), group=self.group)
+        g = self._gather_pair.view(self.world, 2, self.nloc, self.dim)
+        self._c01.view(2, self.world, self.nloc, self.dim).copy_(g.permute(1, 0, 2, 3))
+        return self._c01[0], self._c01[1]
+
+    def _speculative_iteration(self):
+        """Both half-steps as one launch over 3 nloc walker slots (half 0, and half 1 against both
+        possible positions of each partner) plus a small accept launch; bit-identical to two
+        half_step calls.  Collectives (N > 1): the two halves' walker-major mirrors before the
+        launch (one all-gather of the pair buffer, re-laid out by one copy), half 0's decisions
+        between the two launches."""
+        torch = _torch()
+        c0, c1 = self.gather_mirrors()
+        dec_all = self._dec if self.world == 1 else self._dec_all
         self.ops.iteration_begin(c0, c1)
         if self.world > 1:
             torch.distributed.all_gather_into_tensor(self._dec_all, self._dec, group=self.group)

@@ -2,7 +2,7 @@
 # Round evidence in one GPU call: GPU tests, smoke, the PMC passes over the bench's own launches
 # (summary keyed to the kernel sources, copied to profiles/pmc_latest.json for bench.py), bench
 # (N=1, with ESS and CPU baseline), rocprofv3 --kernel-trace --stats of a short bench run, every
-# BASELINE config.  Each GPU step has its own time limit; the chain stops at the first failure.
+# BASELINE config, and the 2-rank rehearsal of the sharded bench.  Each GPU step has its own time limit; the chain stops at the first failure.
 # SKIP_TESTS=1 / SKIP_CONFIGS=1 / SKIP_PMC=1 leave those steps out.
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -21,6 +21,8 @@ if [ "${SKIP_PMC:-0}" != 1 ]; then
 fi
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
+# the N > 1 flow of bench.py (2 ranks on this one GPU over gloo: correctness, not scaling)
+bash scripts/gpu_rehearse_dist.sh > /dev/null
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 --ess-iters 0 --no-cpu > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err"
 cd "$R"
