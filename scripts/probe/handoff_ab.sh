@@ -1,4 +1,7 @@
 #!/bin/bash
+# (History: round 1's level-split layout with the last-arriver combine; the lib_*.so variants were
+# built from commit 119fcdb with its RVM_EXP_* macros, which the current kernel no longer has.
+# The current layout is measured with scripts/probe/prof_clock.py.)
 # A/B of the level-split hand-off (plain 6144-walker launches, S2): product library, combine
 # skipped, hand-off writes + combine skipped, type-B blocks first, LDS-coupled layout.
 set -euo pipefail
