@@ -343,7 +343,26 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                                     : stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wl), sa.iteration, sa.half);
         l_q[(R + 2) * GW + gi] = sa.lnp[wl];
     }
-#define prm(r) stage_row(stager, l_q, GW, gi, (r), walker_param(mapped, params, W, wk, sa, (r), zst, jst, kind, zp, jp))
+    // the walker's parameter rows; a fused MH step spreads its Box-Muller proposals over the
+    // walker's planet lanes (lane q forms rows q, q + L, ...; DPP broadcast within the group), so
+    // each lane draws ceil(R / L) normals instead of R -- same bits, a shorter prologue
+    constexpr int R = PR * NP;
+    double rowv[R];
+    if (L > 1 && mh) {
+        constexpr int NI = (R + L - 1) / L;
+#pragma unroll
+        for (int i = 0; i < NI; i++) {
+            const int r = L * i + pl_idx < R ? L * i + pl_idx : R - 1;
+            const double v = walker_param(true, params, W, wk, sa, r, zst, jst, kind, zp, jp);
+#pragma unroll
+            for (int q = 0; q < L; q++)
+                if (L * i + q < R) rowv[L * i + q] = grp_get<L>(v, q);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; r++) rowv[r] = walker_param(mapped, params, W, wk, sa, r, zst, jst, kind, zp, jp);
+    }
+#define prm(r) stage_row(stager, l_q, GW, gi, (r), rowv[(r)])
     Lane<NP> s;
     double pa[NP], ph[NP], pk[NP], pl[NP], pix[NP], piy[NP];
     int status = RVM_STATUS_OK;
@@ -656,7 +675,6 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     }
 #undef prm
     const int encflag = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
-    constexpr int R = PR * NP;
     // ---- the two directions of a walker meet: the second to arrive finishes it ----------------
     // (one agent-scope exchange carries the other direction's result: no fence, no barrier).
     // row(r), z, u3, lnp0: the walker's proposal and accept inputs (fused stretch half-step)

@@ -254,13 +254,13 @@ class MhChains:
         self.iteration, self.seed, self.step_size = int(d["iteration"]), int(d["seed"]), float(d["step_size"])
         self.Q = torch.empty_like(self.X)
 
-    def step(self, draws_propose=None, draws_accept=None, fused=False):
-        """One MH step of every chain: propose / likelihood / accept launches, or (fused=True,
-        Philox draws) ONE launch, rvm_mh_step: proposal, likelihood and accept fused; bit-identical
-        for the same draws.  The separate launches are the default: in the level-split layout every
-        level wave of a walker forms its proposal (Philox + Box-Muller per parameter) in its
-        prologue, which costs more than the two launches it saves (4096 chains: 14.6M vs 14.2M
-        chain-steps/s, profiles/r02f_configs.jsonl)."""
+    def step(self, draws_propose=None, draws_accept=None, fused=True):
+        """One MH step of every chain: (fused=True, the default, with Philox draws) ONE launch,
+        rvm_mh_step: proposal, likelihood and accept fused; or (fused=False, or injected draws) the
+        propose / likelihood / accept launches; bit-identical for the same draws.  In the
+        level-split layout every level wave of a walker forms its proposal in its prologue; the
+        walker's planet lanes share the Box-Muller draws (rvm_logl.hip), and the fused launch is
+        ahead (4096 chains: 15.3-15.6M vs 14.8-15.1M chain-steps/s, profiles/r02h_configs.jsonl)."""
         import torch
 
         st = _lib.stream_handle()

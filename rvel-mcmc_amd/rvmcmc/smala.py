@@ -194,16 +194,14 @@ class SmalaChains:
     def linalg_failures(self):
         return int(self.failures.sum().item())
 
-    def step(self, z=None, u=None, fused=False):
+    def step(self, z=None, u=None, fused=True):
         """One SMALA step of every chain; z [C][P] / u [C] inject the normals / uniforms.
 
-        fused=True: three launches -- rvm_smala_propose, the stencil likelihood launch
+        fused=True (default): three launches -- rvm_smala_propose, the stencil likelihood launch
         (rvm_smala_stencil_logl; exact: rvm_logl_derivs) and rvm_smala_derive_accept
-        (rvm_smala_metric_accept); fused=False (default) runs the separate fd / logl / derive /
-        accept launches (bit-identical).  The separate launches are the default: the stencil
-        launch's level-split layout forms every stencil point once per level wave, which costs
-        more than the launches saved (256 chains: 491k vs 475k chain-steps/s,
-        profiles/r02f_configs.jsonl)."""
+        (rvm_smala_metric_accept); fused=False runs the separate fd / logl / derive / accept
+        launches (bit-identical; 256 chains: 523k vs 485k chain-steps/s fused vs separate,
+        profiles/r02h_configs.jsonl)."""
         st_h = _lib.stream_handle()
         zp = 0
         if z is not None:

@@ -80,7 +80,7 @@ def config3():
     return {"config": "3: affine, 4096 walkers, HD155358.vels", **_affine(s, obs, 4096)}
 
 
-def config4(chains=256, steps=10, fused=True):
+def config4(chains=256, steps=100, fused=True):
     np.random.seed(2017)
     s = State(planets=[dict(p) for p in S2])
     obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
@@ -123,7 +123,7 @@ def config4u():
     return config4(fused=False)
 
 
-def config1b(chains=4096, steps=20, fused=True):
+def config1b(chains=4096, steps=200, fused=True):
     """Batched MH (MhChains: mcmc.py:107-121 for every chain at once), 4096 chains on the
     2-planet synthetic config, mcmc_benchmark_mh.py:52 scales, step 1e-3."""
     np.random.seed(2017)
