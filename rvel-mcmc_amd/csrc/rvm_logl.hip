@@ -550,6 +550,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #endif
     int redo = 0;      // speculative segments redone gated (counted in the timing build only)
     int spec_off = 0;  // wave-uniform: segments left to run gated after a redo
+    int spec_bo = 4;   // wave-uniform: the next back-off, doubled by each redo (a walker whose orbit
+                       // keeps needing the general solver), back to 4 after a clean segment
     double chi2 = 0.0;
     // level-split hand-off: level 1's column of P.lv_rv (one epoch row per epoch); the other levels'
     // slot in the block's LDS ring ([unit ul][local level ks][RING][WPB] doubles after the schedule)
@@ -577,7 +579,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         s.ir = s_hos[hs][7][lane];
         s.encm = __builtin_amdgcn_readfirstlane(s_hoe[hs] & 0xFFFFFFFFull) |
                  ((unsigned long long)__builtin_amdgcn_readfirstlane(s_hoe[hs] >> 32) << 32);
-        spec_off = __builtin_amdgcn_readfirstlane(s_hosp[hs]);
+        spec_off = __builtin_amdgcn_readfirstlane(s_hosp[hs]) & 0xFFFF;
+        spec_bo = __builtin_amdgcn_readfirstlane(s_hosp[hs]) >> 16;
         // the interaction at the hand-off epoch, from the same positions: the head's bits (its
         // encounter test repeats on positions the head already tested)
         kp = kick_prep<NP, L, D3>(s, 1.875);
@@ -603,7 +606,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 // orbits keep needing the general solver (short periods, high eccentricity in a
                 // wide ensemble) then run gated for a while instead of paying for redos
                 if (spec_off == 0) {
-                    if (segment<6, true, D3, NP, L>(s, kp, h, ns, redo)) spec_off = 4;
+                    if (segment<6, true, D3, NP, L>(s, kp, h, ns, redo)) {
+                        spec_off = spec_bo;
+                        spec_bo = spec_bo < 64 ? 2 * spec_bo : 64;
+                    } else {
+                        spec_bo = 4;
+                    }
                 } else {
                     segment<6, false, D3, NP, L>(s, kp, h, ns, redo);
                     spec_off--;
@@ -777,7 +785,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             s_hos[hs][7][lane] = s.ir;
             if (lane == 0) {
                 s_hoe[hs] = s.encm;
-                s_hosp[hs] = spec_off;
+                s_hosp[hs] = spec_off | (spec_bo << 16);
                 __hip_atomic_store(&s_hof[hs], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             if (bid >= nA) {  // (type-B heads have no combiner role)
