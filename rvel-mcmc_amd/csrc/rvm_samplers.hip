@@ -56,6 +56,11 @@ __global__ void stretch_accept_kernel(int P, int n0, int64_t s0_begin, double* _
 // threads [n, 2n) refresh half 0's walker-major mirror rows that the first half-step changed.
 // A partner on this rank is read from x0 (already updated); any other is rebuilt from the
 // iteration's starting positions and its own draws -- the same bits either way.
+// MAXD > 0 (dim <= MAXD): every load a walker may need -- both variants' logl, the partner rows
+// (x0, or c0 and c1 for both outcomes), its own row -- is issued before any of them is used, so a
+// thread waits for one round of memory latency instead of one per dependent load and dimension
+// (the kernel is latency-bound: n threads, a few loads each).  MAXD = 0: any dim.
+template <int MAXD>
 __global__ void stretch_iteration_end_kernel(const IterEndArgs g) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = g.n, P = g.dim;
@@ -64,31 +69,74 @@ __global__ void stretch_iteration_end_kernel(const IterEndArgs g) {
         double z;
         int j;
         stretch_draw(g.seed, (uint64_t)(g.s1_begin + k), g.iteration, 1u, g.a, g.n_half, z, j);
-        const int v = g.dec_all[j] != 0 ? 1 : 0;
         const int64_t jl = (int64_t)j - g.s0_begin;
         const bool local = jl >= 0 && jl < n;
-        const double lnew = g.lnp_spec[(size_t)(1 + v) * n + k];
-        if (g.lnp_new_out) g.lnp_new_out[k] = lnew;
-        if (g.status_new_out) g.status_new_out[k] = g.st_spec[(size_t)(1 + v) * n + k];
-        const double u3 = stretch_u3(g.seed, (uint64_t)(g.s1_begin + k), g.iteration, 1u);
-        if (stretch_accepts(P, z, lnew, g.lnp1[k], u3)) {
+        if constexpr (MAXD > 0) {
             double zp = 0.0;
             int jp = 0;
-            if (!local && v) stretch_draw(g.seed, (uint64_t)j, g.iteration, 0u, g.a, g.n_half, zp, jp);
-            for (int p = 0; p < P; p++) {
-                double c;
-                if (local) {
-                    c = g.x0[(size_t)p * n + jl];
-                } else {
-                    c = g.c0[(size_t)j * P + p];
-                    if (v) c = stretch_q(g.c1[(size_t)jp * P + p], zp, c);
+            if (!local) stretch_draw(g.seed, (uint64_t)j, g.iteration, 0u, g.a, g.n_half, zp, jp);
+            const int dv = g.dec_all[j];
+            const double l1 = g.lnp_spec[(size_t)n + k], l2 = g.lnp_spec[(size_t)2 * n + k];
+            const int32_t s1 = g.st_spec[(size_t)n + k], s2 = g.st_spec[(size_t)2 * n + k];
+            const double lnp_old = g.lnp1[k];
+            double xv[MAXD], cv[MAXD], cq[MAXD];
+#pragma unroll
+            for (int p = 0; p < MAXD; p++) {
+                if (p < P) {
+                    xv[p] = g.x1[(size_t)p * n + k];
+                    if (local) {
+                        cv[p] = g.x0[(size_t)p * n + jl];
+                        cq[p] = 0.0;
+                    } else {
+                        cv[p] = g.c0[(size_t)j * P + p];
+                        cq[p] = g.c1[(size_t)jp * P + p];
+                    }
                 }
-                const double q = stretch_q(c, z, g.x1[(size_t)p * n + k]);
-                g.x1[(size_t)p * n + k] = q;
-                if (g.x1_aos) g.x1_aos[(size_t)k * P + p] = q;
             }
-            g.lnp1[k] = lnew;
-            if (g.accepted1) g.accepted1[k] += 1;
+            const int v = dv != 0 ? 1 : 0;
+            const double lnew = v ? l2 : l1;
+            if (g.lnp_new_out) g.lnp_new_out[k] = lnew;
+            if (g.status_new_out) g.status_new_out[k] = v ? s2 : s1;
+            const double u3 = stretch_u3(g.seed, (uint64_t)(g.s1_begin + k), g.iteration, 1u);
+            if (stretch_accepts(P, z, lnew, lnp_old, u3)) {
+#pragma unroll
+                for (int p = 0; p < MAXD; p++) {
+                    if (p < P) {
+                        double c = cv[p];
+                        if (!local && v) c = stretch_q(cq[p], zp, c);
+                        const double q = stretch_q(c, z, xv[p]);
+                        g.x1[(size_t)p * n + k] = q;
+                        if (g.x1_aos) g.x1_aos[(size_t)k * P + p] = q;
+                    }
+                }
+                g.lnp1[k] = lnew;
+                if (g.accepted1) g.accepted1[k] += 1;
+            }
+        } else {
+            const int v = g.dec_all[j] != 0 ? 1 : 0;
+            const double lnew = g.lnp_spec[(size_t)(1 + v) * n + k];
+            if (g.lnp_new_out) g.lnp_new_out[k] = lnew;
+            if (g.status_new_out) g.status_new_out[k] = g.st_spec[(size_t)(1 + v) * n + k];
+            const double u3 = stretch_u3(g.seed, (uint64_t)(g.s1_begin + k), g.iteration, 1u);
+            if (stretch_accepts(P, z, lnew, g.lnp1[k], u3)) {
+                double zp = 0.0;
+                int jp = 0;
+                if (!local && v) stretch_draw(g.seed, (uint64_t)j, g.iteration, 0u, g.a, g.n_half, zp, jp);
+                for (int p = 0; p < P; p++) {
+                    double c;
+                    if (local) {
+                        c = g.x0[(size_t)p * n + jl];
+                    } else {
+                        c = g.c0[(size_t)j * P + p];
+                        if (v) c = stretch_q(g.c1[(size_t)jp * P + p], zp, c);
+                    }
+                    const double q = stretch_q(c, z, g.x1[(size_t)p * n + k]);
+                    g.x1[(size_t)p * n + k] = q;
+                    if (g.x1_aos) g.x1_aos[(size_t)k * P + p] = q;
+                }
+                g.lnp1[k] = lnew;
+                if (g.accepted1) g.accepted1[k] += 1;
+            }
         }
     } else if (t < 2 * n) {
         const int i = t - n;
@@ -148,7 +196,10 @@ hipError_t launch_stretch_accept(int P, int n0, int64_t s0b, double* x, double* 
     return hipGetLastError();
 }
 hipError_t launch_stretch_iteration_end(const IterEndArgs& g, hipStream_t st) {
-    stretch_iteration_end_kernel<<<grid1(2 * g.n), 256, 0, st>>>(g);
+    if (g.dim <= 16)
+        stretch_iteration_end_kernel<16><<<grid1(2 * g.n), 256, 0, st>>>(g);
+    else
+        stretch_iteration_end_kernel<0><<<grid1(2 * g.n), 256, 0, st>>>(g);
     return hipGetLastError();
 }
 hipError_t launch_mh_propose(int P, int n, int64_t b, const double* x, const double* scales, double step,
