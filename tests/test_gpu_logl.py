@@ -347,6 +347,27 @@ def test_large_batch_size_independent_results(W):
     assert np.isfinite(big).all()
 
 
+@pytest.mark.parametrize("W", [2048, 6000])
+def test_wide_ball_redos_keep_bits(W):
+    """Wide ball (relative 0.1): the speculative levels redo segments gated and back off
+    (rvm_logl.hip spec_off / spec_bo: 2933 level-2 redos per 6144-slot launch at this width,
+    profiles/r02h_prof_clock_ball.jsonl), and a wave's redo and back-off history depends on its
+    wave-mates -- different in the full batch than for a walker launched alone.  A walker's bits
+    (logL, status, model RVs) must not; 2048 runs the LDS-coupled layout, 6000 the level-split one."""
+    obs = s2_obs_oracle()
+    plan, _ = _plan(obs, S2_PLANETS, max_walkers=W)
+    P = _ball(S2_PLANETS, W, rel=0.1, seed=41)
+    big, st_big, rv_big = _run(plan, P, want_rv=True)
+    rng = np.random.default_rng(3)
+    for i in np.r_[0, 1, 63, W - 1, rng.choice(W, 12, replace=False)]:
+        one, st1, rv1 = _run(plan, P[i:i + 1], want_rv=True)
+        assert st1[0] == st_big[i]
+        np.testing.assert_array_equal(one[0], big[i])
+        np.testing.assert_array_equal(rv1[:, 0], rv_big[:, i])
+    # (statuses of a wide ball: some walkers meet the exit distance, most integrate to the end)
+    assert (st_big == 0).mean() > 0.5
+
+
 @pytest.mark.parametrize("one_sided,npoints", [(False, 300), (True, 300), (True, 100)])
 def test_level_split_ring_wrap_and_empty_direction(one_sided, npoints):
     """Level-split hand-off (rvm_logl.hip): levels 3, 2, 0 pass their per-epoch RVs to the unit's
