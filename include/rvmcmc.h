@@ -52,13 +52,15 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 8
+#define RVM_ABI_VERSION 9
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
 #define RVM_STATUS_PRIOR 1     /* State.priorHard() true (state.py:299-315) -> logl = -inf        */
 #define RVM_STATUS_ENCOUNTER 2 /* pair distance < exit_min_distance (REBOUND Encounter) -> -inf   */
-#define RVM_STATUS_NONFINITE 3 /* non-finite chi2 -> -inf                                          */
+#define RVM_STATUS_NONFINITE 3 /* non-finite chi2, or a level-split hand-off that gave up -> -inf     */
+#define RVM_STATUS_UNRESOLVED 4 /* adaptive resolution: the extrapolation-error estimate still above
+                                   rvm_config.resolve_tol after resolve_max refinements -> -inf      */
 
 #define RVM_MAX_PLANETS 4
 #define RVM_MAX_LEVELS 6
@@ -80,6 +82,13 @@ typedef struct {
     int32_t inclined;      /* 0: coplanar, params [5*n_planets][W] (m, a, h, k, l); 1: inclined,
                               params [7*n_planets][W] (m, a, h, k, l, ix, iy; REBOUND's Pal ix, iy),
                               3-D integration, prior adds ix^2 + iy^2 >= 4 (state.py:311-313)      */
+    double resolve_tol;    /* adaptive resolution: bound on a walker's |logL| error as
+                              estimated from the extrapolation itself -- the change of chi2/npoints
+                              when the coarsest level is dropped -- split evenly over its two
+                              directions.  A direction above its half is integrated again with every
+                              step halved, up to resolve_max times (the reference's IAS15 adapts its
+                              step to the orbit; a fixed plan step does not).  <= 0: off            */
+    int32_t resolve_max;   /* 0..8 refinements; 0 with resolve_tol > 0: flag (UNRESOLVED) only      */
 } rvm_config;
 
 typedef struct rvm_plan rvm_plan;
@@ -96,6 +105,22 @@ void rvm_plan_destroy(rvm_plan* plan);
 /* schedule introspection: total level-1 steps per direction (fwd, bwd), epochs per direction */
 int rvm_plan_info(const rvm_plan* plan, int32_t* steps_fwd, int32_t* steps_bwd, int32_t* epochs_fwd,
                   int32_t* epochs_bwd);
+
+/* Counters of a plan since its creation or the last reset, read in order on `stream` (the call
+ * synchronises that stream; any output pointer may be NULL):
+ *   handoff_timeouts  level-split hand-off waits that gave up (rvm_plan_set_handoff_timeout): their
+ *                     walkers report RVM_STATUS_NONFINITE, the plan's hand-off workspace is dirty
+ *                     and every later level-split launch on the plan reports NONFINITE until reset
+ *   nonfinite         walkers finished with RVM_STATUS_NONFINITE (any launch on the plan)
+ *   unresolved        walkers finished with RVM_STATUS_UNRESOLVED
+ *   refined           walker-directions integrated again by the adaptive resolution (passes)
+ * reset != 0: zero the counters and restore the hand-off workspace, after the stream's earlier work.
+ * The samplers (rvmcmc) check this and raise on timeouts / non-finite results (mcmc.py:28-35: emcee
+ * refuses NaN log-probabilities) rather than treating them as ordinary rejections. */
+int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
+                    int64_t* unresolved, int64_t* refined, void* stream);
+/* Level-split hand-off waits give up after `seconds` without progress (default 2 s; > 0). */
+int rvm_plan_set_handoff_timeout(rvm_plan* plan, double seconds);
 
 /* logl_out[w] = -chi2/npoints_norm or -INF; status_out[w]; rv_out (nullable) = model RV
  * [n_obs][n_walkers] in the plan's input epoch order.  hill_factor = State.hillRadiusFactor

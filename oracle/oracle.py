@@ -71,6 +71,9 @@ def lib():
         L.rvo_logl_whx_seq_batch.argtypes = [C.c_int, C.c_int, dp, C.c_int, C.c_int, C.c_double, dp, dp, dp,
                                              C.c_int, C.c_double, C.c_double, C.c_int, ip, dp,
                                              C.POINTER(C.c_int32)]
+        L.rvo_logl_whx_adapt_batch.argtypes = [C.c_int, C.c_int, dp, C.c_int, C.c_int, C.c_double, dp, dp, dp,
+                                               C.c_int, C.c_double, C.c_double, C.c_int, ip, C.c_double, C.c_int, dp,
+                                               C.POINTER(C.c_int32), C.POINTER(C.c_int32), dp]
         _LIB = L
     return _LIB
 
@@ -232,6 +235,35 @@ def logl_whx_seq_batch(params, np_, obs, dt, mult, hill_factor=1.0, has_hk=1, ha
                                  len(t), float(obs.Npoints), float(dt), len(m), mp, _p(out),
                                  st.ctypes.data_as(C.POINTER(C.c_int32)))
     return out, st
+
+
+ORACLE_UNRESOLVED = 4
+
+
+def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.0, has_hk=1, has_inc=0):
+    """The kernel's algorithm with adaptive resolution (rvm_config.resolve_tol / resolve_max):
+    each direction refines (every step halved) while its extrapolation-error estimate exceeds
+    tol / 2.
+    params [W][np][7] -> (logl[W], status[W], refinements [W][2], estimates [W][2],
+    margins [W][2]); margin = the closest any pass's estimate came to the bound, min |est/(tol/2) - 1|
+    (a decision at roundoff distance may go the other way in a second implementation).  tol = 0 is
+    the plain rvo_whx algorithm."""
+    pl = _f64(params)
+    W = pl.shape[0]
+    t = _f64(np.concatenate([obs.tf, obs.tb]))
+    rv = _f64(np.concatenate([obs.rvf, obs.rvb]))
+    er = _f64(np.concatenate([obs.errorf, obs.errorb]))
+    out = np.zeros(W)
+    st = np.zeros(W, dtype=np.int32)
+    rf = np.zeros((W, 2), dtype=np.int32)
+    est = np.zeros((W, 4))
+    m, mp = _mult(mult)
+    tol_dir = 0.5 * float(tol) if tol > 0 else np.inf
+    lib().rvo_logl_whx_adapt_batch(W, np_, _p(pl), has_hk, has_inc, float(hill_factor), _p(t), _p(rv), _p(er),
+                                   len(t), float(obs.Npoints), float(dt), len(m), mp, tol_dir, int(rf_max), _p(out),
+                                   st.ctypes.data_as(C.POINTER(C.c_int32)), rf.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   _p(est))
+    return out, st, rf, est[:, :2], est[:, 2:]
 
 
 def min_distance_ratio(params, np_, obs, dt, n_levels):

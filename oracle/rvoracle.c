@@ -989,3 +989,127 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
         status[w] = rvo_logl_whx_seq(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs,
                                      err, n, npoints, dt, nl, mult, logl + w);
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Adaptive resolution: restatement of the kernel's per-direction refinement (rvm_logl.hip,    */
+/* DESIGN.md §3).  A direction is integrated with the plan's step; its extrapolation error is   */
+/* estimated by the change of chi2 when the coarsest level is dropped,                          */
+/*   est = sum_i |(r_i - o_i)^2 - (r3_i - o_i)^2| / sigma_i^2 / npoints,                        */
+/* r = all levels' Richardson RV, r3 = the finer nl - 1 levels' (their own Lagrange weights).   */
+/* While est > tol_dir the direction is integrated again with every step halved (level k: mult  */
+/* 2^rf steps per base step), up to rf_max times; still above after that: RVO_UNRESOLVED.       */
+/* An encounter or non-finite RV ends the direction at once (no refinement).                    */
+/* ------------------------------------------------------------------------------------------ */
+enum { RVO_UNRESOLVED = 4 };
+
+
+static int whx_direction_adapt(int np, const double* pl, double hill_factor, const double* at, const double* ob,
+                               const double* s2, int cnt, double sign, double dt, int nl, const int* mult,
+                               double tol_dir, int rf_max, double npoints, double* chi2_out, int* rf_out,
+                               double* est_out, double* margin_out) {
+    double w[8], w3[8];
+    rvo_richardson_weights_seq(nl, mult, w);
+    w3[0] = 0.0;
+    if (nl >= 2) rvo_richardson_weights_seq(nl - 1, mult + 1, w3 + 1);
+    double* lv = (double*)malloc(sizeof(double) * (size_t)(8 * cnt + 1));
+    int st = RVO_OK;
+    double chi2 = 0.0, est = 0.0, margin = INFINITY;
+    int rf = 0;
+    for (rf = 0; rf <= rf_max; rf++) {
+        st = RVO_OK;
+        for (int k = 0; k < nl; k++) {
+            const int s = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, mult[k] << rf, lv + (size_t)k * cnt);
+            if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
+        }
+        if (st != RVO_OK) break;
+        chi2 = 0.0;
+        est = 0.0;
+        for (int i = 0; i < cnt; i++) {
+            double r = 0.0, r3 = 0.0;
+            for (int k = 0; k < nl; k++) r += w[k] * lv[(size_t)k * cnt + i];
+            for (int k = 1; k < nl; k++) r3 += w3[k] * lv[(size_t)k * cnt + i];
+            chi2 += (r - ob[i]) * (r - ob[i]) / s2[i];
+            est += fabs((r - r3) * ((r - ob[i]) + (r3 - ob[i]))) / s2[i];
+        }
+        est /= npoints;
+        if (nl >= 2 && tol_dir < INFINITY && fabs(est / tol_dir - 1.0) < margin) margin = fabs(est / tol_dir - 1.0);
+        if (nl < 2 || !(est > tol_dir)) break;
+        if (rf == rf_max) {
+            st = RVO_UNRESOLVED;
+            break;
+        }
+    }
+    free(lv);
+    *chi2_out = chi2;
+    *rf_out = rf > rf_max ? rf_max : rf;
+    *est_out = est;
+    *margin_out = margin;
+    return st;
+}
+
+/* logp with adaptive resolution: rf_used[2] / est[2] (fwd, bwd) report the refinements taken and
+ * the final estimates.  Status: PRIOR, else the forward direction's non-OK status, else the
+ * backward one's (the kernel's direction meeting).  est[4]: the final estimates (fwd, bwd) and the
+ * closest any pass came to the bound, min |est / tol_dir - 1| (fwd, bwd): a refinement decision
+ * a second implementation may take the other way when that is at roundoff level. */
+int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
+                       const double* rvobs, const double* err, int n, double npoints, double dt, int nl,
+                       const int* mult, double tol_dir, int rf_max, double* logl, int32_t* rf_used, double* est) {
+    rf_used[0] = rf_used[1] = 0;
+    est[0] = est[1] = 0.0;
+    est[2] = est[3] = INFINITY;
+    if (rvo_prior_hard(np, pl, has_hk, has_inc)) {
+        *logl = -INFINITY;
+        return RVO_PRIOR;
+    }
+    int* idx = (int*)malloc(sizeof(int) * (size_t)(n + 1));
+    double* at = (double*)malloc(sizeof(double) * (size_t)(3 * n + 3));
+    double* ob = at + n + 1;
+    double* s2 = ob + n + 1;
+    int sd[2] = {RVO_OK, RVO_OK};
+    double chi2[2] = {0.0, 0.0};
+    for (int dir = 0; dir < 2; dir++) {
+        int cnt = 0;
+        for (int i = 0; i < n; i++)
+            if ((dir == 0) == (t[i] >= 0.0)) idx[cnt++] = i;
+        for (int a = 1; a < cnt; a++) { /* stable insertion sort by |t| */
+            const int key = idx[a];
+            int b = a - 1;
+            while (b >= 0 && fabs(t[idx[b]]) > fabs(t[key])) {
+                idx[b + 1] = idx[b];
+                b--;
+            }
+            idx[b + 1] = key;
+        }
+        for (int a = 0; a < cnt; a++) {
+            at[a] = fabs(t[idx[a]]);
+            ob[a] = rvobs[idx[a]];
+            s2[a] = err[idx[a]] * err[idx[a]];
+        }
+        int rf = 0;
+        double e = 0.0, mg = INFINITY;
+        if (cnt)
+            sd[dir] = whx_direction_adapt(np, pl, hill_factor, at, ob, s2, cnt, dir == 0 ? 1.0 : -1.0, dt, nl, mult,
+                                          tol_dir, rf_max, npoints, &chi2[dir], &rf, &e, &mg);
+        rf_used[dir] = rf;
+        est[dir] = e;
+        est[2 + dir] = mg;
+    }
+    free(idx);
+    free(at);
+    int st = sd[0] != RVO_OK ? sd[0] : sd[1];
+    const double lp = -((chi2[1] + chi2[0]) / npoints);
+    if (st == RVO_OK && !isfinite(lp)) st = RVO_NONFINITE;
+    *logl = st == RVO_OK ? lp : -INFINITY;
+    return st;
+}
+
+void rvo_logl_whx_adapt_batch(int W, int np, const double* pl, int has_hk, int has_inc, double hill_factor,
+                              const double* t, const double* rvobs, const double* err, int n, double npoints,
+                              double dt, int nl, const int* mult, double tol_dir, int rf_max, double* logl,
+                              int32_t* status, int32_t* rf_used, double* est) {
+    for (int w = 0; w < W; w++)
+        status[w] = rvo_logl_whx_adapt(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs,
+                                       err, n, npoints, dt, nl, mult, tol_dir, rf_max, logl + w, rf_used + 2 * w,
+                                       est + 4 * w);
+}

@@ -60,6 +60,7 @@ struct rvm_plan {
     rvm::DevPlan dev;
     void* dmem = nullptr;        // one device allocation: schedule + workspace
     void* lvmem = nullptr;       // level-split layout workspace (DevPlan::lv_*), when usable
+    size_t lv_bytes = 0;
     unsigned long long* slots = nullptr;  // [max_walkers] direction meeting slots (rvm_logl.hip)
     int32_t max_walkers = 0;
     int32_t steps[2] = {0, 0};
@@ -102,6 +103,9 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     }
     if (!(cfg->period_hint >= 0.0) || !std::isfinite(cfg->period_hint))
         return fail(-1, "rvm_plan_create: period_hint must be >= 0");
+    if (std::isnan(cfg->resolve_tol) || cfg->resolve_max < 0 || cfg->resolve_max > 8)
+        return fail(-1, "rvm_plan_create: resolve_tol must be a number and resolve_max in 0..8");
+    const int rmax = cfg->resolve_tol > 0.0 ? cfg->resolve_max : 0;
     for (int i = 0; i < n_obs; i++) {
         if (!std::isfinite(t[i]) || !std::isfinite(rv[i]) || !std::isfinite(sigma[i]))
             return fail(-1, "rvm_plan_create: non-finite observation");
@@ -132,7 +136,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             D.os2.push_back(sigma[i] * sigma[i]);
             total_steps[dd] += n;
         }
-        if (total_steps[dd] * (long long)max_mult > (1LL << 30))
+        if ((total_steps[dd] * (long long)max_mult) << rmax > (1LL << 30))
             return fail(-1, "rvm_plan_create: dt too small for the epoch span");
         if (D.idx.size() > (size_t)RVM_MAX_EPOCHS_PER_DIRECTION)
             return fail(-1, "rvm_plan_create: too many epochs in one direction (the schedule is staged in LDS)");
@@ -140,7 +144,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
 
     // device layout: per direction [seg_n | obs_idx] int32 and [seg_len | obs_rv | obs_s2] f64, + workspace
     const size_t nf = dir[0].idx.size(), nb = dir[1].idx.size();
-    const size_t n_dbl = 3 * (nf + nb) + (size_t)max_walkers;  // schedule f64 | slots (u64)
+    const size_t n_dbl = 3 * (nf + nb) + (size_t)max_walkers + 4;  // schedule f64 | slots | counters (u64)
     const size_t n_int = 2 * (nf + nb);
     const size_t bytes = n_dbl * sizeof(double) + n_int * sizeof(int32_t) + 64;
     rvm_plan* plan = new rvm_plan();
@@ -170,7 +174,9 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             // measured at 6144 slots, scripts/probe/prof_clock.py with RVM_LS_F0: 0.625 -> SIMD 0/1
             // end 6 % after SIMD 2/3, 0.74 -> within 1 %)
             if (nlv == 4) f0 = (double)(mult[3] + mult[0] - mult[2]) / (2.0 * mult[0]) + 0.11;
-            if (const char* ef = getenv("RVM_LS_F0")) f0 = atof(ef);  // (experiments: scripts/probe)
+#ifdef RVM_PROFILE
+            if (const char* ef = getenv("RVM_LS_F0")) f0 = atof(ef);  // (timing build only: scripts/probe)
+#endif
             f0 = std::min(1.0, std::max(0.0, f0));
             const double fr[2] = {f0, 0.5};
             int32_t sp[2] = {0, 0}, pr[2] = {0, 0};
@@ -216,6 +222,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     plan->slots = reinterpret_cast<unsigned long long*>(dd_base + od);
     for (int32_t i = 0; i < max_walkers; i++)  // empty between launches (the kernel restores this)
         reinterpret_cast<unsigned long long*>(hd + od)[i] = 0x7FF4DEADBEEF0001ULL;
+    plan->dev.counters = reinterpret_cast<unsigned long long*>(dd_base + od + max_walkers);  // (zeroed)
     plan->max_walkers = max_walkers;
     e = hipMemcpy(plan->dmem, host.data(), bytes, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -244,6 +251,21 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.nt[k] = 8;
         P.spec[k] = 0;
     }
+    // adaptive resolution: the weights of levels 1 .. n-1 alone (the estimate drops the coarsest)
+    for (int k = 0; k < RVM_MAX_LEVELS; k++) P.lw3[k] = 0.0;
+    for (int k = 1; k < cfg->n_levels; k++) {
+        const double xk = 1.0 / ((double)mult[k] * mult[k]);
+        double wk = 1.0;
+        for (int j = 1; j < cfg->n_levels; j++) {
+            if (j == k) continue;
+            const double xj = 1.0 / ((double)mult[j] * mult[j]);
+            wk *= xj / (xj - xk);
+        }
+        P.lw3[k] = wk;
+    }
+    P.rtol_dir = cfg->resolve_tol > 0.0 && cfg->n_levels >= 2 ? 0.5 * cfg->resolve_tol : INFINITY;
+    P.rmax = P.rtol_dir < INFINITY ? rmax : 0;
+    P.spin_ticks = 200000000ull;  // 2 s of the 100 MHz real-time counter without progress
     for (int k = 0; k < cfg->n_levels; k++) {
         const double xk = 1.0 / ((double)mult[k] * mult[k]);
         double wk = 1.0;
@@ -276,9 +298,11 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const int64_t groups = ((int64_t)max_walkers + wpb - 1) / wpb;
         bool inc = cfg->n_levels == 4;
         for (int k = 1; inc && k < 4; k++) inc = mult[k] > mult[k - 1];
-        // RVM_NO_LEVEL_SPLIT=1 forces the LDS-coupled layout (tests: the no-workspace fallback)
+#ifdef RVM_PROFILE
+        // RVM_NO_LEVEL_SPLIT=1 forces the LDS-coupled layout (timing build only: scripts/probe)
         const char* nols = getenv("RVM_NO_LEVEL_SPLIT");
         if (nols && nols[0] == '1') inc = false;
+#endif
         if (inc && P.n_cu > 0 && 2 * groups > P.n_cu) {
             const int64_t emax = (int64_t)(nf > nb ? nf : nb) > 0 ? (int64_t)(nf > nb ? nf : nb) : 1;
             const size_t b_rv = (size_t)(2 * emax * max_walkers) * sizeof(double);
@@ -292,6 +316,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
                 P.lv_enc = reinterpret_cast<int32_t*>(base + b_rv);
                 P.lv_emax = (int32_t)emax;
                 P.lv_stride = max_walkers;
+                plan->lv_bytes = b_rv + b_enc;
                 // every slot empty (all-ones: the NaN sentinel / -1); the combiners restore this
                 if (hipMemset(plan->lvmem, 0xFF, b_rv + b_enc) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
                     (void)hipFree(plan->lvmem);
@@ -313,6 +338,37 @@ void rvm_plan_destroy(rvm_plan* plan) {
     if (plan->lvmem) (void)hipFree(plan->lvmem);
     if (plan->dmem) (void)hipFree(plan->dmem);
     delete plan;
+}
+
+int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
+                    int64_t* unresolved, int64_t* refined, void* stream) {
+    if (!plan) return fail(-1, "rvm_plan_faults: null plan");
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long h[4] = {0, 0, 0, 0};
+    hipError_t e = hipMemcpyAsync(h, plan->dev.counters, sizeof(h), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return hip_fail(e, "rvm_plan_faults");
+    if (handoff_timeouts) *handoff_timeouts = (int64_t)h[0];
+    if (nonfinite) *nonfinite = (int64_t)h[1];
+    if (unresolved) *unresolved = (int64_t)h[2];
+    if (refined) *refined = (int64_t)h[3];
+    if (reset) {
+        // the hand-off slots back to their sentinels (late level-1 stores of a launch that gave up
+        // have landed: the stream's earlier work is complete), then the counters
+        if (plan->lvmem) e = hipMemsetAsync(plan->lvmem, 0xFF, plan->lv_bytes, st);
+        if (e == hipSuccess) e = hipMemsetAsync(plan->dev.counters, 0, sizeof(h), st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return hip_fail(e, "rvm_plan_faults: reset");
+    }
+    return 0;
+}
+
+int rvm_plan_set_handoff_timeout(rvm_plan* plan, double seconds) {
+    if (!plan) return fail(-1, "rvm_plan_set_handoff_timeout: null plan");
+    if (!(seconds > 0.0) || !(seconds < 1e9)) return fail(-1, "rvm_plan_set_handoff_timeout: seconds out of range");
+    const double ticks = seconds * 1e8;  // 100 MHz real-time counter
+    plan->dev.spin_ticks = ticks < 1.0 ? 1ull : (unsigned long long)ticks;
+    return 0;
 }
 
 int rvm_plan_info(const rvm_plan* plan, int32_t* sf, int32_t* sb, int32_t* ef, int32_t* eb) {

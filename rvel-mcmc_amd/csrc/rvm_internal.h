@@ -7,9 +7,13 @@
 namespace rvm {
 
 // level-split layout: the LDS ring of a type-A block holds at most this many epochs per level
-// (levels wait for the combiner beyond it), and the whole dynamic LDS request stays within
+// (levels wait for the combiner beyond it); the dynamic LDS request plus the kernel's static LDS
+// (read with hipFuncGetAttributes at launch) must stay within the CU's 160 KB
 constexpr int RVM_LS_RING = 64;
-constexpr int RVM_LS_MAX_LDS = 160 * 1024 - 16 * 1024;  // (the kernel's static LDS is < 16 KB)
+constexpr int RVM_LDS_PER_CU = 160 * 1024;
+// adaptive resolution: lane state at t = 0 kept in LDS for the refinement passes, per walker group
+// (rx, ry, vx, vy, rz, vz, r, ir of each of the 64 lanes)
+constexpr int RVM_INIT_DOUBLES = 8 * 64;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
@@ -34,6 +38,18 @@ struct DevPlan {
     int32_t spec[RVM_MAX_LEVELS];  // 1: speculative segments on this level (rvm_logl.hip)
     double inv_mult[RVM_MAX_LEVELS];  // 1 / mult: level step = seg_h1 * inv_mult
     double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
+    // adaptive resolution (rvm_logl.hip): lw3 = the Lagrange weights of levels
+    // 1 .. n_levels-1 alone (lw3[0] = 0); a direction whose estimate
+    //   est = sum_e |(rv - o)^2 - (rv3 - o)^2| / s2 / npoints   (rv3 = sum_k lw3[k] rv_k)
+    // exceeds rtol_dir is integrated again with every step halved, at most rmax times
+    double lw3[RVM_MAX_LEVELS];
+    double rtol_dir;   // +inf: no estimate check
+    int32_t rmax;
+    // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
+    // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
+    // [3] walker-directions refined
+    unsigned long long* counters;
+    unsigned long long spin_ticks;  // hand-off waits give up after this long without progress (100 MHz)
     double npoints;
     int32_t n_obs;
     int32_t inclined;  // 1: 7 parameter rows per planet (ix, iy), 3-D integration

@@ -171,9 +171,22 @@ __device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, in
 #define RVM_LV_EMPTY 0xFFFFFFFFFFFFFFFFULL
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
-// bounded spins (a hand-off that never completes gives up instead of hanging the GPU; blocks are
-// all resident by construction: launch_logl uses the layout only when its grid fits the CUs)
-#define RVM_LS_SPIN_MAX (1u << 20)
+// Bounded waits: a hand-off wait gives up after P.spin_ticks of the 100 MHz real-time counter
+// WITHOUT PROGRESS (the clock restarts at every epoch that arrives, so a long launch never times
+// out while it advances), counts the give-up in the plan's fault counter (rvm_plan_faults) and
+// reports its walkers NONFINITE instead of hanging the GPU.  Blocks are all resident by
+// construction: launch_logl uses the layout only when its grid fits the CUs.
+struct SpinClock {
+    unsigned long long last;
+    __device__ __forceinline__ void restart() { last = __builtin_amdgcn_s_memrealtime(); }
+    __device__ __forceinline__ bool expired(unsigned long long ticks) const {
+        return __builtin_amdgcn_s_memrealtime() - last > ticks;
+    }
+};
+// per-direction flag bits of a walker (encflag / enc): 1 encounter, 2 prior, 4 unresolved after
+// the last refinement, 8 a hand-off of this launch gave up (the values are not trustworthy)
+#define RVM_ENC_UNRESOLVED 4
+#define RVM_ENC_FAULT 8
 
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
 template <int NP, bool D3, bool DEC>
@@ -282,6 +295,13 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     __shared__ unsigned long long s_hoe[2];
     __shared__ int s_hosp[2], s_hof[2];
     __shared__ int s_enc_all[2][RVM_MAX_LEVELS][64];
+    // adaptive resolution: walker slots of each group (LDS-coupled) / unit (level-split) still above
+    // the estimate bound; the level-split combiners' verdicts (0 pending, 1 finished, 2 refine) and
+    // their results for the refinement team
+    __shared__ unsigned long long s_need[2];
+    __shared__ int s_vd[2];
+    __shared__ double s_fchi[2][64];
+    __shared__ int s_fenc[2][64];
     double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
     // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
@@ -471,6 +491,23 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     s.ir = 1.0 / s.r;
     s.encm = 0;
     lane_finish(s);
+    // adaptive resolution: the lanes' state at t = 0 for refinement passes, in LDS after the
+    // schedule and the stretch staging (LDS-coupled: [group][8][64]) or after the level-split ring
+    // ([unit][8][64]; the unit's level-3 wave keeps it)
+    const int ring_sz = emax2 < RVM_LS_RING ? emax2 : RVM_LS_RING;
+    double* l_init = dec ? s_sched + (size_t)8 * emax2 + (size_t)6 * ring_sz * WPB
+                         : s_sched + (size_t)4 * emax2 + (fused ? (size_t)(R + 3) * GW : 0);
+    if (P.rmax > 0 && (dec ? (bid < nA && wv < 2) : lvl == 0)) {
+        double* o = l_init + (size_t)(dec ? wv : grp) * RVM_INIT_DOUBLES + lane;
+        o[0] = s.rx;
+        o[64] = s.ry;
+        o[128] = s.vx;
+        o[192] = s.vy;
+        o[256] = s.rz;
+        o[320] = s.vz;
+        o[384] = s.r;
+        o[448] = s.ir;
+    }
     // the interaction at t = 0 (the first segment's opening half kick) and REBOUND's check of
     // exit_min_distance before the first step -- when it integrates at all: get_rv of an empty
     // epoch list never does
@@ -497,6 +534,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         if (threadIdx.x < 6) (&s_lvp[0][0])[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_cprog[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_hof[threadIdx.x] = 0;
+        if (threadIdx.x < 2) s_vd[threadIdx.x] = 0;
         for (int dd = 0; dd < 2; dd++) {
             const DirSched& SD = dd ? P.bwd : P.fwd;
             double* b = s_sched + (size_t)dd * 4 * emax2;
@@ -553,6 +591,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     int spec_bo = 4;   // wave-uniform: the next back-off, doubled by each redo (a walker whose orbit
                        // keeps needing the general solver), back to 4 after a clean segment
     double chi2 = 0.0;
+    double est = 0.0;  // adaptive resolution: sum_e |(rv - o)^2 - (rv3 - o)^2| / s2 (combiner lanes)
     // level-split hand-off: level 1's column of P.lv_rv (one epoch row per epoch); the other levels'
     // slot in the block's LDS ring ([unit ul][local level ks][RING][WPB] doubles after the schedule)
     const int ul = wv & 1;
@@ -562,13 +601,27 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     gu64* lv1p = dec ? (gu64*)(P.lv_rv + ((size_t)d * P.lv_emax + e_lo) * P.lv_stride + wl) : nullptr;
     int rslot = RING > 0 ? e_lo % RING : 0;
     const int E_int = comb ? 0 : e_hi;  // the combiners integrate nothing
+    bool wfault = false;  // wave-uniform: a hand-off wait of this wave gave up (RVM_ENC_FAULT)
+    SpinClock clk;
     if (dec && part == 2) {
-        // a tail: wait for the head's state at epoch e_lo (same block, LDS)
-        unsigned spins = 0;
+        // a tail: wait for the head's state at epoch e_lo (same block, LDS); the head (type A: wave
+        // + 2, type B: wave - 1) publishes its progress at every epoch
+        const int head = bid < nA ? wv + 2 : wv - 1;
+        int seen = -1;
+        clk.restart();
         while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_hof[hs], __ATOMIC_ACQUIRE,
-                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) == 0 &&
-               ++spins < RVM_LS_SPIN_MAX)
+                                                                 __HIP_MEMORY_SCOPE_WORKGROUP)) == 0) {
+            const int pd = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(s_done + head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (pd != seen) {
+                seen = pd;
+                clk.restart();
+            } else if (clk.expired(P.spin_ticks)) {
+                wfault = true;
+                break;
+            }
             __builtin_amdgcn_s_sleep(8);
+        }
         s.rx = s_hos[hs][0][lane];
         s.ry = s_hos[hs][1][lane];
         s.vx = s_hos[hs][2][lane];
@@ -577,8 +630,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         s.vz = s_hos[hs][5][lane];
         s.r = s_hos[hs][6][lane];
         s.ir = s_hos[hs][7][lane];
-        s.encm = __builtin_amdgcn_readfirstlane(s_hoe[hs] & 0xFFFFFFFFull) |
-                 ((unsigned long long)__builtin_amdgcn_readfirstlane(s_hoe[hs] >> 32) << 32);
+        // (readfirstlane is 32-bit signed: each half through `unsigned`, or a set bit 31 -- an
+        // encounter on lane 30/31 -- would sign-extend into all 32 upper lanes)
+        s.encm = (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(s_hoe[hs] & 0xFFFFFFFFull)) |
+                 ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(s_hoe[hs] >> 32)) << 32);
         spec_off = __builtin_amdgcn_readfirstlane(s_hosp[hs]) & 0xFFFF;
         spec_bo = __builtin_amdgcn_readfirstlane(s_hosp[hs]) >> 16;
         // the interaction at the hand-off epoch, from the same positions: the head's bits (its
@@ -650,12 +705,21 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 lv1p += P.lv_stride;
             } else {
                 // wait while the combiner is a whole ring behind (only when E > RING)
-                if (E > RING) {
-                    unsigned spins = 0;
-                    while (e - __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-                                   s_cprog + ul, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >= RING &&
-                           ++spins < RVM_LS_SPIN_MAX)
+                if (E > RING && !wfault) {
+                    int seen = -1;
+                    for (;;) {
+                        const int cp = __builtin_amdgcn_readfirstlane(
+                            __hip_atomic_load(s_cprog + ul, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                        if (e - cp < RING) break;
+                        if (cp != seen) {
+                            seen = cp;
+                            clk.restart();
+                        } else if (clk.expired(P.spin_ticks)) {
+                            wfault = true;
+                            break;
+                        }
                         __builtin_amdgcn_s_sleep(4);
+                    }
                 }
                 if (pl_idx == 0) ring[((ul * 3 + ks) * RING + rslot) * WPB + slot] = v0;
                 if (lane == 0) __hip_atomic_store(&s_lvp[ul][ks], e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -666,10 +730,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             __syncthreads();
         }
         if (!dec && lvl == 0 && lane < WPB) {  // lane `lane` of wave 0 owns walker slot `lane`
-            double rvx = 0.0;
+            double rvx = 0.0, rv3 = 0.0;
             for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv[e & 1][k][lane];
+            for (int k = 1; k < nl; k++) rv3 += P.lw3[k] * s_rv[e & 1][k][lane];
             const double r = rvx - l_rv[e];
             chi2 += (r * r) / l_s2[e];
+            est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
             const int wo = w0 + lane;
             if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[e] * W + wo] = rvx;
         }
@@ -682,7 +748,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #endif
     }
 #undef prm
-    const int encflag = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) | (status == RVM_STATUS_PRIOR ? 2 : 0);
+    const int encflag = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) |
+                        (status == RVM_STATUS_PRIOR ? 2 : 0) | (wfault ? RVM_ENC_FAULT : 0);
     // ---- the two directions of a walker meet: the second to arrive finishes it ----------------
     // (one agent-scope exchange carries the other direction's result: no fence, no barrier).
     // row(r), z, u3, lnp0: the walker's proposal and accept inputs (fused stretch half-step)
@@ -690,6 +757,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                       const double lnp0) {
         int st = (enc & 2) ? RVM_STATUS_PRIOR : RVM_STATUS_OK;
         if (st == RVM_STATUS_OK && (enc & 1)) st = RVM_STATUS_ENCOUNTER;
+        if (st == RVM_STATUS_OK && (enc & RVM_ENC_FAULT)) st = RVM_STATUS_NONFINITE;
+        if (st == RVM_STATUS_OK && (enc & RVM_ENC_UNRESOLVED)) st = RVM_STATUS_UNRESOLVED;
         if (st == RVM_STATUS_OK && !isfinite(chi2w)) st = RVM_STATUS_NONFINITE;
         const double mine = st == RVM_STATUS_OK ? chi2w : -(double)st;
         const unsigned long long old = __hip_atomic_exchange(
@@ -706,6 +775,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const double lp = stw == RVM_STATUS_OK ? lp0 : -INFINITY;
         if (logl_out) logl_out[wo] = lp;
         if (status_out) status_out[wo] = stw;
+        // (rare: counted for rvm_plan_faults -- never a silent rejection)
+        if (stw == RVM_STATUS_NONFINITE || stw == RVM_STATUS_UNRESOLVED)
+            __hip_atomic_fetch_add(P.counters + (stw == RVM_STATUS_NONFINITE ? 1 : 2), 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         if (fused && (sa.n_spec == 0 || wo < sa.n_spec)) {
             // emcee / MH accept (half 1's slots of a speculative iteration only deliver their
             // logl: rvm_stretch_iteration_end)
@@ -725,24 +798,170 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (sa.dec) sa.dec[wo] = acc ? 1 : 0;
         }
     };
+    // finishing a walker without the LDS-staged proposal (level-split layout): the slot's draws again
+    // (recomputed from an opaque index rather than kept live through the integration)
+    auto finish_recompute = [&](const int w_in, const double chi2w, const int enc) {
+        if (stretch) {
+            int wo = w_in, k2, wk2, j2, jp2;
+            double z2, zp2;
+            asm volatile("" : "+v"(wo));
+            stretch_slot(sa, wo, k2, wk2, z2, j2, zp2, jp2);
+            auto row = [&](int r) { return walker_param(true, params, W, wk2, sa, r, z2, j2, k2, zp2, jp2); };
+            // (lnp0 exists for the accepting kind-0 slots only: sa.lnp is n_spec long)
+            finish(wo, chi2w, enc, row, z2, stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half),
+                   k2 == 0 ? sa.lnp[wo] : 0.0);
+        } else if (mh) {
+            auto row = [&](int r) { return walker_param(true, params, W, w_in, sa, r, 0.0, 0, 0, 0.0, 0); };
+            finish(w_in, chi2w, enc, row, 0.0, mh_u(sa.seed, (uint64_t)(sa.s0_begin + w_in), sa.iteration),
+                   sa.lnp[w_in]);
+        } else {
+            auto row = [&](int) { return 0.0; };
+            finish(w_in, chi2w, enc, row, 0.0, 0.0, 0.0);
+        }
+    };
+
+    // ---- adaptive resolution: one refinement pass with every step halved rf times -------------
+    // Run by the whole block in the LDS-coupled style: this wave integrates level lr of walker group
+    // (LDS-coupled) or unit (level-split) gr -- direction dr, whose schedule sits at
+    // s_sched + dr * 4 * emax2 (level-split) or l_dir -- from the lanes' state at t = 0 (l_init),
+    // gated drifts, one barrier per epoch over eb epochs (the longer direction's count in the
+    // level-split layout, whose units are the two directions); lr < 0: an idle wave (barriers
+    // only).  The combiner lanes (level 0's wave, lane = walker slot) accumulate chi2 (c2) and the
+    // estimate (e2) of the walkers marked in `need` and overwrite their rv_out rows.  The wave's
+    // encounter flags land in s_enc_all[gr][lr][slot] (final barrier).
+    int dummy_redo = 0;
+    auto refine_pass = [&](const int rf, const int lr, const int gr, const int dr, const int eb, const uint64_t need,
+                           double& c2, double& e2) {
+        const DirSched& SR = dr ? P.bwd : P.fwd;
+        const int Er = SR.n_epochs;
+        const double* r_dir = dec ? s_sched + (size_t)dr * 4 * emax2 : l_dir;
+        const double* r_len = r_dir;
+        const double* r_rv = r_dir + Er;
+        const double* r_s2 = r_dir + 2 * Er;
+        const int* r_n = reinterpret_cast<const int*>(r_dir + 3 * Er);
+        const int* r_idx = r_n + Er;
+        const bool work = lr >= 0 && need != 0;
+        const int lr_u = __builtin_amdgcn_readfirstlane(lr < 0 ? 0 : lr);
+        KickPrep<NP> kq{};
+        if (work) {
+            const double* in = l_init + (size_t)gr * RVM_INIT_DOUBLES + lane;
+            s.rx = in[0];
+            s.ry = in[64];
+            s.vx = in[128];
+            s.vy = in[192];
+            s.rz = in[256];
+            s.vz = in[320];
+            s.r = in[384];
+            s.ir = in[448];
+            s.encm = 0;
+            if (Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
+        }
+        const int m_r = P.mult[lr_u] << rf;
+        const int nt_r = P.nt[lr_u];
+        const double sc = ldexp(P.inv_mult[lr_u], -rf);  // (exact: a power-of-two scaling)
+        c2 = 0.0;
+        e2 = 0.0;
+        for (int e = 0; e < eb; e++) {
+            const bool here = e < Er;
+            const int ns = work && here ? r_n[e] * m_r : 0;
+            if (ns > 0) {
+                const double h = r_len[e] * sc;
+                if (nt_r <= 6)
+                    segment<6, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                else if (nt_r == 7)
+                    segment<7, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                else
+                    segment<8, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+            }
+            if (work) {  // (star_vx gathers over the walker's lanes by DPP: outside the lane branch)
+                const double v0 = star_vx<NP, L>(s);
+                if (pl_idx == 0) s_rv_all[gr][e & 1][lr_u][slot] = v0;
+            }
+            __syncthreads();
+            if (work && here && lr == 0 && lane < WPB && ((need >> lane) & 1)) {
+                double rvx = 0.0, rv3 = 0.0;
+                for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv_all[gr][e & 1][k][lane];
+                for (int k = 1; k < nl; k++) rv3 += P.lw3[k] * s_rv_all[gr][e & 1][k][lane];
+                const double r = rvx - r_rv[e];
+                c2 += (r * r) / r_s2[e];
+                e2 += fabs((rvx - rv3) * (r + (rv3 - r_rv[e]))) / r_s2[e];
+                const int wo = w0 + lane;
+                if (rv_out != nullptr && wo < W) rv_out[(size_t)r_idx[e] * W + wo] = rvx;
+            }
+        }
+        if (work && pl_idx == 0) s_enc_all[gr][lr_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
+        __syncthreads();
+    };
+    // Refinement loop over the walker slots still marked in s_need[g] of the active groups (gmask;
+    // set by the caller, one barrier since): the combiner lanes (cmb: level 0's wave, lane < WPB)
+    // update chi2w / enc / need per pass; a walker leaves when its estimate drops to the bound or a
+    // finer pass meets an encounter, and is UNRESOLVED if still above after rmax passes.
+    auto refine_loop = [&](const int lr, const int gr, const int dr, const int gmask, const int eb, const bool cmb,
+                           bool& need, double& chi2w, int& enc) {
+        for (int rf = 1; rf <= P.rmax; rf++) {
+            const uint64_t gneed = s_need[gr];
+            if (lr == 0 && lane == 0 && gneed)
+                __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(gneed),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            double c2, e2;
+            refine_pass(rf, lr, gr, dr, eb, gneed, c2, e2);
+            if (cmb && need) {
+                int er = 0;
+                for (int k = 0; k < nl; k++) er |= s_enc_all[gr][k][lane];
+                chi2w = c2;
+                if (er) {
+                    enc |= er;
+                    need = false;
+                } else if (!(e2 / P.npoints > P.rtol_dir)) {
+                    need = false;
+                } else if (rf == P.rmax) {
+                    enc |= RVM_ENC_UNRESOLVED;
+                    need = false;
+                }
+            }
+            if (lr == 0) {
+                const uint64_t nb = ballot(need);
+                if (lane == 0) s_need[gr] = nb;
+            }
+            __syncthreads();
+            if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) break;
+        }
+    };
+
     if (!dec) {
         if (pl_idx == 0) s_enc[lvl][slot] = encflag;
         __syncthreads();
-        if (lvl == 0 && lane < WPB) {
-            const int wo = w0 + lane;
-            if (wo < W) {
-                int enc = 0;
-                for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
-                const int gl = grp * WPB + lane;
-                auto row = [&](int r) { return l_q[r * GW + gl]; };
-                if (fused)
-                    finish(wo, chi2, enc, row, l_q[R * GW + gl], l_q[(R + 1) * GW + gl], l_q[(R + 2) * GW + gl]);
-                else
-                    finish(wo, chi2, enc, row, 0.0, 0.0, 0.0);
+        const bool cmb = lvl == 0 && lane < WPB;  // lane `lane` of wave 0 owns walker slot `lane`
+        const int wo = w0 + lane;
+        int enc = 0;
+        if (cmb)
+            for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
+        double chi2w = chi2;
+        if (P.rtol_dir < INFINITY) {  // (kernel argument: uniform)
+            bool need = cmb && wo < W && enc == 0 && est / P.npoints > P.rtol_dir;
+            if (P.rmax == 0) {
+                if (need) enc |= RVM_ENC_UNRESOLVED;
+            } else {
+                if (lvl == 0) {
+                    const uint64_t nb = ballot(need);
+                    if (lane == 0) s_need[grp] = nb;
+                }
+                __syncthreads();
+                if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
+                    refine_loop(lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc);
             }
         }
+        if (cmb && wo < W) {
+            const int gl = grp * WPB + lane;
+            auto row = [&](int r) { return l_q[r * GW + gl]; };
+            if (fused)
+                finish(wo, chi2w, enc, row, l_q[R * GW + gl], l_q[(R + 1) * GW + gl], l_q[(R + 2) * GW + gl]);
+            else
+                finish(wo, chi2w, enc, row, 0.0, 0.0, 0.0);
+        }
     } else {
-        // level-split: level waves publish their flags and leave; the combiner finishes the unit
+        // level-split: level waves publish their flags; the combiner finishes the unit, or hands it
+        // to the block's refinement team (all eight waves of a type-A block)
 #ifdef RVM_PROFILE
         const unsigned long long rt_integ = __builtin_amdgcn_s_memrealtime();
         auto prof_dec = [&](unsigned long long rt_arr, int arr) {
@@ -801,7 +1020,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             }
         }
         if (!comb && part != 1) {
-            // a level wave: publish this level's encounter / prior flags and leave
+            // a level wave: publish this level's encounter / prior flags (type B: and leave)
             if (lvl == 1) {
                 if (pl_idx == 0 && valid)
                     __hip_atomic_store((gi32*)(P.lv_enc + (size_t)d * P.lv_stride + w), encflag, __ATOMIC_RELAXED,
@@ -813,98 +1032,142 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #ifdef RVM_PROFILE
             prof_dec(__builtin_amdgcn_s_memrealtime(), lvl);
 #endif
-            return;
-        }
-        // the unit's combiner: consume epoch e once the three local levels have published it
-        // (LDS counters) and level 1's values have landed (every lane's slot off the sentinel);
-        // lowest issue priority (it shares a SIMD with a level-3 or level-2 wave)
-        __builtin_amdgcn_s_setprio(0);
-        unsigned spins = 0;
-        bool hung = false;
-        auto local_published = [&]() {
-            const int p0 = __hip_atomic_load(&s_lvp[ul][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int p1 = __hip_atomic_load(&s_lvp[ul][1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const int p2 = __hip_atomic_load(&s_lvp[ul][2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return __builtin_amdgcn_readfirstlane(p0 < p1 ? (p0 < p2 ? p0 : p2) : (p1 < p2 ? p1 : p2));
-        };
-        gu64* l1 = (gu64*)(P.lv_rv + (size_t)d * P.lv_emax * P.lv_stride + wl);
-        double chi2w = 0.0;
-        int rr = 0;
-        for (int e = 0; e < E; e++) {
-            while (!hung && local_published() <= e) {
-                __builtin_amdgcn_s_sleep(2);
-                hung = ++spins >= RVM_LS_SPIN_MAX;
-            }
-            unsigned long long b1;
-            for (;;) {
-                b1 = valid ? __hip_atomic_load(l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ULL;
-                if (ballot(b1 == RVM_LV_EMPTY) == 0 || hung) break;
-                __builtin_amdgcn_s_sleep(2);
-                hung = ++spins >= RVM_LS_SPIN_MAX;
-            }
-            if (valid && pl_idx == 0) __hip_atomic_store(l1, RVM_LV_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            l1 += P.lv_stride;
-            // levels in order 0..3 (same arithmetic as the LDS-coupled path)
-            const double* rg = ring + (size_t)rr * WPB + slot;
-            const double v[4] = {rg[(ul * 3 + 2) * RING * WPB], __longlong_as_double((long long)b1),
-                                 rg[(ul * 3 + 1) * RING * WPB], rg[(ul * 3 + 0) * RING * WPB]};
-            double rvx = 0.0;
+            if (bid >= nA) return;
+        } else {
+            // the unit's combiner: consume epoch e once the three local levels have published it
+            // (LDS counters) and level 1's values have landed (every lane's slot off the sentinel);
+            // lowest issue priority (it shares a SIMD with a level-3 or level-2 wave).  A plan whose
+            // hand-off workspace is dirty from an earlier give-up (counters[0] != 0, until
+            // rvm_plan_faults resets it) reports every walker NONFINITE without waiting.
+            __builtin_amdgcn_s_setprio(0);
+            bool hung = __hip_atomic_load(P.counters, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0ull;
+            hung = __builtin_amdgcn_readfirstlane((int)hung) != 0;
+            const bool dirty = hung;
+            auto local_published = [&]() {
+                const int p0 = __hip_atomic_load(&s_lvp[ul][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int p1 = __hip_atomic_load(&s_lvp[ul][1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int p2 = __hip_atomic_load(&s_lvp[ul][2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                return __builtin_amdgcn_readfirstlane(p0 < p1 ? (p0 < p2 ? p0 : p2) : (p1 < p2 ? p1 : p2));
+            };
+            gu64* l1 = (gu64*)(P.lv_rv + (size_t)d * P.lv_emax * P.lv_stride + wl);
+            double chi2w = 0.0;
+            int rr = 0;
+            clk.restart();
+            for (int e = 0; e < E; e++) {
+                while (!hung && local_published() <= e) {
+                    __builtin_amdgcn_s_sleep(2);
+                    hung = clk.expired(P.spin_ticks);
+                }
+                unsigned long long b1;
+                for (;;) {
+                    b1 = valid ? __hip_atomic_load(l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ULL;
+                    if (ballot(b1 == RVM_LV_EMPTY) == 0 || hung) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    hung = clk.expired(P.spin_ticks);
+                }
+                if (valid && pl_idx == 0) __hip_atomic_store(l1, RVM_LV_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                l1 += P.lv_stride;
+                clk.restart();  // (an epoch arrived: progress)
+                // levels in order 0..3 (same arithmetic as the LDS-coupled path)
+                const double* rg = ring + (size_t)rr * WPB + slot;
+                const double v[4] = {rg[(ul * 3 + 2) * RING * WPB], __longlong_as_double((long long)b1),
+                                     rg[(ul * 3 + 1) * RING * WPB], rg[(ul * 3 + 0) * RING * WPB]};
+                double rvx = 0.0, rv3 = 0.0;
 #pragma unroll
-            for (int k = 0; k < 4; k++) rvx += P.lw[k] * v[k];
-            const double r = rvx - l_rv[e];
-            chi2w += (r * r) / l_s2[e];
-            if (rv_out != nullptr && valid && pl_idx == 0) rv_out[(size_t)l_idx[e] * W + w] = rvx;
-            if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            rr = rr + 1 == RING ? 0 : rr + 1;
-        }
-        // the levels' flags: local ones after their last counter step (E + 1), level 1's from HBM
-        while (!hung && local_published() <= E) {
-            __builtin_amdgcn_s_sleep(2);
-            hung = ++spins >= RVM_LS_SPIN_MAX;
-        }
-        int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];
-        {
-            gi32* e1p = (gi32*)(P.lv_enc + (size_t)d * P.lv_stride + wl);
-            int f1;
-            for (;;) {
-                f1 = valid ? __hip_atomic_load(e1p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-                if (ballot(f1 < 0) == 0 || hung) break;
+                for (int k = 0; k < 4; k++) rvx += P.lw[k] * v[k];
+#pragma unroll
+                for (int k = 1; k < 4; k++) rv3 += P.lw3[k] * v[k];
+                const double r = rvx - l_rv[e];
+                chi2w += (r * r) / l_s2[e];
+                est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
+                if (rv_out != nullptr && valid && pl_idx == 0) rv_out[(size_t)l_idx[e] * W + w] = rvx;
+                if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                rr = rr + 1 == RING ? 0 : rr + 1;
+            }
+            // the levels' flags: local ones after their last counter step (E + 1), level 1's from HBM
+            while (!hung && local_published() <= E) {
                 __builtin_amdgcn_s_sleep(2);
-                hung = ++spins >= RVM_LS_SPIN_MAX;
+                hung = clk.expired(P.spin_ticks);
             }
-            if (valid && pl_idx == 0) __hip_atomic_store(e1p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            enc |= f1 > 0 ? f1 : 0;
-        }
-        if (hung) chi2w = __builtin_nan("");  // never completed: reported as RVM_STATUS_NONFINITE
+            int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];
+            {
+                gi32* e1p = (gi32*)(P.lv_enc + (size_t)d * P.lv_stride + wl);
+                int f1;
+                for (;;) {
+                    f1 = valid ? __hip_atomic_load(e1p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                    if (ballot(f1 < 0) == 0 || hung) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    hung = clk.expired(P.spin_ticks);
+                }
+                if (valid && pl_idx == 0) __hip_atomic_store(e1p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                enc |= f1 > 0 ? f1 : 0;
+            }
+            if (hung) {  // never completed (or a dirty workspace): NONFINITE, and the give-up counted
+                chi2w = __builtin_nan("");
+                enc |= RVM_ENC_FAULT;
+                if (!dirty && lane == 0)
+                    __hip_atomic_fetch_add(P.counters, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
 #ifdef RVM_PROFILE
-        const unsigned long long rt_arr = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long rt_arr = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (valid) {
-            if (pl_idx != 0) {
-                // (the pair's second lane only helped with the loads)
-            } else if (stretch) {
-                // the slot's draws again (recomputed from an opaque index rather than kept live
-                // through the integration)
-                int wo = w, k2, wk2, j2, jp2;
-                double z2, zp2;
-                asm volatile("" : "+v"(wo));
-                stretch_slot(sa, wo, k2, wk2, z2, j2, zp2, jp2);
-                auto row = [&](int r) { return walker_param(true, params, W, wk2, sa, r, z2, j2, k2, zp2, jp2); };
-                // (lnp0 exists for the accepting kind-0 slots only: sa.lnp is n_spec long)
-                finish(w, chi2w, enc, row, z2, stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half),
-                       k2 == 0 ? sa.lnp[wo] : 0.0);
-            } else if (mh) {
-                auto row = [&](int r) { return walker_param(true, params, W, w, sa, r, 0.0, 0, 0, 0.0, 0); };
-                finish(w, chi2w, enc, row, 0.0, mh_u(sa.seed, (uint64_t)(sa.s0_begin + w), sa.iteration), sa.lnp[w]);
-            } else {
-                auto row = [&](int) { return 0.0; };
-                finish(w, chi2w, enc, row, 0.0, 0.0, 0.0);
+            // adaptive resolution: finish now, or leave the unit to the refinement team
+            bool need = P.rtol_dir < INFINITY && valid && pl_idx == 0 && enc == 0 && est / P.npoints > P.rtol_dir;
+            if (need && P.rmax == 0) {
+                enc |= RVM_ENC_UNRESOLVED;
+                need = false;
             }
-        }
+            const bool refine = ballot(need) != 0;
+            if (!refine) {
+                if (valid && pl_idx == 0) finish_recompute(w, chi2w, enc);
+            } else if (valid && pl_idx == 0) {
+                s_fchi[ul][slot] = chi2w;
+                s_fenc[ul][slot] = enc | (need ? 16 : 0);
+            }
+            if (lane == 0) __hip_atomic_store(s_vd + ul, refine ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef RVM_PROFILE
-        prof_dec(rt_arr, nl - 1);
+            prof_dec(rt_arr, nl - 1);
+#endif
+        }
+        // every wave of a type-A block: wait for both units' verdicts, then leave, or refine as one
+        // LDS-coupled team.  (Unbounded on purpose: every wait of a combiner is bounded, so both
+        // verdicts always come; a wave that left early would break the team's barriers.)
+        __builtin_amdgcn_s_setprio(0);
+        int v0 = 0, v1 = 0;
+        for (;;) {
+            v0 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(s_vd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            v1 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(s_vd + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+            if (v0 != 0 && v1 != 0) break;
+            __builtin_amdgcn_s_sleep(8);
+        }
+        if (v0 != 2 && v1 != 2) return;
+        // the refinement team.  Both units refine: wave wv takes level lr of its own unit gr = wv & 1
+        // (SIMD i carries levels (0, 3) or (1, 2) of the two units).  One unit refines: waves 0..3
+        // take its levels 0..3, one per SIMD (each at the lone-wave rate), waves 4..7 idle.
+        __builtin_amdgcn_s_setprio(1);
+        const bool both = v0 == 2 && v1 == 2;
+        const int gr = both ? ul : (v0 == 2 ? 0 : 1);
+        const int lr = both ? (wv < 4 ? (wv >> 1) : 5 - (wv >> 1)) : (wv < 4 ? wv : -1);
+        d = gr;  // (the finishing lanes meet the other direction as unit gr: finish() reads d)
+        const bool cmb = lr == 0 && lane < WPB;
+        const bool mine = (gr == 0 ? v0 : v1) == 2;
+        double chi2w = 0.0;
+        int enc = 0;
+        bool need = false;
+        if (cmb && mine) {
+            chi2w = s_fchi[gr][lane];
+            const int f = s_fenc[gr][lane];
+            enc = f & 15;
+            need = (f & 16) != 0 && w0 + lane < W;
+        }
+        if (lr == 0) {
+            const uint64_t nb = ballot(need);
+            if (lane == 0) s_need[gr] = nb;
+        }
+        __syncthreads();
+        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc);
+        if (cmb && mine && w0 + lane < W) finish_recompute(w0 + lane, chi2w, enc);
         return;
-#endif
     }
 #ifdef RVM_PROFILE
     PROF_T(t_end);
@@ -930,9 +1193,39 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #endif
 }
 
-hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
-                       double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
-    const int lpw = P.n_planets == 1 ? 1 : (P.n_planets == 2 ? 2 : 4);  // LanesPerWalker
+// Dynamic-LDS budget of one logl_kernel instantiation on the current device: the CU's 160 KB minus
+// the kernel's own static LDS (hipFuncGetAttributes; ~28 KB), with the attribute that admits a
+// dynamic request beyond 64 KB set once per device and instantiation.
+template <int NPV, bool D3V, bool DECV>
+static size_t lds_budget() {
+    static size_t budget[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return 32 * 1024;
+    }
+    if (budget[dev] == 0) {
+        const void* f = reinterpret_cast<const void*>(&logl_kernel<NPV, D3V, DECV>);
+        hipFuncAttributes fa{};
+        size_t b = 32 * 1024;  // (conservative if the runtime cannot tell)
+        if (hipFuncGetAttributes(&fa, f) == hipSuccess && fa.sharedSizeBytes < (size_t)RVM_LDS_PER_CU) {
+            const size_t lim = (size_t)RVM_LDS_PER_CU - fa.sharedSizeBytes;
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim) == hipSuccess)
+                b = lim;
+            else if (fa.sharedSizeBytes < 64 * 1024)
+                b = 64 * 1024 - fa.sharedSizeBytes;
+        }
+        (void)hipGetLastError();
+        budget[dev] = b;
+    }
+    return budget[dev];
+}
+
+template <int NPV, bool D3V>
+static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, double hill_factor,
+                                unsigned long long* slots, double* logl, int32_t* status, double* rv_out,
+                                const StretchArgs& sa, hipStream_t stream) {
+    const int lpw = LanesPerWalker<NPV>::value;
     const int wpb = 64 / lpw;
     const int groups = (W + wpb - 1) / wpb;
     // one walker group per block while the blocks fit one per CU (every wave alone on its SIMD:
@@ -942,9 +1235,10 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
     dim3 grid((groups + G - 1) / G, 2);
     dim3 block(64 * P.n_levels * G);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
-    const size_t rows = (size_t)(P.inclined ? 7 : 5) * P.n_planets;
+    const size_t rows = (size_t)(D3V ? 7 : 5) * NPV;
     const bool fused = sa.c != nullptr || sa.mh_scale != nullptr;
-    size_t smem = (size_t)emax * 4 * sizeof(double) + (fused ? (rows + 3) * G * wpb * sizeof(double) : 0);
+    const size_t init = P.rmax > 0 ? (size_t)RVM_INIT_DOUBLES * sizeof(double) : 0;  // per group / unit
+    size_t smem = (size_t)emax * 4 * sizeof(double) + (fused ? (rows + 3) * G * wpb * sizeof(double) : 0) + G * init;
     // level-split layout (logl_kernel) when it lowers the heaviest SIMD's load: in steps per base
     // step, max(m3, m2 + m0, 2 m1) for one round of <= n_cu blocks, against m3 per round of
     // single-group blocks or max_i(m_i + m_{n-1-i}) per round of two-group blocks
@@ -961,8 +1255,9 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
         const int c_cpl = G == 1 ? m[3] * ((2 * groups + P.n_cu - 1) / P.n_cu)
                                  : std::max(m[0] + m[3], m[1] + m[2]) * ((groups + P.n_cu - 1) / P.n_cu);
         const int ring = emax < RVM_LS_RING ? emax : RVM_LS_RING;
-        const size_t smem_ls = (size_t)emax * 8 * sizeof(double) + (size_t)6 * ring * wpb * sizeof(double);
-        if (na + nb <= P.n_cu && c_dec < c_cpl && smem_ls <= (size_t)RVM_LS_MAX_LDS) {
+        const size_t smem_ls =
+            (size_t)emax * 8 * sizeof(double) + (size_t)6 * ring * wpb * sizeof(double) + 2 * init;
+        if (na + nb <= P.n_cu && c_dec < c_cpl && smem_ls <= lds_budget<NPV, D3V, true>()) {
             nA = na;
             grid = dim3(na + nb, 1);
             block = dim3(8 * 64);
@@ -972,40 +1267,36 @@ hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hil
             smem = smem_ls;
         }
     }
-#define RVM_LAUNCH(NPV, D3V)                                                                                \
-    do {                                                                                                 \
-        if (nA > 0) {                                                                                    \
-            static bool lds_set = false; /* dynamic LDS beyond 64 KB: once per instantiation */         \
-            if (!lds_set) {                                                                              \
-                (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&logl_kernel<NPV, D3V, true>),   \
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, RVM_LS_MAX_LDS);   \
-                lds_set = true;                                                                          \
-            }                                                                                            \
-            logl_kernel<NPV, D3V, true><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, \
-                                                                       logl, status, sa, nA, tB | (splitA << 8)); \
-        } else                                                                                           \
-            logl_kernel<NPV, D3V, false><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots,  \
-                                                                        rv_out, logl, status, sa, nA, 8);  \
-    } while (0)
+    if (nA > 0) {
+        logl_kernel<NPV, D3V, true><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, logl,
+                                                                   status, sa, nA, tB | (splitA << 8));
+    } else {
+        if (smem > lds_budget<NPV, D3V, false>()) return hipErrorInvalidConfiguration;
+        logl_kernel<NPV, D3V, false><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, logl,
+                                                                    status, sa, nA, 8);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
+                       double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
     const bool inc = P.inclined != 0;
+#define RVM_LAUNCH(NPV) \
+    (inc ? launch_logl_t<NPV, true>(P, W, params, hill_factor, slots, logl, status, rv_out, sa, stream) \
+         : launch_logl_t<NPV, false>(P, W, params, hill_factor, slots, logl, status, rv_out, sa, stream))
     switch (P.n_planets) {
         case 1:
-            if (inc) RVM_LAUNCH(1, true); else RVM_LAUNCH(1, false);
-            break;
+            return RVM_LAUNCH(1);
         case 2:
-            if (inc) RVM_LAUNCH(2, true); else RVM_LAUNCH(2, false);
-            break;
+            return RVM_LAUNCH(2);
         case 3:
-            if (inc) RVM_LAUNCH(3, true); else RVM_LAUNCH(3, false);
-            break;
+            return RVM_LAUNCH(3);
         case 4:
-            if (inc) RVM_LAUNCH(4, true); else RVM_LAUNCH(4, false);
-            break;
+            return RVM_LAUNCH(4);
         default:
             return hipErrorInvalidValue;
     }
 #undef RVM_LAUNCH
-    return hipGetLastError();
 }
 
 }  // namespace rvm

@@ -15,9 +15,10 @@ RVM_STATUS_OK = 0
 RVM_STATUS_PRIOR = 1
 RVM_STATUS_ENCOUNTER = 2
 RVM_STATUS_NONFINITE = 3
+RVM_STATUS_UNRESOLVED = 4
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
-ABI_VERSION = 8  # include/rvmcmc.h RVM_ABI_VERSION
+ABI_VERSION = 9  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):
@@ -29,6 +30,8 @@ class RvmConfig(C.Structure):
         ("level_mult", C.c_int32 * RVM_MAX_LEVELS),
         ("period_hint", C.c_double),
         ("inclined", C.c_int32),
+        ("resolve_tol", C.c_double),
+        ("resolve_max", C.c_int32),
     ]
 
 
@@ -76,6 +79,9 @@ SIGNATURES = {
     "rvm_plan_create": (C.c_int, [C.POINTER(RvmConfig), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                   C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "rvm_plan_destroy": (None, [C.c_void_p]),
+    "rvm_plan_faults": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                  C.POINTER(C.c_int64), C.POINTER(C.c_int64), _dp]),
+    "rvm_plan_set_handoff_timeout": (C.c_int, [C.c_void_p, C.c_double]),
     "rvm_plan_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                 C.POINTER(C.c_int32)]),
     "rvm_logl_batch": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_double, _dp, _dp, _dp, _dp]),

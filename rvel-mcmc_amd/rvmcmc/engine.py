@@ -55,6 +55,15 @@ class IntegratorConfig:
     steps_per_orbit: float = 8.0
     levels: tuple = (4, 5, 6, 7)
     dt: Optional[float] = None
+    # adaptive resolution (rvm_config.resolve_tol / resolve_max): a walker whose
+    # estimated extrapolation error exceeds resolve_tol (in logL) is integrated again with every
+    # step halved, up to resolve_max times -- the plan's step is fixed from the sampler's initial
+    # state, the reference's IAS15 adapts to every proposal.  The estimate (the chi2 change when the
+    # coarsest level is dropped) bounds the error vs IAS15 with margin (wide-ball S2 proposals:
+    # max |dlogL| 3.3e-7 at 5e-7, tests/test_gpu_ias15_decisions.py); the bench's tight ball
+    # estimates <= 7.5e-8 and never refines.  resolve_tol = 0 turns it off.
+    resolve_tol: float = 5e-7
+    resolve_max: int = 4
 
     @property
     def mult(self) -> tuple:
@@ -73,6 +82,10 @@ class IntegratorConfig:
             return float(self.dt)
         raw = min_period(planets) / float(self.steps_per_orbit)
         return 2.0 ** (round(math.log2(raw) * DT_GRID) / DT_GRID)
+
+    def resolve(self) -> tuple:
+        """(resolve_tol, resolve_max) for plan_for / LoglPlan."""
+        return float(self.resolve_tol), int(self.resolve_max)
 
     def plan_args(self, planets):
         """(dt, level multipliers, period hint) for plan_for / LoglPlan; the hint (Stumpff series
@@ -120,7 +133,7 @@ class LoglPlan:
     """rvm_plan for one observation set on one device."""
 
     def __init__(self, t, rv, sigma, npoints, n_planets, dt, levels=4, max_walkers=4096, device=None,
-                 period_hint=0.0, inclined=False):
+                 period_hint=0.0, inclined=False, resolve=(0.0, 0)):
         torch = _torch()
         self.lib = _lib.load()
         self.device = torch.device(device) if device is not None else default_device()
@@ -139,9 +152,10 @@ class LoglPlan:
         self.rows = (7 if self.inclined else 5) * self.n_planets
         self.npoints = float(npoints)
         self.max_walkers = int(max_walkers)
+        self.resolve_tol, self.resolve_max = float(resolve[0]), int(resolve[1])
         lm = (C.c_int32 * _lib.RVM_MAX_LEVELS)(*self.mult)
         cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints, lm, self.period_hint,
-                             int(self.inclined))
+                             int(self.inclined), self.resolve_tol, self.resolve_max)
         handle = C.c_void_p()
         dp = C.POINTER(C.c_double)
         with torch.cuda.device(self.device):
@@ -149,6 +163,29 @@ class LoglPlan:
                                           sigma.ctypes.data_as(dp), self.n_obs, self.max_walkers, C.byref(handle))
         _lib.check(rc, "rvm_plan_create")
         self._h = handle
+
+    def faults(self, reset=False, stream=None) -> dict:
+        """rvm_plan_faults: the plan's counters (synchronises the stream): hand-off timeouts, NONFINITE
+        and UNRESOLVED results, refined walker-directions; reset=True zeroes them and restores the
+        hand-off workspace."""
+        vals = [C.c_int64() for _ in range(4)]
+        _lib.check(self.lib.rvm_plan_faults(self._h, int(bool(reset)), *[C.byref(v) for v in vals],
+                                            _lib.stream_handle(stream)), "rvm_plan_faults")
+        return dict(handoff_timeouts=vals[0].value, nonfinite=vals[1].value, unresolved=vals[2].value,
+                    refined=vals[3].value)
+
+    def check_faults(self, what="plan", stream=None) -> dict:
+        """Raise RvmError on hand-off timeouts or NONFINITE results since the last check (emcee
+        raises on a NaN log-probability, mcmc.py:28-35 / emcee 2.2.1; a stalled hand-off must never
+        pass as an ordinary rejection); returns the counters (then reset)."""
+        f = self.faults(reset=True, stream=stream)
+        if f["handoff_timeouts"] or f["nonfinite"]:
+            raise _lib.RvmError(f"{what}: {f['handoff_timeouts']} level-split hand-off timeout(s), {f['nonfinite']} "
+                                f"non-finite log-likelihood(s) on the GPU (rvm_plan_faults)")
+        return f
+
+    def set_handoff_timeout(self, seconds):
+        _lib.check(self.lib.rvm_plan_set_handoff_timeout(self._h, float(seconds)), "rvm_plan_set_handoff_timeout")
 
     def info(self):
         vals = [C.c_int32() for _ in range(4)]
@@ -316,10 +353,24 @@ def obs_arrays(obs):
     return t, rv, er
 
 
+FAULT_CHECK_EVERY = 256  # sampler iterations between automatic rvm_plan_faults checks (0: never)
+
+
+def periodic_fault_check(sampler, plan):
+    """Every `fault_check_every` iterations (a sampler attribute, default FAULT_CHECK_EVERY) read the
+    plan's counters and raise on a hand-off timeout or a NONFINITE result (LoglPlan.check_faults):
+    the check synchronises the stream, so it is amortised over many iterations rather than run per
+    step; `sampler.check_faults()` runs it on demand."""
+    every = getattr(sampler, "fault_check_every", FAULT_CHECK_EVERY)
+    if plan is not None and every and sampler.iteration % every == 0:
+        sampler.last_faults = plan.check_faults(type(sampler).__name__)
+
+
 PLAN_CACHE_SIZE = 32  # plans kept per observation set
 
 
-def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0.0, inclined=False) -> LoglPlan:
+def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0.0, inclined=False,
+             resolve=(0.0, 0)) -> LoglPlan:
     """Cached LoglPlan on an Observation object (keyed by device, the caller's current stream and
     the integrator settings: a plan's workspace is single-stream, include/rvmcmc.h)."""
     torch = _torch()
@@ -327,12 +378,13 @@ def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0
     cache = obs.__dict__.setdefault("_rvm_plans", {})
     mult = level_multipliers(levels)
     stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
-    key = (str(dev), int(stream), int(n_planets), float(dt), mult, float(period_hint), bool(inclined))
+    resolve = (float(resolve[0]), int(resolve[1]))
+    key = (str(dev), int(stream), int(n_planets), float(dt), mult, float(period_hint), bool(inclined), resolve)
     plan = cache.pop(key, None)
     if plan is None or plan.max_walkers < max_walkers:
         t, rv, er = obs_arrays(obs)
         cap = max(int(max_walkers), plan.max_walkers * 2 if plan else 0, 64)
-        plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, mult, cap, dev, period_hint, inclined)
+        plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, mult, cap, dev, period_hint, inclined, resolve)
     cache[key] = plan  # most recently used last
     while len(cache) > PLAN_CACHE_SIZE:  # bounded: the least recently used plan is dropped (freed
         cache.pop(next(iter(cache)))      # when no sampler holds it any more)

@@ -49,7 +49,7 @@ class DeviceOps:
         dt, mult, hint = st.integrator.plan_args(st.planets)
         # room for the 3 n walker slots of a speculative iteration (iteration_begin)
         self.plan = engine.plan_for(sampler.obs, sampler.pmap.n_planets, dt, mult, 3 * sampler.nloc,
-                                    sampler.device, hint, sampler.pmap.inclined)
+                                    sampler.device, hint, sampler.pmap.inclined, st.integrator.resolve())
         self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
         self.track_status = False  # set True to histogram per-walker statuses (costs a small kernel)
         self.status_counts = torch.zeros(4, dtype=torch.int64, device=sampler.device)
@@ -334,6 +334,14 @@ class EnsembleSampler:
             self.half_step(A, self.lnp[0], B, 0)
             self.half_step(B, self.lnp[1], A, 1)
         self.iteration += 1
+        engine.periodic_fault_check(self, self.plan)
+
+    def check_faults(self):
+        """Raise on level-split hand-off timeouts or NONFINITE log-likelihoods since the last check
+        (rvm_plan_faults; also run every FAULT_CHECK_EVERY iterations by step()); returns the
+        counters, including walker-directions refined by the adaptive resolution."""
+        self.last_faults = self.plan.check_faults(type(self).__name__)
+        return self.last_faults
 
     def gather_mirrors(self):
         """Both halves' walker-major mirrors [W/2][dim] in global order: this rank's own at N = 1,

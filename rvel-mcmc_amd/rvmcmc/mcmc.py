@@ -226,7 +226,8 @@ class MhChains:
         self.lib = _lib.load()
         self.pmap = self.state.param_map()
         dt, mult, hint = self.state.integrator.plan_args(self.state.planets)
-        self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, mult, self.n, self.device, hint, self.pmap.inclined)
+        self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, mult, self.n, self.device, hint, self.pmap.inclined,
+                                    self.state.integrator.resolve())
         self.scales = torch.as_tensor(_scales_vector(self.state, scales), device=self.device)
         if X0 is None:
             X0 = np.tile(self.state.get_params()[:, None], (1, self.n))
@@ -272,6 +273,7 @@ class MhChains:
                                                 float(self.state.hillRadiusFactor), 0, 0, self.accepted.data_ptr(),
                                                 st), "rvm_mh_step")
             self.iteration += 1
+            engine.periodic_fault_check(self, self.plan)
             return
         _lib.check(self.lib.rvm_mh_propose(self.dim, self.n, 0, self.X.data_ptr(), self.scales.data_ptr(),
                                            self.step_size, self.seed, self.iteration,
@@ -283,6 +285,12 @@ class MhChains:
                                           draws_accept.data_ptr() if draws_accept is not None else 0,
                                           self.accepted.data_ptr(), st), "rvm_mh_accept")
         self.iteration += 1
+        engine.periodic_fault_check(self, self.plan)
+
+    def check_faults(self):
+        """rvm_plan_faults of the chains' plan: raises on hand-off timeouts / NONFINITE results."""
+        self.last_faults = self.plan.check_faults(type(self).__name__)
+        return self.last_faults
 
 
 from .smala import Alsmala, Smala, SmalaChains  # noqa: E402  (re-export with the reference's module layout)

@@ -224,6 +224,7 @@ class SmalaChains:
                                                         st_h), "rvm_smala_metric_accept")
             self._keep = (lp, g, H, st)
             self.iteration += 1
+            engine.periodic_fault_check(self, self._fault_plan())
             return
         if fused:
             lp, st, rv = self._stencil_logl(self.Xs)
@@ -233,6 +234,7 @@ class SmalaChains:
                 float(self.obs.Npoints), self.alpha, self.eps, cur, prop, self.seed, self.iteration, up,
                 self.accepted.data_ptr(), self.failures.data_ptr(), st_h), "rvm_smala_derive_accept")
             self.iteration += 1
+            engine.periodic_fault_check(self, self._fault_plan())
             return
         self._derive_into(self.Xs, self.prop, fused=False)
         _lib.check(self.lib.rvm_smala_accept(self.P, self.n, 0, self.X.data_ptr(), C.byref(self.cache["_c"]),
@@ -240,6 +242,15 @@ class SmalaChains:
                                              self.iteration, up, self.accepted.data_ptr(), self.failures.data_ptr(),
                                              st_h), "rvm_smala_accept")
         self.iteration += 1
+        engine.periodic_fault_check(self, self._fault_plan())
+
+    def _fault_plan(self):
+        return self.state._plan(self.obs, max_walkers=(2 * self.P + 1) * self.n, device=self.device)
+
+    def check_faults(self):
+        """rvm_plan_faults of the chains' plan: raises on hand-off timeouts / NONFINITE results."""
+        self.last_faults = self._fault_plan().check_faults(type(self).__name__)
+        return self.last_faults
 
 
 class Smala:

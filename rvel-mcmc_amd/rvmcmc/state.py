@@ -168,7 +168,7 @@ class State(object):
     def _plan(self, obs, max_walkers=1, device=None):
         dt, mult, hint = self.integrator.plan_args(self.planets)
         return engine.plan_for(obs, len(self.planets), dt, mult, max_walkers, device, hint,
-                               engine.is_inclined(self.planets))
+                               engine.is_inclined(self.planets), self.integrator.resolve())
 
     def get_rv(self, times):
         """state.py:61-73: model RV (star barycentric vx) at `times`; raises Encounter."""
@@ -208,6 +208,13 @@ class State(object):
         lp, st = self._eval(obs)
         if st == 2:
             raise Encounter("Two particles had a close encounter (d<exit_min_distance).")
+        if st == 3:  # (the reference would hand emcee a NaN, which it refuses)
+            from ._lib import RvmError
+
+            raise RvmError("non-finite chi2 on the GPU (RVM_STATUS_NONFINITE)")
+        if st == 4:
+            log.warning("walker not resolved to the plan's tolerance after the last refinement (UNRESOLVED): "
+                        "logp = -inf")
         return -lp
 
     def get_logp(self, obs):  # state.py:103-110

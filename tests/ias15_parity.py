@@ -12,9 +12,12 @@ IAS15 oracle as the likelihood:
 
 A device decision may differ from the IAS15-driven one only where the two likelihoods legitimately
 differ: walkers whose margin |lnpdiff - ln u| is below MARGIN (the WH + Richardson vs IAS15
-tolerance, T2 5e-8, with headroom), and proposals whose status differs (an encounter caught by one
-integrator and not the other: the kernel tests the exit distance at every kick, REBOUND after each
-IAS15 step -- SURVEY H2).  Both are counted and reported; every other decision must be identical.
+tolerance, T2 1e-6), proposals whose status differs (an encounter caught by one integrator and not
+the other: the kernel tests the exit distance at every kick, REBOUND after each IAS15 step --
+SURVEY H2), and chaotic proposals whose IAS15 logL itself moves by more than ROUNDOFF_REL (relative)
+when an input moves by 1e-15 (ias15_roundoff: no second integrator can follow them).  All three are
+counted and reported; every other decision must be identical, and every other OK proposal must
+have |dlogL| <= MARGIN.
 """
 import json
 import os
@@ -25,6 +28,8 @@ import numpy as np
 import oracle as O
 
 MARGIN = 1e-6  # walkers with |lnpdiff - ln U| < 1e-6 are exempt (counted)
+ROUNDOFF_REL = 1e-9  # IAS15 logL response to a 1e-15 relative input nudge, relative to max(1, |logL|)
+NUDGES = [(0, 4, 1), (-1, 4, -1), (0, 1, 1), (-1, 1, -1)]
 ST_OK, ST_PRIOR, ST_ENC = 0, 1, 2
 
 
@@ -44,6 +49,27 @@ def ias15_logl(P, n_planets, obs, hill=1.0, has_inc=0):
     with ThreadPoolExecutor(nt) as ex:
         parts = list(ex.map(lambda ix: O.logl_ias15_batch(P[ix], n_planets, obs, hill, 1, has_inc), chunks))
     return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]).astype(np.int32)
+
+
+def ias15_roundoff(P, n_planets, obs, ref, hill=1.0, has_inc=0):
+    """Per-proposal roundoff sensitivity of the IAS15 logL: max over 1e-15 relative nudges of one
+    input (l, a of the first / last planet) of |logL' - logL| / max(1, |logL|) (inf where a nudge
+    flips the status).  Measured on the device-independent reference alone, so an exemption by it
+    cannot be earned by the device's own error."""
+    sens = np.zeros(len(P))
+    if len(P) == 0:
+        return sens
+    st0 = None
+    for pl, par, sgn in NUDGES:
+        P2 = np.array(P, dtype=np.float64, copy=True)
+        P2[:, pl, par] *= 1 + sgn * 1e-15
+        r2, s2 = ias15_logl(P2, n_planets, obs, hill, has_inc)
+        if st0 is None:
+            st0 = ias15_logl(P, n_planets, obs, hill, has_inc)[1]
+        both = (s2 == 0) & (st0 == 0)
+        sens[both] = np.maximum(sens[both], np.abs(r2[both] - ref[both]) / np.maximum(1.0, np.abs(ref[both])))
+        sens[s2 != st0] = np.inf
+    return sens
 
 
 def to_oracle(pm, X):
@@ -83,16 +109,16 @@ class Tally:
         self.max_dlogl_ok = 0.0
         self.n_enc_ref = 0
         self.n_prior = 0
-        self.exempt_explained = 0
-        self.disagree_explained = 0
+        self.exempt_roundoff = 0
+        self.disagree_roundoff = 0
         self.n_beyond_margin_dlogl = 0
+        self.beyond_margin_not_roundoff = 0
 
     def add(self, acc_dev, acc_ref, margin, st_dev, st_ref, lnq_dev=None, lnq_ref=None, idx_offset=0,
-            explained=None):
-        """margin: |lnpdiff_ias15 - ln u| per decision.  explained (optional, bool): the decision's
-        margin is below the measured |lnpdiff_device - lnpdiff_ias15|, i.e. the likelihood
-        difference itself can flip it (used where T2 is not expected to hold, e.g. walkers far
-        from the plan's period basis); counted separately."""
+            roundoff=None):
+        """margin: |lnpdiff_ias15 - ln u| per decision.  roundoff (optional): the IAS15 logL's own
+        roundoff sensitivity per proposal (ias15_roundoff); proposals above ROUNDOFF_REL are
+        exempt from the decision and T2 checks (counted separately)."""
         acc_dev = np.asarray(acc_dev, bool)
         acc_ref = np.asarray(acc_ref, bool)
         st_dev = np.asarray(st_dev)
@@ -100,11 +126,13 @@ class Tally:
         near = margin < MARGIN
         sdiff = st_dev != st_ref
         exempt = near | sdiff
-        if explained is not None:
-            expl = np.asarray(explained, bool) & ~exempt
-            self.exempt_explained += int(expl.sum())
-            self.disagree_explained += int(((acc_dev != acc_ref) & expl).sum())
-            exempt = exempt | expl
+        chaotic = np.zeros(len(acc_dev), bool)
+        if roundoff is not None:
+            chaotic = np.asarray(roundoff) > ROUNDOFF_REL
+            ro = chaotic & ~exempt
+            self.exempt_roundoff += int(ro.sum())
+            self.disagree_roundoff += int(((acc_dev != acc_ref) & ro).sum())
+            exempt = exempt | ro
         same = acc_dev == acc_ref
         self.n += len(acc_dev)
         self.agree += int(same.sum())
@@ -124,6 +152,11 @@ class Tally:
                 dl = np.abs(lnq_dev[ok] - lnq_ref[ok])
                 self.max_dlogl_ok = max(self.max_dlogl_ok, float(np.max(dl)))
                 self.n_beyond_margin_dlogl += int((dl > MARGIN).sum())
+                self.beyond_margin_not_roundoff += int(((dl > MARGIN) & ~chaotic[ok]).sum())
+                nc = ~chaotic[ok]
+                if nc.any():
+                    self.max_dlogl_ok_not_roundoff = max(getattr(self, "max_dlogl_ok_not_roundoff", 0.0),
+                                                         float(np.max(dl[nc])))
 
     def report(self, **extra):
         d = {"test": self.name, "decisions": self.n, "identical": self.agree,
@@ -132,8 +165,11 @@ class Tally:
              "mismatches_not_exempt": len(self.mismatch), "accepted_ias15": self.accepted_ref,
              "encounters_ias15": self.n_enc_ref, "prior_rejections": self.n_prior,
              "max_abs_dlogl_ok_proposals": self.max_dlogl_ok, "ok_proposals_dlogl_above_margin":
-             self.n_beyond_margin_dlogl, "exempt_explained_by_dlogl": self.exempt_explained,
-             "differing_explained_by_dlogl": self.disagree_explained, "margin": MARGIN}
+             self.n_beyond_margin_dlogl, "exempt_ias15_roundoff_sensitive": self.exempt_roundoff,
+             "differing_ias15_roundoff_sensitive": self.disagree_roundoff,
+             "ok_proposals_dlogl_above_margin_not_roundoff": self.beyond_margin_not_roundoff,
+             "max_abs_dlogl_ok_proposals_not_roundoff": getattr(self, "max_dlogl_ok_not_roundoff", 0.0),
+             "margin": MARGIN, "roundoff_rel": ROUNDOFF_REL}
         d.update(extra)
         line = json.dumps(d)
         print(line)

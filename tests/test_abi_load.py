@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 8
+    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 9
 
 
 def test_python_binding_matches_header():
@@ -66,6 +66,13 @@ def test_argument_errors_do_not_touch_the_device():
     cfg2 = _lib.RvmConfig(2, 0.5, 4, 100.0)
     rc = lib.rvm_plan_create(C.byref(cfg2), t, ones, ones, n, 64, C.byref(h))
     assert rc < 0 and b"too many epochs" in lib.rvm_last_error()
+    # adaptive resolution bounds, and the fault-counter / timeout entry points on a null plan
+    cfg3 = _lib.RvmConfig(2, 0.5, 4, 100.0)
+    cfg3.resolve_tol, cfg3.resolve_max = 5e-7, 9
+    rc = lib.rvm_plan_create(C.byref(cfg3), z, z, z, 1, 64, C.byref(h))
+    assert rc < 0 and b"resolve_max" in lib.rvm_last_error()
+    assert lib.rvm_plan_faults(None, 0, None, None, None, None, 0) < 0
+    assert lib.rvm_plan_set_handoff_timeout(None, 1.0) < 0
     # workspace: per (chain, pair i >= j) and direction, 4 f64 partial sums and an int32 status
     assert lib.rvm_logl_derivs_workspace_bytes(256, 10) == 256 * 55 * 2 * (4 * 8 + 4)
 
@@ -75,8 +82,9 @@ def test_struct_layouts_match_header():
     import ctypes as C
 
     # int32 n_planets | pad | f64 dt | int32 n_levels | pad | f64 npoints | int32 mult[6] | f64 hint
-    # | int32 inclined | pad
-    assert C.sizeof(_lib.RvmConfig) == 72 and _lib.RvmConfig.inclined.offset == 64
+    # | int32 inclined | pad | f64 resolve_tol | int32 resolve_max | pad
+    assert C.sizeof(_lib.RvmConfig) == 88 and _lib.RvmConfig.inclined.offset == 64
+    assert _lib.RvmConfig.resolve_tol.offset == 72 and _lib.RvmConfig.resolve_max.offset == 80
     assert _lib.RvmConfig.level_mult.offset == 32 and _lib.RvmConfig.period_hint.offset == 56
     assert C.sizeof(_lib.SmalaCache) == 7 * 8
 
@@ -97,9 +105,10 @@ def test_struct_layouts_match_compiled_header(tmp_path):
 #include <stdio.h>
 #include "rvmcmc.h"
 int main(void) {
-    printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(rvm_config), offsetof(rvm_config, level_mult),
+    printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(rvm_config), offsetof(rvm_config, level_mult),
            offsetof(rvm_config, inclined), sizeof(rvm_smala_cache), sizeof(rvm_param_map),
-           offsetof(rvm_param_map, src), offsetof(rvm_param_map, base));
+           offsetof(rvm_param_map, src), offsetof(rvm_param_map, base), offsetof(rvm_config, resolve_tol),
+           offsetof(rvm_config, resolve_max));
     return 0;
 }
 """)
@@ -108,4 +117,4 @@ int main(void) {
     got = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
     assert got == [C.sizeof(_lib.RvmConfig), _lib.RvmConfig.level_mult.offset, _lib.RvmConfig.inclined.offset,
                    C.sizeof(_lib.SmalaCache), C.sizeof(_lib.ParamMapC), _lib.ParamMapC.src.offset,
-                   _lib.ParamMapC.base.offset]
+                   _lib.ParamMapC.base.offset, _lib.RvmConfig.resolve_tol.offset, _lib.RvmConfig.resolve_max.offset]

@@ -62,7 +62,7 @@ def _device_logl(ens_or_plan, pm, Q, hill):
     return lp.cpu().numpy(), st.cpu().numpy()
 
 
-def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, explain=False, seed=2017, ball_seed=0):
+def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, roundoff=False, seed=2017, ball_seed=0):
     """Run the device EnsembleSampler (default path) and compare its decisions, iteration by
     iteration, with emcee 2.2.1 restated in numpy on IAS15 logL and the same Philox draws."""
     torch = _torch()
@@ -104,13 +104,22 @@ def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, explain=Fa
                 acc_ref = d_ref > np.log(u3)
                 margin = np.abs(d_ref - np.log(u3))
                 margin = np.where(np.isnan(margin), np.inf, margin)
-                expl = margin <= np.abs(d_dev - d_ref)
+            sens = None
+            if roundoff:
+                # the IAS15 logL's own roundoff sensitivity, for the proposals where it could matter
+                # (a decision that differs, or an OK proposal beyond T2): chaotic ones are exempt
+                sens = np.zeros(n)
+                okk = (sq_dev == 0) & (sq_ref == 0)
+                with np.errstate(invalid="ignore"):
+                    look = (d_dev > np.log(u3)) != acc_ref
+                    look |= okk & (np.abs(lq_dev - lq_ref) > IP.MARGIN)
+                ix = np.nonzero(look & (sq_ref == 0))[0]
+                sens[ix] = IP.ias15_roundoff(IP.to_oracle(pm, q[ix]), npl, obs, lq_ref[ix], hill)
             acc_dev = np.any(after[h] != before[h], axis=1)
             # the device sampler itself is exact: its decisions follow its own logL bit for bit
             np.testing.assert_array_equal(acc_dev, d_dev > np.log(u3))
             np.testing.assert_array_equal(after[h][acc_dev], q[acc_dev])
-            tally.add(acc_dev, acc_ref, margin, sq_dev, sq_ref, lq_dev, lq_ref, idx_offset=h * hk,
-                      explained=expl if explain else None)
+            tally.add(acc_dev, acc_ref, margin, sq_dev, sq_ref, lq_dev, lq_ref, idx_offset=h * hk, roundoff=sens)
             lnp_ref[h] = np.where(acc_dev, lq_ref, lnp_ref[h])  # follow the device chain
     return tally, dict(walkers=W, ball=ball, iterations=iterations, warm_iterations=warm, speculative=bool(spec))
 
@@ -129,16 +138,20 @@ def test_stretch_vs_ias15_bench_config():
 
 def test_stretch_vs_ias15_wide_ball_encounters():
     """A wide initial ball (0.6 x the emcee scales): prior rejections and close-encounter exits
-    occur; walkers far from the plan's period basis leave the T2 regime (their logL is still
-    compared, and a flipped decision must be explained by the measured logL difference)."""
+    occur, and most proposals are far from the plan's period basis (short periods, eccentric or
+    crossing orbits).  The adaptive resolution (IntegratorConfig.resolve_tol) keeps
+    every OK proposal within T2 (1e-6) of IAS15 all the same; only proposals on which IAS15 itself
+    is roundoff-sensitive (a 1e-15 input nudge moves its logL by > 1e-9 relative) are exempt, and
+    counted.  (Round 2, fixed step: 580 OK proposals beyond 1e-6, max |dlogL| 81.)"""
     tally, info = stretch_parity("stretch/wide-ball S2 2048 walkers", S2_PLANETS, s2_obs_oracle(), 2048, 0.6,
-                                 warm=0, explain=True, ball_seed=3)
+                                 warm=0, roundoff=True, ball_seed=3)
     rep = tally.report(**info)
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
     assert rep["encounters_ias15"] > 20 and rep["prior_rejections"] > 20
-    assert rep["exempt_status_disagreement"] <= max(2, rep["decisions"] // 100)
-    assert rep["identical"] >= rep["decisions"] - rep["exempt_status_disagreement"] - rep["exempt_near_margin"] \
-        - rep["exempt_explained_by_dlogl"]
+    assert rep["exempt_status_disagreement"] <= max(4, rep["decisions"] // 100)
+    assert rep["ok_proposals_dlogl_above_margin_not_roundoff"] == 0
+    assert rep["max_abs_dlogl_ok_proposals_not_roundoff"] <= T2_ABS
+    assert rep["exempt_ias15_roundoff_sensitive"] <= rep["decisions"] // 100
 
 
 def test_stretch_vs_ias15_hd155358():

@@ -1,0 +1,216 @@
+"""Adaptive resolution and the plan's fault counters (include/rvmcmc.h).
+
+The reference integrates every proposal with adaptive IAS15 (state.py:36-73), so its accuracy does
+not depend on where a walker is; a plan's Wisdom-Holman step is fixed from the sampler's initial
+state.  With rvm_config.resolve_tol a direction whose extrapolation-error estimate (the chi2
+change when the coarsest Richardson level is dropped) exceeds resolve_tol / 2 is integrated again
+with every step halved, up to resolve_max times.  Checked here:
+
+  * T1 of the adaptive kernel against the oracle's restatement of the same rule
+    (oracle.logl_whx_adapt_batch), both launch layouts, on a wide ball that refines heavily;
+  * the bench's tight ball never refines, and gives the bits of a plan without the rule;
+  * resolve_max = 0 flags (UNRESOLVED) exactly the walkers the oracle flags;
+  * a level-split hand-off that gives up is counted (rvm_plan_faults), its walkers are NONFINITE,
+    the plan stays poisoned until reset, and after the reset the next launch is bit-identical to a
+    fresh plan's.
+Reference-physics (IAS15) accuracy of the rule over the proposals a sampler makes is in
+tests/test_gpu_ias15_decisions.py.
+"""
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import S2_PLANETS, S2_SCALES, s2_obs_oracle
+
+pytestmark = pytest.mark.gpu
+
+TOL, RMAX = 5e-7, 4
+T1_REL = 1e-11 * 35.0  # tests/test_gpu_logl.py: 1e-11 sum|w| (levels 4..7)
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch
+
+
+def _plan(obs, W, resolve=(TOL, RMAX)):
+    from rvmcmc import engine
+
+    dt, mult, hint = engine.IntegratorConfig().plan_args(S2_PLANETS)
+    t, rv, er = engine.obs_arrays(obs)
+    return engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint, resolve=resolve), dt, mult
+
+
+def _x0():
+    return np.array([p[k] for p in S2_PLANETS for k in "mahkl"]), np.array([S2_SCALES[k] for _ in S2_PLANETS
+                                                                             for k in "mahkl"])
+
+
+def wide_walkers(W, ball=0.6, seed=3):
+    """Half a sampler-like ball (x0 + ball * scales * N(0,1), mcmc.py:45-51), half stretch
+    proposals between its members (q = c - z (c - x), z in [1/2, 2]): [W][10] kernel rows."""
+    x0, sc = _x0()
+    rng = np.random.default_rng(seed)
+    n = W // 2
+    X = x0 + ball * sc * rng.standard_normal((n, 10))
+    j = rng.integers(0, n, W - n)
+    z = (rng.random(W - n) + 1.0) ** 2 / 2.0
+    Q = X[j] - z[:, None] * (X[j] - X[:W - n])
+    return np.concatenate([X, Q])
+
+
+def _oracle_P(X):
+    P = np.zeros((len(X), 2, 7))
+    P[:, :, :5] = X.reshape(-1, 2, 5)
+    return P
+
+
+def _run(plan, X):
+    torch = _torch()
+    K = torch.as_tensor(np.ascontiguousarray(X.T), device="cuda")
+    lp, st, _ = plan.logl(K)
+    torch.cuda.synchronize()
+    return lp.cpu().numpy(), st.cpu().numpy()
+
+
+def _par(fn, P, nt=16):
+    idx = np.array_split(np.arange(len(P)), nt)
+    with ThreadPoolExecutor(nt) as ex:
+        parts = list(ex.map(lambda ix: fn(P[ix]), idx))
+    return [np.concatenate([p[k] for p in parts]) for k in range(len(parts[0]))]
+
+
+def _adapt_oracle(P, obs, dt, mult, tol=TOL, rmax=RMAX):
+    return _par(lambda p: O.logl_whx_adapt_batch(p, 2, obs, dt, mult, tol, rmax), P)
+
+
+@pytest.mark.parametrize("W", [512, 6144])  # LDS-coupled layout / level-split layout (bench shape)
+def test_t1_adaptive_wide_ball(W):
+    obs = s2_obs_oracle()
+    plan, dt, mult = _plan(obs, W)
+    X = wide_walkers(W)
+    got, st = _run(plan, X)
+    f = plan.faults(reset=True)
+    P = _oracle_P(X)
+    ref, st_ref, rf, est, margin = _adapt_oracle(P, obs, dt, mult)
+    # chaotic walkers (close approaches) and refinement decisions at roundoff distance from the
+    # bound may legitimately go the other way in a second implementation: the oracle's own
+    # response to 1e-15 relative input nudges (of logL, of the status, of the refinements taken and
+    # of the final estimate -- a difference of two extrapolations, which near a close approach moves
+    # by up to tens of percent under such a nudge), and its closest approach to the bound
+    sens = np.zeros(W)
+    flips = np.zeros(W, dtype=bool)
+    for pl, par, sgn in [(0, 4, 1), (1, 4, -1), (0, 1, 1)]:
+        P2 = P.copy()
+        P2[:, pl, par] *= 1 + sgn * 1e-15
+        r2, s2, rf2, est2, _ = _adapt_oracle(P2, obs, dt, mult)
+        flips |= (s2 != st_ref) | np.any(rf2 != rf, axis=1)
+        with np.errstate(invalid="ignore"):  # (an estimate whose roundoff response is not small
+            # against its distance from the bound)
+            flips |= np.any(np.abs(est2 - est) > 0.02 * np.abs(est - 0.5 * TOL), axis=1)
+        both = (st_ref == 0) & (s2 == 0)
+        sens[both] = np.maximum(sens[both], np.abs(r2[both] - ref[both]) / np.maximum(1.0, np.abs(ref[both])))
+    sensitive = flips | (sens > 1e-9) | (margin.min(axis=1) < 1e-6)
+    refined = int(rf.sum())
+    print(f"W={W}: oracle refined walker-directions {refined} (passes {int((2 ** rf - 1).sum())}), kernel "
+          f"counters {f}, statuses {np.bincount(st, minlength=5).tolist()}, sensitive {int(sensitive.sum())}")
+    assert refined > W // 10, "the wide ball must exercise the refinement passes"
+    assert f["refined"] > 0 and f["handoff_timeouts"] == 0
+    mism = st != st_ref
+    assert np.all(~mism | sensitive), np.nonzero(mism & ~sensitive)
+    assert mism.sum() <= max(2, W // 100)
+    ok = (st == 0) & (st_ref == 0)
+    err = np.abs(got[ok] - ref[ok]) / np.maximum(1.0, np.abs(ref[ok]))
+    bound = np.maximum(T1_REL, 1e3 * sens[ok])
+    bad = (err > bound) & ~sensitive[ok]
+    assert not bad.any(), (np.nonzero(ok)[0][bad][:10], err[bad][:10])
+    assert np.mean(err <= T1_REL) > 0.9
+    # walkers the oracle leaves UNRESOLVED are UNRESOLVED on the device too (up to sensitivity)
+    assert np.all(((st == 4) == (st_ref == 4)) | sensitive)
+    assert f["unresolved"] == int((st == 4).sum())
+
+
+def test_tight_ball_never_refines_and_keeps_the_bits():
+    """The bench config (6144 walker slots of the tight S2 ball): no walker crosses the bound, so
+    the rule costs nothing and changes no bit."""
+    obs = s2_obs_oracle()
+    W = 6144
+    x0, sc = _x0()
+    X = x0 + 1e-3 * sc * np.random.default_rng(7).standard_normal((W, 10))
+    plan, _, _ = _plan(obs, W)
+    plan_off, _, _ = _plan(obs, W, resolve=(0.0, 0))
+    got, st = _run(plan, X)
+    got0, st0 = _run(plan_off, X)
+    f = plan.faults()
+    np.testing.assert_array_equal(st, st0)
+    np.testing.assert_array_equal(got, got0)
+    assert f == dict(handoff_timeouts=0, nonfinite=0, unresolved=0, refined=0), f
+
+
+def test_flag_only_matches_oracle():
+    """resolve_max = 0: walkers above the bound are reported UNRESOLVED (logl -inf), not refined."""
+    obs = s2_obs_oracle()
+    W = 256
+    X = wide_walkers(W, ball=0.3, seed=11)
+    plan, dt, mult = _plan(obs, W, resolve=(TOL, 0))
+    got, st = _run(plan, X)
+    ref, st_ref, rf, est, margin = _adapt_oracle(_oracle_P(X), obs, dt, mult, TOL, 0)
+    near = margin.min(axis=1) < 1e-6
+    assert (st_ref == 4).sum() > 10
+    assert np.all((st == st_ref) | near)
+    assert np.all(np.isneginf(got[st == 4]))
+    f = plan.faults()
+    assert f["unresolved"] == int((st == 4).sum()) and f["refined"] == 0
+
+
+def test_handoff_timeout_is_reported_and_reset():
+    """A level-split hand-off that gives up (forced by a 10 ns timeout) is counted, its walkers
+    are NONFINITE, later launches on the poisoned plan report NONFINITE rather than stale values,
+    check_faults raises, and after the reset the next launch gives a fresh plan's bits."""
+    from rvmcmc import _lib
+
+    obs = s2_obs_oracle()
+    W = 6144
+    x0, sc = _x0()
+    X = x0 + 1e-3 * sc * np.random.default_rng(5).standard_normal((W, 10))
+    fresh, _, _ = _plan(obs, W)
+    want, st_want = _run(fresh, X)
+    plan, _, _ = _plan(obs, W)
+    plan.set_handoff_timeout(1e-8)
+    _, st = _run(plan, X)
+    f = plan.faults()
+    assert f["handoff_timeouts"] > 0 and f["nonfinite"] > 0, f
+    assert (st == _lib.RVM_STATUS_NONFINITE).sum() == f["nonfinite"]
+    plan.set_handoff_timeout(2.0)
+    _, st2 = _run(plan, X)  # poisoned workspace: nothing stale passes as a value
+    assert np.all(st2 == _lib.RVM_STATUS_NONFINITE)
+    with pytest.raises(_lib.RvmError, match="hand-off timeout"):
+        plan.check_faults("test")  # (reads and resets)
+    got, st3 = _run(plan, X)
+    np.testing.assert_array_equal(st3, st_want)
+    np.testing.assert_array_equal(got, want)
+    assert plan.faults()["handoff_timeouts"] == 0
+
+
+def test_level_split_encounter_on_the_last_lower_lane_stays_local():
+    """Regression (found by the wide-ball T1 test above): the level-split head -> tail hand-off
+    rebuilt the 64-bit encounter mask from two 32-bit readfirstlane values and the lower one
+    sign-extended, so an encounter of the walker on lanes 30/31 (slot 15 of a 32-walker group) marked
+    all 16 walkers of the group's upper half ENCOUNTER.  Walkers with planet 2 beside planet 1 on
+    slot 15 of every other group of a tight ball: every other walker must stay OK, as the oracle says."""
+    obs = s2_obs_oracle()
+    W = 6144
+    x0, sc = _x0()
+    X = x0 + 1e-3 * sc * np.random.default_rng(9).standard_normal((W, 10))
+    hit = np.arange(15, W, 64)
+    X[hit, 6] = X[hit, 1] * 1.01  # planet 2 next to planet 1: an encounter from t = 0
+    X[hit, 9] = X[hit, 4] + 0.01
+    plan, dt, mult = _plan(obs, W)
+    got, st = _run(plan, X)
+    ref, st_ref, _, _, _ = _adapt_oracle(_oracle_P(X), obs, dt, mult)
+    assert np.all(st_ref[hit] == 2) and np.all(np.delete(st_ref, hit) == 0)
+    np.testing.assert_array_equal(st, st_ref)
