@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 9
+#define RVM_ABI_VERSION 10
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -85,8 +85,10 @@ typedef struct {
     double resolve_tol;    /* adaptive resolution: bound on a walker's |logL| error as
                               estimated from the extrapolation itself -- the change of chi2/npoints
                               when the coarsest level is dropped -- split evenly over its two
-                              directions.  A direction above its half is integrated again with every
-                              step halved, up to resolve_max times (the reference's IAS15 adapts its
+                              directions.  A direction above its half first gets one extra level
+                              (the extension, rvm_plan_extension) joined to its stored levels; if
+                              that does not settle it, it is integrated again with every step
+                              halved, up to resolve_max times (the reference's IAS15 adapts its
                               step to the orbit; a fixed plan step does not).  <= 0: off            */
     int32_t resolve_max;   /* 0..8 refinements; 0 with resolve_tol > 0: flag (UNRESOLVED) only      */
 } rvm_config;
@@ -105,6 +107,12 @@ void rvm_plan_destroy(rvm_plan* plan);
 /* schedule introspection: total level-1 steps per direction (fwd, bwd), epochs per direction */
 int rvm_plan_info(const rvm_plan* plan, int32_t* steps_fwd, int32_t* steps_bwd, int32_t* epochs_fwd,
                   int32_t* epochs_bwd);
+/* The adaptive resolution's extension level of a plan: *ext_mult = its steps per base step
+ * (max(level_mult) + 1), or 0 when the plan has none -- resolution off or flag-only, n_levels < 2 or
+ * = RVM_MAX_LEVELS, or its stored levels (8 * n_levels * 2 * max(epochs per direction) * max_walkers
+ * bytes of device memory, written by every launch) above RVM_EXT_MAX_BYTES. */
+#define RVM_EXT_MAX_BYTES (4ull << 30)
+int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult);
 
 /* Counters of a plan since its creation or the last reset, read in order on `stream` (the call
  * synchronises that stream; any output pointer may be NULL):
@@ -113,7 +121,7 @@ int rvm_plan_info(const rvm_plan* plan, int32_t* steps_fwd, int32_t* steps_bwd, 
  *                     and every later level-split launch on the plan reports NONFINITE until reset
  *   nonfinite         walkers finished with RVM_STATUS_NONFINITE (any launch on the plan)
  *   unresolved        walkers finished with RVM_STATUS_UNRESOLVED
- *   refined           walker-directions integrated again by the adaptive resolution (passes)
+ *   refined           walker-direction passes of the adaptive resolution (extension + halvings)
  * reset != 0: zero the counters and restore the hand-off workspace, after the stream's earlier work.
  * The samplers (rvmcmc) check this and raise on timeouts / non-finite results (mcmc.py:28-35: emcee
  * refuses NaN log-probabilities) rather than treating them as ordinary rejections. */

@@ -72,8 +72,8 @@ def lib():
                                              C.c_int, C.c_double, C.c_double, C.c_int, ip, dp,
                                              C.POINTER(C.c_int32)]
         L.rvo_logl_whx_adapt_batch.argtypes = [C.c_int, C.c_int, dp, C.c_int, C.c_int, C.c_double, dp, dp, dp,
-                                               C.c_int, C.c_double, C.c_double, C.c_int, ip, C.c_double, C.c_int, dp,
-                                               C.POINTER(C.c_int32), C.POINTER(C.c_int32), dp]
+                                               C.c_int, C.c_double, C.c_double, C.c_int, ip, C.c_int, C.c_double, C.c_int,
+                                               dp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dp]
         _LIB = L
     return _LIB
 
@@ -240,14 +240,23 @@ def logl_whx_seq_batch(params, np_, obs, dt, mult, hill_factor=1.0, has_hk=1, ha
 ORACLE_UNRESOLVED = 4
 
 
-def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.0, has_hk=1, has_inc=0):
+def ext_multiplier(mult, rf_max):
+    """The extension level's steps per base step (0: none): one more than the finest level, when
+    the plan refines at all and has room for one more level (RVM_MAX_LEVELS = 6; rvm_abi.hip --
+    a plan whose stored levels would not fit its memory cap has none: rvm_plan_extension)."""
+    m = [int(x) for x in mult]
+    return max(m) + 1 if rf_max > 0 and 2 <= len(m) < 6 else 0
+
+
+def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.0, has_hk=1, has_inc=0, ext=None):
     """The kernel's algorithm with adaptive resolution (rvm_config.resolve_tol / resolve_max):
-    each direction refines (every step halved) while its extrapolation-error estimate exceeds
-    tol / 2.
-    params [W][np][7] -> (logl[W], status[W], refinements [W][2], estimates [W][2],
-    margins [W][2]); margin = the closest any pass's estimate came to the bound, min |est/(tol/2) - 1|
-    (a decision at roundoff distance may go the other way in a second implementation).  tol = 0 is
-    the plain rvo_whx algorithm."""
+    a direction whose extrapolation-error estimate exceeds tol / 2 gets the extension level (ext
+    steps per base step; default ext_multiplier) and, if that does not settle it, passes with every
+    step halved (rvoracle.c whx_direction_adapt).
+    params [W][np][7] -> (logl[W], status[W], stages [W][2] (0 the plan's step, 1 the extension,
+    1 + r r halvings; without the extension r), estimates [W][2], margins [W][2]); margin = the
+    closest any decision came to its bound, min |x/bound - 1| (a decision at roundoff distance may
+    go the other way in a second implementation).  tol = 0 is the plain rvo_whx algorithm."""
     pl = _f64(params)
     W = pl.shape[0]
     t = _f64(np.concatenate([obs.tf, obs.tb]))
@@ -259,10 +268,11 @@ def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.
     est = np.zeros((W, 4))
     m, mp = _mult(mult)
     tol_dir = 0.5 * float(tol) if tol > 0 else np.inf
+    ext = ext_multiplier(mult, rf_max) if ext is None else int(ext)
     lib().rvo_logl_whx_adapt_batch(W, np_, _p(pl), has_hk, has_inc, float(hill_factor), _p(t), _p(rv), _p(er),
-                                   len(t), float(obs.Npoints), float(dt), len(m), mp, tol_dir, int(rf_max), _p(out),
-                                   st.ctypes.data_as(C.POINTER(C.c_int32)), rf.ctypes.data_as(C.POINTER(C.c_int32)),
-                                   _p(est))
+                                   len(t), float(obs.Npoints), float(dt), len(m), mp, ext, tol_dir, int(rf_max),
+                                   _p(out), st.ctypes.data_as(C.POINTER(C.c_int32)),
+                                   rf.ctypes.data_as(C.POINTER(C.c_int32)), _p(est))
     return out, st, rf, est[:, :2], est[:, 2:]
 
 

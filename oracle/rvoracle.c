@@ -996,26 +996,48 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /* estimated by the change of chi2 when the coarsest level is dropped,                          */
 /*   est = sum_i |(r_i - o_i)^2 - (r3_i - o_i)^2| / sigma_i^2 / npoints,                        */
 /* r = all levels' Richardson RV, r3 = the finer nl - 1 levels' (their own Lagrange weights).   */
-/* While est > tol_dir the direction is integrated again with every step halved (level k: mult  */
-/* 2^rf steps per base step), up to rf_max times; still above after that: RVO_UNRESOLVED.       */
+/* Above the bound (est > tol_dir):                                                             */
+/*  stage 1, the extension (ext_mult > 0): one more level, ext_mult steps per base step, joins  */
+/*   the stored levels: r5 = Richardson over all nl + 1 levels, r4x = over the finer nl levels   */
+/*   (the coarsest dropped).  Accepted (chi2 from r5) when both                                 */
+/*     sum |(r5 - o)^2 - (r4x - o)^2| / s2 <= EXT_TOL_FRAC * tol_dir * npoints   (converged)    */
+/*     sum |(r5 - o)^2 - (r - o)^2| / s2   <= EXT_GAIN_MAX * (est * npoints)     (consistent:   */
+/*   the extension moved the answer by at most half the first estimate);                        */
+/*  stages 2..: every step halved (level k: mult 2^rf steps per base step, rf = 1..rf_max) while  */
+/*   est > tol_dir; still above after rf_max: RVO_UNRESOLVED.                                   */
 /* An encounter or non-finite RV ends the direction at once (no refinement).                    */
 /* ------------------------------------------------------------------------------------------ */
 enum { RVO_UNRESOLVED = 4 };
+#define EXT_TOL_FRAC 0.25
+#define EXT_GAIN_MAX 0.5
 
+
+static double margin_of(double x, double bound) {
+    return bound > 0.0 ? fabs(x / bound - 1.0) : INFINITY;
+}
 
 static int whx_direction_adapt(int np, const double* pl, double hill_factor, const double* at, const double* ob,
-                               const double* s2, int cnt, double sign, double dt, int nl, const int* mult,
-                               double tol_dir, int rf_max, double npoints, double* chi2_out, int* rf_out,
+                               const double* s2, int cnt, double sign, double dt, int nl, const int* mult, int ext_mult,
+                               double tol_dir, int rf_max, double npoints, double* chi2_out, int* stage_out,
                                double* est_out, double* margin_out) {
-    double w[8], w3[8];
+    double w[8], w3[8], w5[9], w4x[9];
     rvo_richardson_weights_seq(nl, mult, w);
     w3[0] = 0.0;
     if (nl >= 2) rvo_richardson_weights_seq(nl - 1, mult + 1, w3 + 1);
-    double* lv = (double*)malloc(sizeof(double) * (size_t)(8 * cnt + 1));
-    int st = RVO_OK;
+    const int ext = ext_mult > 0 && rf_max > 0 && nl >= 2 && nl < 8;
+    if (ext) {
+        int m5[9];
+        for (int k = 0; k < nl; k++) m5[k] = mult[k];
+        m5[nl] = ext_mult;
+        rvo_richardson_weights_seq(nl + 1, m5, w5);
+        w4x[0] = 0.0;
+        rvo_richardson_weights_seq(nl, m5 + 1, w4x + 1);
+    }
+    double* lv = (double*)malloc(sizeof(double) * (size_t)(9 * cnt + 1));
+    double* lv0 = (double*)malloc(sizeof(double) * (size_t)(8 * cnt + 1)); /* the main pass's levels */
+    int st = RVO_OK, stage = 0;
     double chi2 = 0.0, est = 0.0, margin = INFINITY;
-    int rf = 0;
-    for (rf = 0; rf <= rf_max; rf++) {
+    for (int rf = 0; rf <= rf_max; rf++) {
         st = RVO_OK;
         for (int k = 0; k < nl; k++) {
             const int s = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, mult[k] << rf, lv + (size_t)k * cnt);
@@ -1031,30 +1053,64 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
             chi2 += (r - ob[i]) * (r - ob[i]) / s2[i];
             est += fabs((r - r3) * ((r - ob[i]) + (r3 - ob[i]))) / s2[i];
         }
+        const double est_raw = est;
         est /= npoints;
-        if (nl >= 2 && tol_dir < INFINITY && fabs(est / tol_dir - 1.0) < margin) margin = fabs(est / tol_dir - 1.0);
+        if (nl >= 2 && tol_dir < INFINITY && margin_of(est, tol_dir) < margin) margin = margin_of(est, tol_dir);
         if (nl < 2 || !(est > tol_dir)) break;
+        if (rf == 0 && ext) {
+            /* stage 1: the extension level over the main pass's stored levels */
+            stage = 1;
+            memcpy(lv0, lv, sizeof(double) * (size_t)nl * cnt);
+            double* lx = lv + (size_t)nl * cnt;
+            st = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, ext_mult, lx);
+            if (st != RVO_OK) break;
+            double c5 = 0.0, e5 = 0.0, dd = 0.0;
+            for (int i = 0; i < cnt; i++) {
+                double r = 0.0, r5 = 0.0, r4x = 0.0;
+                for (int k = 0; k < nl; k++) r += w[k] * lv0[(size_t)k * cnt + i];
+                for (int k = 0; k < nl; k++) r5 += w5[k] * lv0[(size_t)k * cnt + i];
+                r5 += w5[nl] * lx[i];
+                for (int k = 1; k < nl; k++) r4x += w4x[k] * lv0[(size_t)k * cnt + i];
+                r4x += w4x[nl] * lx[i];
+                const double q = r5 - ob[i];
+                c5 += (q * q) / s2[i];
+                e5 += fabs((r5 - r4x) * (q + (r4x - ob[i]))) / s2[i];
+                dd += fabs((r5 - r) * (q + (r - ob[i]))) / s2[i];
+            }
+            const double b5 = EXT_TOL_FRAC * tol_dir * npoints, bg = EXT_GAIN_MAX * est_raw;
+            if (margin_of(e5, b5) < margin) margin = margin_of(e5, b5);
+            if (margin_of(dd, bg) < margin) margin = margin_of(dd, bg);
+            if (e5 <= b5 && dd <= bg) {
+                chi2 = c5;
+                est = e5 / npoints;
+                break;
+            }
+        }
         if (rf == rf_max) {
             st = RVO_UNRESOLVED;
             break;
         }
+        stage = (ext ? 2 : 1) + rf;
     }
     free(lv);
+    free(lv0);
     *chi2_out = chi2;
-    *rf_out = rf > rf_max ? rf_max : rf;
+    *stage_out = stage;
     *est_out = est;
     *margin_out = margin;
     return st;
 }
 
-/* logp with adaptive resolution: rf_used[2] / est[2] (fwd, bwd) report the refinements taken and
+/* logp with adaptive resolution: rf_used[2] / est[2] (fwd, bwd) report the stage reached (0 the
+ * plan's step, 1 the extension, 2.. halvings; without the extension 1.. halvings) and
  * the final estimates.  Status: PRIOR, else the forward direction's non-OK status, else the
  * backward one's (the kernel's direction meeting).  est[4]: the final estimates (fwd, bwd) and the
  * closest any pass came to the bound, min |est / tol_dir - 1| (fwd, bwd): a refinement decision
  * a second implementation may take the other way when that is at roundoff level. */
 int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
                        const double* rvobs, const double* err, int n, double npoints, double dt, int nl,
-                       const int* mult, double tol_dir, int rf_max, double* logl, int32_t* rf_used, double* est) {
+                       const int* mult, int ext_mult, double tol_dir, int rf_max, double* logl, int32_t* rf_used,
+                       double* est) {
     rf_used[0] = rf_used[1] = 0;
     est[0] = est[1] = 0.0;
     est[2] = est[3] = INFINITY;
@@ -1090,7 +1146,7 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
         double e = 0.0, mg = INFINITY;
         if (cnt)
             sd[dir] = whx_direction_adapt(np, pl, hill_factor, at, ob, s2, cnt, dir == 0 ? 1.0 : -1.0, dt, nl, mult,
-                                          tol_dir, rf_max, npoints, &chi2[dir], &rf, &e, &mg);
+                                          ext_mult, tol_dir, rf_max, npoints, &chi2[dir], &rf, &e, &mg);
         rf_used[dir] = rf;
         est[dir] = e;
         est[2 + dir] = mg;
@@ -1106,10 +1162,11 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
 
 void rvo_logl_whx_adapt_batch(int W, int np, const double* pl, int has_hk, int has_inc, double hill_factor,
                               const double* t, const double* rvobs, const double* err, int n, double npoints,
-                              double dt, int nl, const int* mult, double tol_dir, int rf_max, double* logl,
-                              int32_t* status, int32_t* rf_used, double* est) {
+                              double dt, int nl, const int* mult, int ext_mult, double tol_dir, int rf_max,
+                              double* logl, int32_t* status, int32_t* rf_used, double* est) {
     for (int w = 0; w < W; w++)
         status[w] = rvo_logl_whx_adapt(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs,
-                                       err, n, npoints, dt, nl, mult, tol_dir, rf_max, logl + w, rf_used + 2 * w,
+                                       err, n, npoints, dt, nl, mult, ext_mult, tol_dir, rf_max, logl + w,
+                                       rf_used + 2 * w,
                                        est + 4 * w);
 }

@@ -61,6 +61,7 @@ struct rvm_plan {
     void* dmem = nullptr;        // one device allocation: schedule + workspace
     void* lvmem = nullptr;       // level-split layout workspace (DevPlan::lv_*), when usable
     size_t lv_bytes = 0;
+    void* xmem = nullptr;        // the extension's stored levels (DevPlan::lvx), when the plan has one
     unsigned long long* slots = nullptr;  // [max_walkers] direction meeting slots (rvm_logl.hip)
     int32_t max_walkers = 0;
     int32_t steps[2] = {0, 0};
@@ -329,6 +330,55 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             // (no workspace: launches keep the LDS-coupled layout)
         }
     }
+    // the extension level (rvm_logl.hip extend_pass): max(mult) + 1 steps per base step, its
+    // Stumpff series as the finest level's, and room for every launch's main-pass levels
+    P.ext_mult = 0;
+    P.ext_nt = 8;
+    P.inv_ext = 1.0;
+    P.lvx = nullptr;
+    P.lvx_emax = 0;
+    P.lvx_stride = 0;
+    for (int k = 0; k <= RVM_MAX_LEVELS; k++) P.lw5[k] = P.lw4x[k] = 0.0;
+    if (P.rmax > 0 && cfg->n_levels >= 2 && cfg->n_levels < RVM_MAX_LEVELS) {
+        const int nl = cfg->n_levels;
+        const size_t emax = std::max<size_t>(std::max(nf, nb), 1);
+        const size_t bx = 2 * emax * (size_t)nl * (size_t)max_walkers * sizeof(double);
+        if (bx <= RVM_EXT_MAX_BYTES) {
+            if (hipMalloc(&plan->xmem, bx) != hipSuccess) {
+                plan->xmem = nullptr;
+                (void)hipGetLastError();
+                rvm_plan_destroy(plan);
+                return fail(-3, "rvm_plan_create: hipMalloc of the extension's stored levels failed");
+            }
+            int m5[RVM_MAX_LEVELS + 1];
+            int fin = 0;
+            for (int k = 0; k < nl; k++) {
+                m5[k] = mult[k];
+                if (mult[k] > mult[fin]) fin = k;
+            }
+            m5[nl] = mult[fin] + 1;
+            auto lagrange = [&](int k0, int n, double* w) {  // weights of levels k0 .. n-1 of m5
+                for (int k = k0; k < n; k++) {
+                    const double xk = 1.0 / ((double)m5[k] * m5[k]);
+                    double wk = 1.0;
+                    for (int j = k0; j < n; j++) {
+                        if (j == k) continue;
+                        const double xj = 1.0 / ((double)m5[j] * m5[j]);
+                        wk *= xj / (xj - xk);
+                    }
+                    w[k] = wk;
+                }
+            };
+            lagrange(0, nl + 1, P.lw5);
+            lagrange(1, nl + 1, P.lw4x);
+            P.ext_mult = m5[nl];
+            P.ext_nt = P.nt[fin];
+            P.inv_ext = 1.0 / m5[nl];
+            P.lvx = reinterpret_cast<double*>(plan->xmem);
+            P.lvx_emax = (int32_t)emax;
+            P.lvx_stride = max_walkers;
+        }
+    }
     *out = plan;
     return 0;
 }
@@ -336,8 +386,15 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
 void rvm_plan_destroy(rvm_plan* plan) {
     if (!plan) return;
     if (plan->lvmem) (void)hipFree(plan->lvmem);
+    if (plan->xmem) (void)hipFree(plan->xmem);
     if (plan->dmem) (void)hipFree(plan->dmem);
     delete plan;
+}
+
+int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult) {
+    if (!plan) return fail(-1, "rvm_plan_extension: null plan");
+    if (ext_mult) *ext_mult = plan->dev.ext_mult;
+    return 0;
 }
 
 int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,

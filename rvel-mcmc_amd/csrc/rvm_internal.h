@@ -14,6 +14,9 @@ constexpr int RVM_LDS_PER_CU = 160 * 1024;
 // adaptive resolution: lane state at t = 0 kept in LDS for the refinement passes, per walker group
 // (rx, ry, vx, vy, rz, vz, r, ir of each of the 64 lanes)
 constexpr int RVM_INIT_DOUBLES = 8 * 64;
+// the extension's acceptance (rvm_logl.hip extend_pass; oracle/rvoracle.c EXT_TOL_FRAC / EXT_GAIN_MAX)
+constexpr double RVM_EXT_TOL_FRAC = 0.25;
+constexpr double RVM_EXT_GAIN_MAX = 0.5;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
@@ -45,9 +48,18 @@ struct DevPlan {
     double lw3[RVM_MAX_LEVELS];
     double rtol_dir;   // +inf: no estimate check
     int32_t rmax;
+    // the extension (stage 1, rvm_logl.hip extend_pass): one more level of ext_mult steps per base
+    // step (0: none) joined to the main pass's levels, which every launch stores in lvx
+    // [2][lvx_emax][n_levels][lvx_stride]; lw5 = weights of all n_levels + 1 levels, lw4x = of the
+    // finer n_levels (lw4x[0] = 0)
+    int32_t ext_mult, ext_nt;
+    double inv_ext;
+    double lw5[RVM_MAX_LEVELS + 1], lw4x[RVM_MAX_LEVELS + 1];
+    double* lvx;
+    int32_t lvx_emax, lvx_stride;
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
-    // [3] walker-directions refined
+    // [3] walker-direction refinement passes (extension + halvings)
     unsigned long long* counters;
     unsigned long long spin_ticks;  // hand-off waits give up after this long without progress (100 MHz)
     double npoints;

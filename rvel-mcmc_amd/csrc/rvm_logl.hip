@@ -300,7 +300,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // their results for the refinement team
     __shared__ unsigned long long s_need[2];
     __shared__ int s_vd[2];
-    __shared__ double s_fchi[2][64];
+    __shared__ double s_fchi[2][64], s_fest[2][64];
     __shared__ int s_fenc[2][64];
     double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
@@ -738,6 +738,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
             const int wo = w0 + lane;
             if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[e] * W + wo] = rvx;
+            if (P.ext_mult > 0 && wo < W) {  // the levels, for a later extension (extend_pass)
+                double* xo = P.lvx + ((size_t)(d * P.lvx_emax + e) * nl) * P.lvx_stride + wo;
+                for (int k = 0; k < nl; k++) xo[(size_t)k * P.lvx_stride] = s_rv[e & 1][k][lane];
+            }
         }
         n1 = n1_next;
         len = len_next;
@@ -892,12 +896,127 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         if (work && pl_idx == 0) s_enc_all[gr][lr_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
         __syncthreads();
     };
+    // ---- adaptive resolution, stage 1: the extension level ----------------------------------
+    // One wave per group / unit -- its combiner wave -- integrates one more level (P.ext_mult steps
+    // per base step) of direction dr from t = 0 and joins it, epoch by epoch, to the main pass's
+    // levels stored in P.lvx: r5 = all nl + 1 levels (lw5), r4x = the finer nl (lw4x).  A marked
+    // walker (combiner lane `lane`, its bit in need_m) is settled -- chi2 from r5 -- when the pair
+    // agrees (sum |(r5-o)^2 - (r4x-o)^2| / s2 <= RVM_EXT_TOL_FRAC rtol_dir npoints) and r5 moved the
+    // answer by at most RVM_EXT_GAIN_MAX of the main pass's estimate est0 (both sums before the
+    // division by npoints); an encounter of the extension ends it ENCOUNTER, a non-finite one
+    // NONFINITE; otherwise the halving passes follow.  One wave, no barrier: each epoch's value
+    // moves from the walker's first lane to its combiner lane by a shuffle, and the stored levels
+    // of the next epoch load while this one integrates.
+    auto extend_pass = [&](const int gr, const int dr, const uint64_t need_m, bool& need, double& chi2w, int& enc,
+                           const double est0) {
+        const DirSched& SR = dr ? P.bwd : P.fwd;
+        const int Er = SR.n_epochs;
+        const double* r_dir = dec ? s_sched + (size_t)dr * 4 * emax2 : l_dir;
+        const double* r_len = r_dir;
+        const double* r_rv = r_dir + Er;
+        const double* r_s2 = r_dir + 2 * Er;
+        const int* r_n = reinterpret_cast<const int*>(r_dir + 3 * Er);
+        const int* r_idx = r_n + Er;
+        {
+            const double* in = l_init + (size_t)gr * RVM_INIT_DOUBLES + lane;
+            s.rx = in[0];
+            s.ry = in[64];
+            s.vx = in[128];
+            s.vy = in[192];
+            s.rz = in[256];
+            s.vz = in[320];
+            s.r = in[384];
+            s.ir = in[448];
+            s.encm = 0;
+        }
+        KickPrep<NP> kq{};
+        if (Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
+        const int mx = P.ext_mult;
+        const int ntx = P.ext_nt;
+        const double ix = P.inv_ext;
+        const int cs = lane & (WPB - 1);  // combiner lane -> walker slot
+        const bool cl = lane < WPB && ((need_m >> lane) & 1);
+        const int wo = w0 + cs;
+        const double* xs = P.lvx + (size_t)dr * P.lvx_emax * nl * P.lvx_stride + (cl ? wo : 0);
+        double a[RVM_MAX_LEVELS];
+#pragma unroll
+        for (int k = 0; k < RVM_MAX_LEVELS; k++) a[k] = cl && k < nl && Er > 0 ? xs[(size_t)k * P.lvx_stride] : 0.0;
+        double c5 = 0.0, e5 = 0.0, dd = 0.0;
+        for (int e = 0; e < Er; e++) {
+            double b[RVM_MAX_LEVELS];
+            const bool nx = cl && e + 1 < Er;
+#pragma unroll
+            for (int k = 0; k < RVM_MAX_LEVELS; k++)
+                b[k] = nx && k < nl ? xs[((size_t)(e + 1) * nl + k) * P.lvx_stride] : 0.0;
+            const int ns = r_n[e] * mx;
+            if (ns > 0) {
+                const double h = r_len[e] * ix;
+                if (ntx <= 6)
+                    segment<6, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                else if (ntx == 7)
+                    segment<7, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                else
+                    segment<8, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+            }
+            const double v = star_vx<NP, L>(s);
+            const double vx = __shfl(v, cs * L);
+            if (cl) {
+                double r = 0.0, r5 = 0.0, r4x = 0.0;
+#pragma unroll
+                for (int k = 0; k < RVM_MAX_LEVELS; k++)
+                    if (k < nl) r += P.lw[k] * a[k];
+#pragma unroll
+                for (int k = 0; k < RVM_MAX_LEVELS; k++)
+                    if (k < nl) r5 += P.lw5[k] * a[k];
+                r5 += P.lw5[nl] * vx;
+#pragma unroll
+                for (int k = 1; k < RVM_MAX_LEVELS; k++)
+                    if (k < nl) r4x += P.lw4x[k] * a[k];
+                r4x += P.lw4x[nl] * vx;
+                const double q = r5 - r_rv[e];
+                c5 += (q * q) / r_s2[e];
+                e5 += fabs((r5 - r4x) * (q + (r4x - r_rv[e]))) / r_s2[e];
+                dd += fabs((r5 - r) * (q + (r - r_rv[e]))) / r_s2[e];
+                if (rv_out != nullptr && wo < W) rv_out[(size_t)r_idx[e] * W + wo] = r5;
+            }
+#pragma unroll
+            for (int k = 0; k < RVM_MAX_LEVELS; k++) a[k] = b[k];
+        }
+        const bool xenc = ((s.encm >> (cs * L)) & kick_enc_bits<NP>()) != 0;
+        if (cl && need) {
+            if (xenc) {
+                enc |= 1;
+                chi2w = c5;
+                need = false;
+            } else if (!isfinite(c5)) {
+                chi2w = c5;  // (NONFINITE at the direction meeting)
+                need = false;
+            } else if (e5 <= RVM_EXT_TOL_FRAC * P.rtol_dir * P.npoints && dd <= RVM_EXT_GAIN_MAX * est0) {
+                chi2w = c5;
+                need = false;
+            }
+        }
+    };
     // Refinement loop over the walker slots still marked in s_need[g] of the active groups (gmask;
-    // set by the caller, one barrier since): the combiner lanes (cmb: level 0's wave, lane < WPB)
-    // update chi2w / enc / need per pass; a walker leaves when its estimate drops to the bound or a
-    // finer pass meets an encounter, and is UNRESOLVED if still above after rmax passes.
+    // set by the caller, one barrier since): first the extension (the combiner waves, lr == 0),
+    // then halving passes; the combiner lanes (cmb: level 0's wave, lane < WPB) update chi2w / enc /
+    // need per pass; a walker leaves when its estimate drops to the bound or a finer pass meets an
+    // encounter, and is UNRESOLVED if still above after rmax passes.  est0: the main pass's estimate.
     auto refine_loop = [&](const int lr, const int gr, const int dr, const int gmask, const int eb, const bool cmb,
-                           bool& need, double& chi2w, int& enc) {
+                           bool& need, double& chi2w, int& enc, const double est0) {
+        if (P.ext_mult > 0) {
+            const uint64_t gneed = s_need[gr];
+            if (lr == 0 && gneed) {
+                if (lane == 0)
+                    __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(gneed),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                extend_pass(gr, dr, gneed, need, chi2w, enc, est0);
+                const uint64_t nb = ballot(need);
+                if (lane == 0) s_need[gr] = nb;
+            }
+            __syncthreads();
+            if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) return;
+        }
         for (int rf = 1; rf <= P.rmax; rf++) {
             const uint64_t gneed = s_need[gr];
             if (lr == 0 && lane == 0 && gneed)
@@ -948,7 +1067,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 }
                 __syncthreads();
                 if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
-                    refine_loop(lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc);
+                    refine_loop(lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc, est);
             }
         }
         if (cmb && wo < W) {
@@ -1081,6 +1200,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 chi2w += (r * r) / l_s2[e];
                 est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
                 if (rv_out != nullptr && valid && pl_idx == 0) rv_out[(size_t)l_idx[e] * W + w] = rvx;
+                if (P.ext_mult > 0 && valid && pl_idx == 0) {  // the levels, for a later extension
+                    double* xo = P.lvx + ((size_t)(d * P.lvx_emax + e) * 4) * P.lvx_stride + w;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) xo[(size_t)k * P.lvx_stride] = v[k];
+                }
                 if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 rr = rr + 1 == RING ? 0 : rr + 1;
             }
@@ -1122,6 +1246,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 if (valid && pl_idx == 0) finish_recompute(w, chi2w, enc);
             } else if (valid && pl_idx == 0) {
                 s_fchi[ul][slot] = chi2w;
+                s_fest[ul][slot] = est;
                 s_fenc[ul][slot] = enc | (need ? 16 : 0);
             }
             if (lane == 0) __hip_atomic_store(s_vd + ul, refine ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1151,11 +1276,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         d = gr;  // (the finishing lanes meet the other direction as unit gr: finish() reads d)
         const bool cmb = lr == 0 && lane < WPB;
         const bool mine = (gr == 0 ? v0 : v1) == 2;
-        double chi2w = 0.0;
+        double chi2w = 0.0, est0 = 0.0;
         int enc = 0;
         bool need = false;
         if (cmb && mine) {
             chi2w = s_fchi[gr][lane];
+            est0 = s_fest[gr][lane];
             const int f = s_fenc[gr][lane];
             enc = f & 15;
             need = (f & 16) != 0 && w0 + lane < W;
@@ -1165,7 +1291,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (lane == 0) s_need[gr] = nb;
         }
         __syncthreads();
-        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc);
+        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, est0);
         if (cmb && mine && w0 + lane < W) finish_recompute(w0 + lane, chi2w, enc);
         return;
     }

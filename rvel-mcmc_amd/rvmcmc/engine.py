@@ -163,6 +163,9 @@ class LoglPlan:
                                           sigma.ctypes.data_as(dp), self.n_obs, self.max_walkers, C.byref(handle))
         _lib.check(rc, "rvm_plan_create")
         self._h = handle
+        ext = C.c_int32()
+        _lib.check(self.lib.rvm_plan_extension(self._h, C.byref(ext)), "rvm_plan_extension")
+        self.ext_mult = ext.value  # the adaptive resolution's extension level (0: none)
 
     def faults(self, reset=False, stream=None) -> dict:
         """rvm_plan_faults: the plan's counters (synchronises the stream): hand-off timeouts, NONFINITE

@@ -34,8 +34,11 @@ ST_OK, ST_PRIOR, ST_ENC = 0, 1, 2
 
 
 def n_threads():
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
-    return max(1, min(n, os.cpu_count() or 1))
+    """The CPUs this process may run on (the GPU box's share; os.cpu_count() is the whole machine)."""
+    try:
+        return max(1, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        return max(1, os.cpu_count() or 1)
 
 
 def ias15_logl(P, n_planets, obs, hill=1.0, has_inc=0):

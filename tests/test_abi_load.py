@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 9
+    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 10
 
 
 def test_python_binding_matches_header():
@@ -73,6 +73,7 @@ def test_argument_errors_do_not_touch_the_device():
     assert rc < 0 and b"resolve_max" in lib.rvm_last_error()
     assert lib.rvm_plan_faults(None, 0, None, None, None, None, 0) < 0
     assert lib.rvm_plan_set_handoff_timeout(None, 1.0) < 0
+    assert lib.rvm_plan_extension(None, None) < 0
     # workspace: per (chain, pair i >= j) and direction, 4 f64 partial sums and an int32 status
     assert lib.rvm_logl_derivs_workspace_bytes(256, 10) == 256 * 55 * 2 * (4 * 8 + 4)
 

@@ -17,7 +17,7 @@ import pytest
 import ias15_parity as IP
 import oracle as O
 from conftest import S2_PLANETS, S2_SCALES
-from test_gpu_logl import LEVELS, _assert_t1, oracle_sensitivity
+from test_gpu_resolve import assert_t1_adaptive
 
 pytestmark = pytest.mark.gpu
 
@@ -62,13 +62,15 @@ def test_config5_shard_8192_walkers():
 
     idx = np.r_[0:32, 2048:2080, 4096:4128, W - 32:W]
     P = IP.to_oracle(pm, X[idx])
-    dt = ens.plan.dt
-    ref, st_ref = O.logl_whx_batch(P, 3, obs, dt, LEVELS)
-    _assert_t1(lnp[idx], st_all.cpu().numpy()[idx], ref, st_ref, sens=oracle_sensitivity(P, 3, obs, dt, LEVELS))
+    plan = ens.plan  # (the default IntegratorConfig: adaptive resolution on)
+    assert plan.resolve_tol > 0 and plan.ext_mult == O.ext_multiplier(plan.mult, plan.resolve_max)
+    rf, _ = assert_t1_adaptive(lnp[idx], st_all.cpu().numpy()[idx], P, 3, obs, plan.dt, plan.mult, plan.resolve_tol,
+                               plan.resolve_max)
     ias, st_ias = IP.ias15_logl(P, 3, obs, ens.hill_factor)
     assert (st_ias == 0).all()
     d2 = np.abs(lnp[idx] - ias)
     print(json.dumps({"test": "config5 shard", "walkers": W, "iterations": 4, "acceptance": float(acc.mean() / 4),
                       "speculative": bool(ens.speculating()), "t2_max_abs_dlogl": float(d2.max()),
-                      "t2_subset": int(len(idx))}))
+                      "t2_subset": int(len(idx)),
+                      "subset_directions_extended": int((rf == 1).sum()), "subset_directions_halved": int((rf >= 2).sum())}))
     assert d2.max() <= T2_ABS

@@ -154,6 +154,18 @@ def test_stretch_vs_ias15_wide_ball_encounters():
     assert rep["exempt_ias15_roundoff_sensitive"] <= rep["decisions"] // 100
 
 
+def test_stretch_vs_ias15_config2():
+    """BASELINE config 2's own shape: 1024 walkers of the 2-planet synthetic config (512 per half,
+    one speculative launch of 1536 walker slots per iteration), every proposal of two iterations."""
+    tally, info = stretch_parity("stretch/config2 S2 1024 walkers", S2_PLANETS, s2_obs_oracle(), 1024, 1e-3)
+    rep = tally.report(**info)
+    assert info["speculative"]
+    assert rep["decisions"] == 2 * 1024
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["exempt_status_disagreement"] == 0
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
+
+
 def test_stretch_vs_ias15_hd155358():
     planets, obs = _hd()
     tally, info = stretch_parity("stretch/HD155358 512 walkers", planets, obs, 512, 1e-3)
@@ -229,19 +241,20 @@ def test_mh_vs_ias15(case):
     assert 0 < rep["accepted_ias15"] < rep["decisions"]
 
 
-def test_smala_step_vs_ias15():
+def smala_parity(name, hessian, C_, eps=0.5, alpha=1e3, warm=2):
     """One batched SMALA step (mcmc.py:167-187) with injected z, u: the accept ratio's likelihood
     terms from IAS15, its proposal-density terms from the device metric (exact derivatives, pinned
-    against IAS15 differences in test_gpu_derivs.py)."""
+    against IAS15 differences in test_gpu_derivs.py, or config 4's Gauss-Newton metric from the
+    FD stencil's per-epoch RVs)."""
     torch = _torch()
     from rvmcmc.smala import SmalaChains
     from rvmcmc.state import State
 
     s = State(planets=[dict(p) for p in S2_PLANETS])
     obs = s2_obs_oracle()
-    C_, dim, eps = 128, s.Nvars, 0.5
-    sm = SmalaChains(s, obs, eps=eps, alpha=1e3, n_chains=C_, seed=5, hessian="exact")
-    for _ in range(2):
+    dim = s.Nvars
+    sm = SmalaChains(s, obs, eps=eps, alpha=alpha, n_chains=C_, seed=5, hessian=hessian)
+    for _ in range(warm):
         sm.step()
     pm, hill = sm.pmap, sm.state.hillRadiusFactor
     rng = np.random.default_rng(6)
@@ -259,7 +272,7 @@ def test_smala_step_vs_ias15():
     ls_ref, ss_ref = IP.ias15_logl(IP.to_oracle(pm, xs.T), pm.n_planets, obs, hill)
     _, ss_dev, _ = sm.state.get_logp_batch(obs, torch.as_tensor(xs, device="cuda"), hill_factor=hill, pmap=pm)
     ss_dev = ss_dev.cpu().numpy()
-    ls_dev = p["lp"]  # the proposal's logp as the device step used it (exact-derivative launch)
+    ls_dev = p["lp"]  # the proposal's logp as the device step used it
 
     def logq(y, mu, G, logdet):
         d = y - mu
@@ -276,11 +289,30 @@ def test_smala_step_vs_ias15():
               - logq(xs[:, i], c0["mu"][:, i], G0, c0["logdet"][i]))
         acc_ref[i] = np.exp(lr) > u[i]
         margin[i] = abs(lr - np.log(u[i]))
-    tally = IP.Tally("smala/S2 128 chains exact metric")
+    tally = IP.Tally(name)
     tally.add(acc_dev, acc_ref, margin, ss_dev, ss_ref, ls_dev, ls_ref)
-    rep = tally.report(chains=C_, eps=eps, alpha=1e3)
+    return tally.report(chains=C_, eps=eps, alpha=alpha, hessian=hessian), tally
+
+
+def test_smala_step_vs_ias15():
+    """Exact-metric SMALA (the reference's Hessian, state.py:253-294), 128 chains."""
+    rep, tally = smala_parity("smala/S2 128 chains exact metric", "exact", 128)
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
-    # eps = 0.5 in the metric's units reaches several posterior widths: a few proposals leave the
-    # T2 regime (measured: 1 of 128 at 2.7e-6); they are counted, and their decisions still agree
-    assert rep["ok_proposals_dlogl_above_margin"] <= C_ // 20
+    # eps = 0.5 in the metric's units reaches several posterior widths: the exact-derivative launch
+    # (rvm_logl_derivs) has no adaptive resolution, so a few proposals may leave the T2 regime
+    # (measured round 2: 1 of 128 at 2.7e-6); they are counted, and their decisions still agree
+    assert rep["ok_proposals_dlogl_above_margin"] <= 128 // 20
     assert 0 < rep["accepted_ias15"]
+
+
+def test_smala_fd_step_vs_ias15():
+    """Config 4's own SMALA path (BASELINE.json configs[3]): 256 chains, the FD stencil formed in
+    one likelihood launch (23 integrations per chain and step), Gauss-Newton + SoftAbs metric derived
+    on the device (mcmc.py:144-187 with the FD/GN metric).  Likelihood terms of the accept ratio from
+    IAS15, proposal-density terms from the device metric; the stencil's centre logL is the adaptive
+    kernel's (T2 holds)."""
+    rep, tally = smala_parity("smala/S2 256 chains FD Gauss-Newton (config 4)", "gauss-newton", 256)
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["exempt_status_disagreement"] == 0
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
+    assert 0 < rep["accepted_ias15"] < rep["decisions"]

@@ -3,7 +3,8 @@
 The reference integrates every proposal with adaptive IAS15 (state.py:36-73), so its accuracy does
 not depend on where a walker is; a plan's Wisdom-Holman step is fixed from the sampler's initial
 state.  With rvm_config.resolve_tol a direction whose extrapolation-error estimate (the chi2
-change when the coarsest Richardson level is dropped) exceeds resolve_tol / 2 is integrated again
+change when the coarsest Richardson level is dropped) exceeds resolve_tol / 2 first gets the
+extension level joined to its stored levels, and if that does not settle it is integrated again
 with every step halved, up to resolve_max times.  Checked here:
 
   * T1 of the adaptive kernel against the oracle's restatement of the same rule
@@ -88,38 +89,30 @@ def _adapt_oracle(P, obs, dt, mult, tol=TOL, rmax=RMAX):
     return _par(lambda p: O.logl_whx_adapt_batch(p, 2, obs, dt, mult, tol, rmax), P)
 
 
-@pytest.mark.parametrize("W", [512, 6144])  # LDS-coupled layout / level-split layout (bench shape)
-def test_t1_adaptive_wide_ball(W):
-    obs = s2_obs_oracle()
-    plan, dt, mult = _plan(obs, W)
-    X = wide_walkers(W)
-    got, st = _run(plan, X)
-    f = plan.faults(reset=True)
-    P = _oracle_P(X)
-    ref, st_ref, rf, est, margin = _adapt_oracle(P, obs, dt, mult)
-    # chaotic walkers (close approaches) and refinement decisions at roundoff distance from the
-    # bound may legitimately go the other way in a second implementation: the oracle's own
-    # response to 1e-15 relative input nudges (of logL, of the status, of the refinements taken and
-    # of the final estimate -- a difference of two extrapolations, which near a close approach moves
-    # by up to tens of percent under such a nudge), and its closest approach to the bound
+def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX, has_inc=0):
+    """T1 of an adaptive-resolution launch against the oracle's restatement of the same rule
+    (oracle.logl_whx_adapt_batch): statuses and logL, up to sensitivity.  Chaotic walkers (close
+    approaches) and decisions at roundoff distance from their bound may legitimately go the other
+    way in a second implementation: the oracle's own response to 1e-15 relative input nudges (of
+    logL, of the status, of the stage reached and of the final estimate -- a difference of two
+    extrapolations, which near a close approach moves by up to tens of percent under such a nudge),
+    and its closest approach to any decision's bound.  Returns (stages [W][2], sensitive [W])."""
+    W = len(got)
+    fn = lambda p: O.logl_whx_adapt_batch(p, n_planets, obs, dt, mult, tol, rmax, has_inc=has_inc)
+    ref, st_ref, rf, est, margin = _par(fn, P)
     sens = np.zeros(W)
     flips = np.zeros(W, dtype=bool)
-    for pl, par, sgn in [(0, 4, 1), (1, 4, -1), (0, 1, 1)]:
+    for pl, par, sgn in [(0, 4, 1), (-1, 4, -1), (0, 1, 1)]:
         P2 = P.copy()
         P2[:, pl, par] *= 1 + sgn * 1e-15
-        r2, s2, rf2, est2, _ = _adapt_oracle(P2, obs, dt, mult)
+        r2, s2, rf2, est2, _ = _par(fn, P2)
         flips |= (s2 != st_ref) | np.any(rf2 != rf, axis=1)
         with np.errstate(invalid="ignore"):  # (an estimate whose roundoff response is not small
             # against its distance from the bound)
-            flips |= np.any(np.abs(est2 - est) > 0.02 * np.abs(est - 0.5 * TOL), axis=1)
+            flips |= np.any(np.abs(est2 - est) > 0.02 * np.abs(est - 0.5 * tol), axis=1)
         both = (st_ref == 0) & (s2 == 0)
         sens[both] = np.maximum(sens[both], np.abs(r2[both] - ref[both]) / np.maximum(1.0, np.abs(ref[both])))
     sensitive = flips | (sens > 1e-9) | (margin.min(axis=1) < 1e-6)
-    refined = int(rf.sum())
-    print(f"W={W}: oracle refined walker-directions {refined} (passes {int((2 ** rf - 1).sum())}), kernel "
-          f"counters {f}, statuses {np.bincount(st, minlength=5).tolist()}, sensitive {int(sensitive.sum())}")
-    assert refined > W // 10, "the wide ball must exercise the refinement passes"
-    assert f["refined"] > 0 and f["handoff_timeouts"] == 0
     mism = st != st_ref
     assert np.all(~mism | sensitive), np.nonzero(mism & ~sensitive)
     assert mism.sum() <= max(2, W // 100)
@@ -131,6 +124,22 @@ def test_t1_adaptive_wide_ball(W):
     assert np.mean(err <= T1_REL) > 0.9
     # walkers the oracle leaves UNRESOLVED are UNRESOLVED on the device too (up to sensitivity)
     assert np.all(((st == 4) == (st_ref == 4)) | sensitive)
+    return rf, sensitive
+
+
+@pytest.mark.parametrize("W", [512, 6144])  # LDS-coupled layout / level-split layout (bench shape)
+def test_t1_adaptive_wide_ball(W):
+    obs = s2_obs_oracle()
+    plan, dt, mult = _plan(obs, W)
+    assert plan.ext_mult == O.ext_multiplier(mult, RMAX) == max(mult) + 1
+    X = wide_walkers(W)
+    got, st = _run(plan, X)
+    f = plan.faults(reset=True)
+    rf, sensitive = assert_t1_adaptive(got, st, _oracle_P(X), 2, obs, dt, mult)
+    print(f"W={W}: oracle walker-directions at the extension {int((rf == 1).sum())}, halved {int((rf >= 2).sum())}; "
+          f"kernel counters {f}, statuses {np.bincount(st, minlength=5).tolist()}, sensitive {int(sensitive.sum())}")
+    assert (rf == 1).sum() > W // 20 and (rf >= 2).sum() > W // 20, "the wide ball must exercise both stages"
+    assert f["refined"] > 0 and f["handoff_timeouts"] == 0
     assert f["unresolved"] == int((st == 4).sum())
 
 

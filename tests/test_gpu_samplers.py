@@ -188,7 +188,7 @@ def test_fused_half_step_matches_three_launch_path(case):
 
 
 @pytest.mark.parametrize("case", ["s2", "s2_fixed_params", "s2_wide", "one_planet", "three_planets", "inclined",
-                                  "s2_large", "s2_bench_shape", "s2_bench_shape_wide"])
+                                  "s2_large", "s2_config2", "s2_bench_shape", "s2_bench_shape_wide"])
 def test_speculative_iteration_matches_half_steps(case):
     """rvm_stretch_iteration_begin / _end (both half-steps from one launch of 3 n walker slots,
     half 1 evaluated against both possible positions of its partner) against two fused half-step
@@ -215,6 +215,8 @@ def test_speculative_iteration_matches_half_steps(case):
         planets[1].update(ix=0.01, iy=0.03)
     elif case == "s2_large":
         W, iters = 2 * 8256, 2
+    elif case == "s2_config2":  # BASELINE config 2: 1024 walkers, 2-planet S2 (512 per half, 1536 slots)
+        W, iters = 1024, 4
     elif case == "s2_bench_shape":  # bench.py's shape: the 6144-slot launch runs the level-split layout
         W, iters = 4096, 3
     elif case == "s2_bench_shape_wide":  # the same under uneven load: redone segments, prior / encounter exits

@@ -68,7 +68,8 @@ def test_adaptive_resolution_keeps_t2_on_a_wide_ball():
     """The kernel algorithm with adaptive resolution (oracle restatement, rvm_config.resolve_tol =
     5e-7, resolve_max = 4) against IAS15 on walkers of a 0.6x ball and stretch proposals between
     them -- far from the plan's period basis: every OK/OK proposal within the SURVEY §8c T2 bound
-    (1e-6) unless IAS15 itself is roundoff-sensitive there.  Without the rule the same walkers miss
+    (1e-6) unless IAS15 itself is roundoff-sensitive there, whether the extension level settled a
+    direction or halving passes followed.  Without the rule the same walkers miss
     T2 by up to 1e2 (profiles/r02_parity_ias15.jsonl:2)."""
     from rvmcmc import engine
 
@@ -89,6 +90,6 @@ def test_adaptive_resolution_keeps_t2_on_a_wide_ball():
     sens = IP.ias15_roundoff(P[ok], 2, obs, li[ok])
     d_adapt = np.abs(la[ok] - li[ok])[sens <= IP.ROUNDOFF_REL]
     ok0 = (s0 == 0) & (si == 0)
-    assert rf.sum() > 10 and ok.sum() > 40
+    assert (rf == 1).sum() > 5 and (rf >= 2).sum() > 5 and ok.sum() > 40  # (both stages: extension, halving)
     assert d_adapt.max() <= IP.MARGIN, d_adapt.max()
     assert np.abs(l0[ok0] - li[ok0]).max() > 1e-3  # (the fixed-step algorithm alone misses T2 here)
