@@ -122,11 +122,14 @@ int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult);
  *   nonfinite         walkers finished with RVM_STATUS_NONFINITE (any launch on the plan)
  *   unresolved        walkers finished with RVM_STATUS_UNRESOLVED
  *   refined           walker-direction passes of the adaptive resolution (extension + halvings)
+ *   truncated         refinements cut short because the proposal's accept test fails whatever
+ *                     further passes give (fused sampler launches): such a proposal
+ *                     is rejected and keeps the last pass's logL
  * reset != 0: zero the counters and restore the hand-off workspace, after the stream's earlier work.
  * The samplers (rvmcmc) check this and raise on timeouts / non-finite results (mcmc.py:28-35: emcee
  * refuses NaN log-probabilities) rather than treating them as ordinary rejections. */
 int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
-                    int64_t* unresolved, int64_t* refined, void* stream);
+                    int64_t* unresolved, int64_t* refined, int64_t* truncated, void* stream);
 /* Level-split hand-off waits give up after `seconds` without progress (default 2 s; > 0). */
 int rvm_plan_set_handoff_timeout(rvm_plan* plan, double seconds);
 
@@ -194,15 +197,17 @@ int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_
  *   [n_half][n_params] as at the start of the iteration, global order (on one rank: the walker-major
  *   mirrors); they must not be written before end has run.  s0_begin / s1_begin: global index of
  *   this rank's first walker of half 0 (its index within the half) and of half 1 (n_half + its
- *   index within half 1): the Philox keys.
+ *   index within half 1): the Philox keys.  lnp1 (nullable): half 1's log-probabilities [n_loc] as at the start of
+ *   the iteration -- its accept inputs, which lets the adaptive resolution cut a refinement short
+ *   on a certain reject (rvm_plan_faults `truncated`); NULL refines half 1's slots fully.
  * end: half 1's accepts with the variant dec_all[j] selects (dec_all: half 0's decisions in
  *   global order, [n_half]; on one rank dec itself); x1, lnp1 in place, x1_aos / x0_aos (nullable)
  *   mirrors updated; lnp_new_out / status_new_out (nullable): the chosen proposals' logl, status. */
 int rvm_stretch_iteration_begin(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_loc,
                                 int64_t s0_begin, int64_t s1_begin, double* x0, double* lnp0, const double* x1,
-                                int32_t n_half, const double* c0, const double* c1, double a, uint64_t seed,
-                                uint64_t iteration, double hill_factor, double* lnp_spec, int32_t* status_spec,
-                                int32_t* dec, int32_t* accepted0, void* stream);
+                                const double* lnp1, int32_t n_half, const double* c0, const double* c1, double a,
+                                uint64_t seed, uint64_t iteration, double hill_factor, double* lnp_spec,
+                                int32_t* status_spec, int32_t* dec, int32_t* accepted0, void* stream);
 int rvm_stretch_iteration_end(int32_t n_params, int32_t n_loc, int64_t s0_begin, int64_t s1_begin, const double* x0,
                               double* x0_aos, const int32_t* dec, const int32_t* dec_all, double* x1, double* x1_aos,
                               double* lnp1, int32_t n_half, const double* c0, const double* c1,

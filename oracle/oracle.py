@@ -39,7 +39,7 @@ def build(force: bool = False) -> str:
 def lib():
     global _LIB
     if _LIB is None:
-        so = os.path.join(_HERE, "liboracle.so")
+        so = os.environ.get("RVO_LIB") or os.path.join(_HERE, "liboracle.so")  # (RVO_LIB: a study build)
         if not os.path.exists(so):
             build()
         L = C.CDLL(so)
@@ -73,7 +73,9 @@ def lib():
                                              C.POINTER(C.c_int32)]
         L.rvo_logl_whx_adapt_batch.argtypes = [C.c_int, C.c_int, dp, C.c_int, C.c_int, C.c_double, dp, dp, dp,
                                                C.c_int, C.c_double, C.c_double, C.c_int, ip, C.c_int, C.c_double, C.c_int,
-                                               dp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dp]
+                                               C.POINTER(C.c_int32), C.c_int, dp, dp, dp,
+                                               dp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dp,
+                                               C.POINTER(C.c_int32)]
         _LIB = L
     return _LIB
 
@@ -248,7 +250,8 @@ def ext_multiplier(mult, rf_max):
     return max(m) + 1 if rf_max > 0 and 2 <= len(m) < 6 else 0
 
 
-def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.0, has_hk=1, has_inc=0, ext=None):
+def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.0, has_hk=1, has_inc=0, ext=None,
+                         ctx=None):
     """The kernel's algorithm with adaptive resolution (rvm_config.resolve_tol / resolve_max):
     a direction whose extrapolation-error estimate exceeds tol / 2 gets the extension level (ext
     steps per base step; default ext_multiplier) and, if that does not settle it, passes with every
@@ -256,7 +259,9 @@ def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.
     params [W][np][7] -> (logl[W], status[W], stages [W][2] (0 the plan's step, 1 the extension,
     1 + r r halvings; without the extension r), estimates [W][2], margins [W][2]); margin = the
     closest any decision came to its bound, min |x/bound - 1| (a decision at roundoff distance may
-    go the other way in a second implementation).  tol = 0 is the plain rvo_whx algorithm."""
+    go the other way in a second implementation).  tol = 0 is the plain rvo_whx algorithm.
+    ctx = dict(mode [W] (0 none, 1 emcee stretch, 2 MH), dim, z [W], u [W], lnp0 [W]): the sampler's
+    accept inputs of each walker, for the certain-reject cut; then a sixth result, cut [W][2]."""
     pl = _f64(params)
     W = pl.shape[0]
     t = _f64(np.concatenate([obs.tf, obs.tb]))
@@ -265,14 +270,24 @@ def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.
     out = np.zeros(W)
     st = np.zeros(W, dtype=np.int32)
     rf = np.zeros((W, 2), dtype=np.int32)
+    cut = np.zeros((W, 2), dtype=np.int32)
     est = np.zeros((W, 4))
     m, mp = _mult(mult)
     tol_dir = 0.5 * float(tol) if tol > 0 else np.inf
     ext = ext_multiplier(mult, rf_max) if ext is None else int(ext)
+    ip32 = C.POINTER(C.c_int32)
+    if ctx is not None:
+        mode = np.ascontiguousarray(np.asarray(ctx["mode"], dtype=np.int32))
+        dz, du, dl = (_f64(np.broadcast_to(np.asarray(ctx[k], dtype=np.float64), (W,))) for k in ("z", "u", "lnp0"))
+        cargs = (mode.ctypes.data_as(ip32), int(ctx["dim"]), _p(dz), _p(du), _p(dl))
+    else:
+        cargs = (None, 0, None, None, None)
     lib().rvo_logl_whx_adapt_batch(W, np_, _p(pl), has_hk, has_inc, float(hill_factor), _p(t), _p(rv), _p(er),
                                    len(t), float(obs.Npoints), float(dt), len(m), mp, ext, tol_dir, int(rf_max),
-                                   _p(out), st.ctypes.data_as(C.POINTER(C.c_int32)),
-                                   rf.ctypes.data_as(C.POINTER(C.c_int32)), _p(est))
+                                   *cargs, _p(out), st.ctypes.data_as(ip32), rf.ctypes.data_as(ip32), _p(est),
+                                   cut.ctypes.data_as(ip32))
+    if ctx is not None:
+        return out, st, rf, est[:, :2], est[:, 2:], cut
     return out, st, rf, est[:, :2], est[:, 2:]
 
 

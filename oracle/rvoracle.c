@@ -998,29 +998,47 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /* r = all levels' Richardson RV, r3 = the finer nl - 1 levels' (their own Lagrange weights).   */
 /* Above the bound (est > tol_dir):                                                             */
 /*  stage 1, the extension (ext_mult > 0): one more level, ext_mult steps per base step, joins  */
-/*   the stored levels: r5 = Richardson over all nl + 1 levels, r4x = over the finer nl levels   */
-/*   (the coarsest dropped).  Accepted (chi2 from r5) when both                                 */
-/*     sum |(r5 - o)^2 - (r4x - o)^2| / s2 <= EXT_TOL_FRAC * tol_dir * npoints   (converged)    */
-/*     sum |(r5 - o)^2 - (r - o)^2| / s2   <= EXT_GAIN_MAX * (est * npoints)     (consistent:   */
-/*   the extension moved the answer by at most half the first estimate);                        */
+/*   the stored levels: r5 = Richardson over all nl + 1 levels.  Accepted (chi2 from r5) when    */
+/*     sum |(r5 - o)^2 - (r - o)^2| / s2 <= EXT_ACCEPT * tol_dir * npoints                        */
+/*   -- the change of chi2 the extension brought, an estimate of the main pass's own error (and  */
+/*   a conservative one of r5's: measured, r5's error stays below 0.5 tol_dir wherever this      */
+/*   holds);                                                                        */
 /*  stages 2..: every step halved (level k: mult 2^rf steps per base step, rf = 1..rf_max) while  */
 /*   est > tol_dir; still above after rf_max: RVO_UNRESOLVED.                                   */
+/* Certain rejects (a sampler's accept inputs given: dmode 1 emcee stretch, 2 MH): after a       */
+/* halving pass whose estimate is still above the bound, the direction stops (status OK, this    */
+/* pass's chi2) when the accept test fails even at lp_hi = -(chi2 - d2) / npoints, d2 = the     */
+/* pass's change of chi2 from the previous pass (the main pass for rf = 1),                      */
+/*   d2 = sum |(r - o)^2 - (r_prev - o)^2| / s2.                                                */
 /* An encounter or non-finite RV ends the direction at once (no refinement).                    */
 /* ------------------------------------------------------------------------------------------ */
 enum { RVO_UNRESOLVED = 4 };
-#define EXT_TOL_FRAC 0.25
-#define EXT_GAIN_MAX 0.5
+#ifndef EXT_ACCEPT /* (overridable for studies of the rule: -DEXT_ACCEPT=...) */
+#define EXT_ACCEPT 2.0
+#endif
 
 
 static double margin_of(double x, double bound) {
     return bound > 0.0 ? fabs(x / bound - 1.0) : INFINITY;
 }
 
+typedef struct {
+    int mode; /* 0 none, 1 emcee stretch, 2 MH */
+    int dim;
+    double z, u, lnp0;
+} rvo_decide;
+
+/* the sampler's accept test at lp (rvm_stretch.h stretch_accepts / mh_accepts) */
+static int decide_accepts(const rvo_decide* dc, double lp) {
+    if (dc->mode == 1) return (double)(dc->dim - 1) * log(dc->z) + lp - dc->lnp0 > log(dc->u);
+    return exp(lp - dc->lnp0) > dc->u;
+}
+
 static int whx_direction_adapt(int np, const double* pl, double hill_factor, const double* at, const double* ob,
                                const double* s2, int cnt, double sign, double dt, int nl, const int* mult, int ext_mult,
-                               double tol_dir, int rf_max, double npoints, double* chi2_out, int* stage_out,
-                               double* est_out, double* margin_out) {
-    double w[8], w3[8], w5[9], w4x[9];
+                               double tol_dir, int rf_max, double npoints, const rvo_decide* dc, double* chi2_out,
+                               int* stage_out, double* est_out, double* margin_out, int* cut_out) {
+    double w[8], w3[8], w5[9];
     rvo_richardson_weights_seq(nl, mult, w);
     w3[0] = 0.0;
     if (nl >= 2) rvo_richardson_weights_seq(nl - 1, mult + 1, w3 + 1);
@@ -1030,12 +1048,12 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
         for (int k = 0; k < nl; k++) m5[k] = mult[k];
         m5[nl] = ext_mult;
         rvo_richardson_weights_seq(nl + 1, m5, w5);
-        w4x[0] = 0.0;
-        rvo_richardson_weights_seq(nl, m5 + 1, w4x + 1);
     }
     double* lv = (double*)malloc(sizeof(double) * (size_t)(9 * cnt + 1));
     double* lv0 = (double*)malloc(sizeof(double) * (size_t)(8 * cnt + 1)); /* the main pass's levels */
+    double* prev = (double*)malloc(sizeof(double) * (size_t)(cnt + 1));   /* the last pass's RV */
     int st = RVO_OK, stage = 0;
+    *cut_out = 0;
     double chi2 = 0.0, est = 0.0, margin = INFINITY;
     for (int rf = 0; rf <= rf_max; rf++) {
         st = RVO_OK;
@@ -1046,17 +1064,31 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
         if (st != RVO_OK) break;
         chi2 = 0.0;
         est = 0.0;
+        double d2 = 0.0;
         for (int i = 0; i < cnt; i++) {
             double r = 0.0, r3 = 0.0;
             for (int k = 0; k < nl; k++) r += w[k] * lv[(size_t)k * cnt + i];
             for (int k = 1; k < nl; k++) r3 += w3[k] * lv[(size_t)k * cnt + i];
             chi2 += (r - ob[i]) * (r - ob[i]) / s2[i];
             est += fabs((r - r3) * ((r - ob[i]) + (r3 - ob[i]))) / s2[i];
+            if (rf > 0) d2 += fabs((r - prev[i]) * ((r - ob[i]) + (prev[i] - ob[i]))) / s2[i];
+            prev[i] = r;
         }
-        const double est_raw = est;
         est /= npoints;
         if (nl >= 2 && tol_dir < INFINITY && margin_of(est, tol_dir) < margin) margin = margin_of(est, tol_dir);
         if (nl < 2 || !(est > tol_dir)) break;
+        if (rf > 0 && ext_mult > 0 && dc != NULL && dc->mode != 0) {
+            const double lp_hi = -(chi2 - d2) / npoints;
+            const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0
+                                                 : lp_hi - dc->lnp0;
+            const double lu = log(dc->u);
+            const double mg = fabs(lnpdiff - lu) / (1.0 + fabs(lu));
+            if (mg < margin) margin = mg;
+            if (!decide_accepts(dc, lp_hi)) { /* a certain reject: keep this pass */
+                *cut_out = 1;
+                break;
+            }
+        }
         if (rf == 0 && ext) {
             /* stage 1: the extension level over the main pass's stored levels */
             stage = 1;
@@ -1064,25 +1096,21 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
             double* lx = lv + (size_t)nl * cnt;
             st = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, ext_mult, lx);
             if (st != RVO_OK) break;
-            double c5 = 0.0, e5 = 0.0, dd = 0.0;
+            double c5 = 0.0, dd = 0.0;
             for (int i = 0; i < cnt; i++) {
-                double r = 0.0, r5 = 0.0, r4x = 0.0;
+                double r = 0.0, r5 = 0.0;
                 for (int k = 0; k < nl; k++) r += w[k] * lv0[(size_t)k * cnt + i];
                 for (int k = 0; k < nl; k++) r5 += w5[k] * lv0[(size_t)k * cnt + i];
                 r5 += w5[nl] * lx[i];
-                for (int k = 1; k < nl; k++) r4x += w4x[k] * lv0[(size_t)k * cnt + i];
-                r4x += w4x[nl] * lx[i];
                 const double q = r5 - ob[i];
                 c5 += (q * q) / s2[i];
-                e5 += fabs((r5 - r4x) * (q + (r4x - ob[i]))) / s2[i];
                 dd += fabs((r5 - r) * (q + (r - ob[i]))) / s2[i];
             }
-            const double b5 = EXT_TOL_FRAC * tol_dir * npoints, bg = EXT_GAIN_MAX * est_raw;
-            if (margin_of(e5, b5) < margin) margin = margin_of(e5, b5);
-            if (margin_of(dd, bg) < margin) margin = margin_of(dd, bg);
-            if (e5 <= b5 && dd <= bg) {
+            const double bx = EXT_ACCEPT * tol_dir * npoints;
+            if (margin_of(dd, bx) < margin) margin = margin_of(dd, bx);
+            if (dd <= bx) {
                 chi2 = c5;
-                est = e5 / npoints;
+                est = dd / npoints;
                 break;
             }
         }
@@ -1094,6 +1122,7 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
     }
     free(lv);
     free(lv0);
+    free(prev);
     *chi2_out = chi2;
     *stage_out = stage;
     *est_out = est;
@@ -1109,9 +1138,10 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
  * a second implementation may take the other way when that is at roundoff level. */
 int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
                        const double* rvobs, const double* err, int n, double npoints, double dt, int nl,
-                       const int* mult, int ext_mult, double tol_dir, int rf_max, double* logl, int32_t* rf_used,
-                       double* est) {
+                       const int* mult, int ext_mult, double tol_dir, int rf_max, const rvo_decide* dc,
+                       double* logl, int32_t* rf_used, double* est, int32_t* cut) {
     rf_used[0] = rf_used[1] = 0;
+    cut[0] = cut[1] = 0;
     est[0] = est[1] = 0.0;
     est[2] = est[3] = INFINITY;
     if (rvo_prior_hard(np, pl, has_hk, has_inc)) {
@@ -1142,11 +1172,12 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
             ob[a] = rvobs[idx[a]];
             s2[a] = err[idx[a]] * err[idx[a]];
         }
-        int rf = 0;
+        int rf = 0, ct = 0;
         double e = 0.0, mg = INFINITY;
         if (cnt)
             sd[dir] = whx_direction_adapt(np, pl, hill_factor, at, ob, s2, cnt, dir == 0 ? 1.0 : -1.0, dt, nl, mult,
-                                          ext_mult, tol_dir, rf_max, npoints, &chi2[dir], &rf, &e, &mg);
+                                          ext_mult, tol_dir, rf_max, npoints, dc, &chi2[dir], &rf, &e, &mg, &ct);
+        cut[dir] = ct;
         rf_used[dir] = rf;
         est[dir] = e;
         est[2 + dir] = mg;
@@ -1163,10 +1194,12 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
 void rvo_logl_whx_adapt_batch(int W, int np, const double* pl, int has_hk, int has_inc, double hill_factor,
                               const double* t, const double* rvobs, const double* err, int n, double npoints,
                               double dt, int nl, const int* mult, int ext_mult, double tol_dir, int rf_max,
-                              double* logl, int32_t* status, int32_t* rf_used, double* est) {
-    for (int w = 0; w < W; w++)
+                              const int32_t* dmode, int dim, const double* dz, const double* du, const double* dlnp0,
+                              double* logl, int32_t* status, int32_t* rf_used, double* est, int32_t* cut) {
+    for (int w = 0; w < W; w++) {
+        rvo_decide dc = {dmode ? dmode[w] : 0, dim, dz ? dz[w] : 1.0, du ? du[w] : 0.5, dlnp0 ? dlnp0[w] : 0.0};
         status[w] = rvo_logl_whx_adapt(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs,
-                                       err, n, npoints, dt, nl, mult, ext_mult, tol_dir, rf_max, logl + w,
-                                       rf_used + 2 * w,
-                                       est + 4 * w);
+                                       err, n, npoints, dt, nl, mult, ext_mult, tol_dir, rf_max, &dc, logl + w,
+                                       rf_used + 2 * w, est + 4 * w, cut + 2 * w);
+    }
 }

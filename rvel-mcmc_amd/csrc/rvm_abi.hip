@@ -145,7 +145,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
 
     // device layout: per direction [seg_n | obs_idx] int32 and [seg_len | obs_rv | obs_s2] f64, + workspace
     const size_t nf = dir[0].idx.size(), nb = dir[1].idx.size();
-    const size_t n_dbl = 3 * (nf + nb) + (size_t)max_walkers + 4;  // schedule f64 | slots | counters (u64)
+    const size_t n_dbl = 3 * (nf + nb) + (size_t)max_walkers + 5;  // schedule f64 | slots | counters (u64)
     const size_t n_int = 2 * (nf + nb);
     const size_t bytes = n_dbl * sizeof(double) + n_int * sizeof(int32_t) + 64;
     rvm_plan* plan = new rvm_plan();
@@ -336,13 +336,16 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.ext_nt = 8;
     P.inv_ext = 1.0;
     P.lvx = nullptr;
+    P.rvp = nullptr;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
-    for (int k = 0; k <= RVM_MAX_LEVELS; k++) P.lw5[k] = P.lw4x[k] = 0.0;
+    P.ext_spec = 0;
+    for (int k = 0; k <= RVM_MAX_LEVELS; k++) P.lw5[k] = 0.0;
     if (P.rmax > 0 && cfg->n_levels >= 2 && cfg->n_levels < RVM_MAX_LEVELS) {
         const int nl = cfg->n_levels;
         const size_t emax = std::max<size_t>(std::max(nf, nb), 1);
-        const size_t bx = 2 * emax * (size_t)nl * (size_t)max_walkers * sizeof(double);
+        const size_t bl = 2 * emax * (size_t)nl * (size_t)max_walkers * sizeof(double);  // levels
+        const size_t bx = bl + 2 * emax * (size_t)max_walkers * sizeof(double);         // + last RV
         if (bx <= RVM_EXT_MAX_BYTES) {
             if (hipMalloc(&plan->xmem, bx) != hipSuccess) {
                 plan->xmem = nullptr;
@@ -357,7 +360,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
                 if (mult[k] > mult[fin]) fin = k;
             }
             m5[nl] = mult[fin] + 1;
-            auto lagrange = [&](int k0, int n, double* w) {  // weights of levels k0 .. n-1 of m5
+            auto lagrange = [&](int k0, int n, double* w) {  // Lagrange-at-zero weights of levels k0 .. n-1 of m5
                 for (int k = k0; k < n; k++) {
                     const double xk = 1.0 / ((double)m5[k] * m5[k]);
                     double wk = 1.0;
@@ -370,11 +373,12 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
                 }
             };
             lagrange(0, nl + 1, P.lw5);
-            lagrange(1, nl + 1, P.lw4x);
             P.ext_mult = m5[nl];
             P.ext_nt = P.nt[fin];
+            P.ext_spec = P.spec[fin];  // (a finer step than the finest level's: speculate where it does)
             P.inv_ext = 1.0 / m5[nl];
             P.lvx = reinterpret_cast<double*>(plan->xmem);
+            P.rvp = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(plan->xmem) + bl);
             P.lvx_emax = (int32_t)emax;
             P.lvx_stride = max_walkers;
         }
@@ -398,10 +402,10 @@ int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult) {
 }
 
 int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
-                    int64_t* unresolved, int64_t* refined, void* stream) {
+                    int64_t* unresolved, int64_t* refined, int64_t* truncated, void* stream) {
     if (!plan) return fail(-1, "rvm_plan_faults: null plan");
     hipStream_t st = (hipStream_t)stream;
-    unsigned long long h[4] = {0, 0, 0, 0};
+    unsigned long long h[5] = {0, 0, 0, 0, 0};
     hipError_t e = hipMemcpyAsync(h, plan->dev.counters, sizeof(h), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e != hipSuccess) return hip_fail(e, "rvm_plan_faults");
@@ -409,6 +413,7 @@ int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, in
     if (nonfinite) *nonfinite = (int64_t)h[1];
     if (unresolved) *unresolved = (int64_t)h[2];
     if (refined) *refined = (int64_t)h[3];
+    if (truncated) *truncated = (int64_t)h[4];
     if (reset) {
         // the hand-off slots back to their sentinels (late level-1 stores of a launch that gave up
         // have landed: the stream's earlier work is complete), then the counters
@@ -492,9 +497,9 @@ int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_
 
 int rvm_stretch_iteration_begin(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params, int32_t n_loc,
                                 int64_t s0_begin, int64_t s1_begin, double* x0, double* lnp0, const double* x1,
-                                int32_t n_half, const double* c0, const double* c1, double a, uint64_t seed,
-                                uint64_t iteration, double hill_factor, double* lnp_spec, int32_t* status_spec,
-                                int32_t* dec, int32_t* accepted0, void* stream) {
+                                const double* lnp1, int32_t n_half, const double* c0, const double* c1, double a,
+                                uint64_t seed, uint64_t iteration, double hill_factor, double* lnp_spec,
+                                int32_t* status_spec, int32_t* dec, int32_t* accepted0, void* stream) {
     if (!plan || !map) return fail(-1, "rvm_stretch_iteration_begin: null plan or map");
     if (n_loc == 0) return 0;
     if (n_loc < 0 || (int64_t)3 * n_loc > plan->max_walkers)
@@ -526,6 +531,7 @@ int rvm_stretch_iteration_begin(const rvm_plan* plan, const rvm_param_map* map, 
     sa.x1 = x1;
     sa.s1_begin = s1_begin;
     sa.dec = dec;
+    sa.lnp1 = lnp1;
     for (int r = 0; r < RVM_MAX_PARAM_ROWS; r++) {
         const int k = r < rows ? map->src[r] : -1;
         if (k >= n_params) return fail(-1, "rvm_stretch_iteration_begin: map source index out of range");

@@ -14,9 +14,9 @@ constexpr int RVM_LDS_PER_CU = 160 * 1024;
 // adaptive resolution: lane state at t = 0 kept in LDS for the refinement passes, per walker group
 // (rx, ry, vx, vy, rz, vz, r, ir of each of the 64 lanes)
 constexpr int RVM_INIT_DOUBLES = 8 * 64;
-// the extension's acceptance (rvm_logl.hip extend_pass; oracle/rvoracle.c EXT_TOL_FRAC / EXT_GAIN_MAX)
-constexpr double RVM_EXT_TOL_FRAC = 0.25;
-constexpr double RVM_EXT_GAIN_MAX = 0.5;
+// the extension's acceptance bound, in units of the direction's tolerance (rvm_logl.hip extend_pass;
+// oracle/rvoracle.c EXT_ACCEPT)
+constexpr double RVM_EXT_ACCEPT = 2.0;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
@@ -50,16 +50,18 @@ struct DevPlan {
     int32_t rmax;
     // the extension (stage 1, rvm_logl.hip extend_pass): one more level of ext_mult steps per base
     // step (0: none) joined to the main pass's levels, which every launch stores in lvx
-    // [2][lvx_emax][n_levels][lvx_stride]; lw5 = weights of all n_levels + 1 levels, lw4x = of the
-    // finer n_levels (lw4x[0] = 0)
-    int32_t ext_mult, ext_nt;
+    // [2][lvx_emax][n_levels][lvx_stride]; lw5 = the weights of all n_levels + 1 levels.  rvp
+    // [2][lvx_emax][lvx_stride]: the last pass's extrapolated RV (main pass, then each halving pass)
+    int32_t ext_mult, ext_nt, ext_spec;
     double inv_ext;
-    double lw5[RVM_MAX_LEVELS + 1], lw4x[RVM_MAX_LEVELS + 1];
+    double lw5[RVM_MAX_LEVELS + 1];
     double* lvx;
+    double* rvp;
     int32_t lvx_emax, lvx_stride;
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
-    // [3] walker-direction refinement passes (extension + halvings)
+    // [3] walker-direction refinement passes (extension + halvings), [4] refinements cut short as
+    // certain rejects
     unsigned long long* counters;
     unsigned long long spin_ticks;  // hand-off waits give up after this long without progress (100 MHz)
     double npoints;
@@ -104,6 +106,8 @@ struct StretchArgs {
     const double* x1;   // half 1's free parameters [dim][n_spec]
     int64_t s1_begin;   // global index of half 1's walker 0 (Philox key)
     int32_t* dec;       // [n_spec] half 0's accept decisions (1 accepted)
+    const double* lnp1;  // [n_spec] half 1's log-probabilities (nullable): its accept inputs, for the
+                         // adaptive resolution's certain-reject test
     // fused MH step (rvm_mh_step; c == nullptr, mh_scale != nullptr): walker w is chain w with
     // free parameters x [dim][xstride], proposal q = x + mh_step * mh_scale[p] * N(0,1) formed in the
     // prologue (Philox keyed by s0_begin + w), MH accept at the end against lnp

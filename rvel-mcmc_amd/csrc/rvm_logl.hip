@@ -300,7 +300,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // their results for the refinement team
     __shared__ unsigned long long s_need[2];
     __shared__ int s_vd[2];
-    __shared__ double s_fchi[2][64], s_fest[2][64];
+    __shared__ double s_fchi[2][64];
     __shared__ int s_fenc[2][64];
     double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
@@ -738,9 +738,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
             const int wo = w0 + lane;
             if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[e] * W + wo] = rvx;
-            if (P.ext_mult > 0 && wo < W) {  // the levels, for a later extension (extend_pass)
+            if (P.ext_mult > 0 && wo < W) {  // the levels and the RV, for a later refinement
                 double* xo = P.lvx + ((size_t)(d * P.lvx_emax + e) * nl) * P.lvx_stride + wo;
                 for (int k = 0; k < nl; k++) xo[(size_t)k * P.lvx_stride] = s_rv[e & 1][k][lane];
+                P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + wo] = rvx;
             }
         }
         n1 = n1_next;
@@ -830,12 +831,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // s_sched + dr * 4 * emax2 (level-split) or l_dir -- from the lanes' state at t = 0 (l_init),
     // gated drifts, one barrier per epoch over eb epochs (the longer direction's count in the
     // level-split layout, whose units are the two directions); lr < 0: an idle wave (barriers
-    // only).  The combiner lanes (level 0's wave, lane = walker slot) accumulate chi2 (c2) and the
-    // estimate (e2) of the walkers marked in `need` and overwrite their rv_out rows.  The wave's
-    // encounter flags land in s_enc_all[gr][lr][slot] (final barrier).
+    // only).  The combiner lanes (level 0's wave, lane = walker slot) accumulate chi2 (c2), the
+    // estimate (e2) and the change of chi2 from the previous pass (d2: sum |(rv - o)^2 - (rv_prev -
+    // o)^2| / s2, the previous pass's RV kept in P.rvp; +inf without it) of the walkers marked in
+    // `need` and overwrite their rv_out rows.  The wave's encounter flags land in
+    // s_enc_all[gr][lr][slot] (final barrier).
     int dummy_redo = 0;
     auto refine_pass = [&](const int rf, const int lr, const int gr, const int dr, const int eb, const uint64_t need,
-                           double& c2, double& e2) {
+                           double& c2, double& e2, double& d2) {
         const DirSched& SR = dr ? P.bwd : P.fwd;
         const int Er = SR.n_epochs;
         const double* r_dir = dec ? s_sched + (size_t)dr * 4 * emax2 : l_dir;
@@ -865,8 +868,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const double sc = ldexp(P.inv_mult[lr_u], -rf);  // (exact: a power-of-two scaling)
         c2 = 0.0;
         e2 = 0.0;
+        d2 = P.ext_mult > 0 ? 0.0 : INFINITY;
+        const bool mine = work && lr == 0 && lane < WPB && ((need >> lane) & 1) && P.ext_mult > 0;
+        double* pp = P.rvp + (size_t)dr * P.lvx_emax * P.lvx_stride + (mine ? w0 + lane : 0);
         for (int e = 0; e < eb; e++) {
             const bool here = e < Er;
+            const double pv = mine && here ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued before the segment)
             const int ns = work && here ? r_n[e] * m_r : 0;
             if (ns > 0) {
                 const double h = r_len[e] * sc;
@@ -889,6 +896,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 const double r = rvx - r_rv[e];
                 c2 += (r * r) / r_s2[e];
                 e2 += fabs((rvx - rv3) * (r + (rv3 - r_rv[e]))) / r_s2[e];
+                if (mine) {
+                    d2 += fabs((rvx - pv) * (r + (pv - r_rv[e]))) / r_s2[e];
+                    pp[(size_t)e * P.lvx_stride] = rvx;
+                }
                 const int wo = w0 + lane;
                 if (rv_out != nullptr && wo < W) rv_out[(size_t)r_idx[e] * W + wo] = rvx;
             }
@@ -899,16 +910,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // ---- adaptive resolution, stage 1: the extension level ----------------------------------
     // One wave per group / unit -- its combiner wave -- integrates one more level (P.ext_mult steps
     // per base step) of direction dr from t = 0 and joins it, epoch by epoch, to the main pass's
-    // levels stored in P.lvx: r5 = all nl + 1 levels (lw5), r4x = the finer nl (lw4x).  A marked
-    // walker (combiner lane `lane`, its bit in need_m) is settled -- chi2 from r5 -- when the pair
-    // agrees (sum |(r5-o)^2 - (r4x-o)^2| / s2 <= RVM_EXT_TOL_FRAC rtol_dir npoints) and r5 moved the
-    // answer by at most RVM_EXT_GAIN_MAX of the main pass's estimate est0 (both sums before the
-    // division by npoints); an encounter of the extension ends it ENCOUNTER, a non-finite one
-    // NONFINITE; otherwise the halving passes follow.  One wave, no barrier: each epoch's value
+    // levels stored in P.lvx: r5 = all nl + 1 levels (lw5).  A marked walker (combiner lane `lane`,
+    // its bit in need_m) is settled -- chi2 from r5 -- when the extension changed chi2 by at most
+    // sum |(r5-o)^2 - (r-o)^2| / s2 <= RVM_EXT_ACCEPT rtol_dir npoints (r = the main pass's RV); an
+    // encounter of the extension ends it ENCOUNTER, a non-finite one NONFINITE; otherwise the
+    // halving passes follow.  One wave, no barrier: each epoch's value
     // moves from the walker's first lane to its combiner lane by a shuffle, and the stored levels
     // of the next epoch load while this one integrates.
-    auto extend_pass = [&](const int gr, const int dr, const uint64_t need_m, bool& need, double& chi2w, int& enc,
-                           const double est0) {
+    auto extend_pass = [&](const int gr, const int dr, const uint64_t need_m, bool& need, double& chi2w, int& enc) {
         const DirSched& SR = dr ? P.bwd : P.fwd;
         const int Er = SR.n_epochs;
         const double* r_dir = dec ? s_sched + (size_t)dr * 4 * emax2 : l_dir;
@@ -941,7 +950,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         double a[RVM_MAX_LEVELS];
 #pragma unroll
         for (int k = 0; k < RVM_MAX_LEVELS; k++) a[k] = cl && k < nl && Er > 0 ? xs[(size_t)k * P.lvx_stride] : 0.0;
-        double c5 = 0.0, e5 = 0.0, dd = 0.0;
+        double c5 = 0.0, dd = 0.0;
+        int x_off = 0, x_bo = 4;  // speculation back-off (as the main pass's spec_off / spec_bo)
         for (int e = 0; e < Er; e++) {
             double b[RVM_MAX_LEVELS];
             const bool nx = cl && e + 1 < Er;
@@ -951,7 +961,19 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             const int ns = r_n[e] * mx;
             if (ns > 0) {
                 const double h = r_len[e] * ix;
-                if (ntx <= 6)
+                if (P.ext_spec && ntx <= 6) {  // (the main pass's speculation policy: same bits)
+                    if (x_off == 0) {
+                        if (segment<6, true, D3, NP, L>(s, kq, h, ns, dummy_redo)) {
+                            x_off = x_bo;
+                            x_bo = x_bo < 64 ? 2 * x_bo : 64;
+                        } else {
+                            x_bo = 4;
+                        }
+                    } else {
+                        segment<6, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                        x_off--;
+                    }
+                } else if (ntx <= 6)
                     segment<6, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
                 else if (ntx == 7)
                     segment<7, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
@@ -961,7 +983,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             const double v = star_vx<NP, L>(s);
             const double vx = __shfl(v, cs * L);
             if (cl) {
-                double r = 0.0, r5 = 0.0, r4x = 0.0;
+                double r = 0.0, r5 = 0.0;
 #pragma unroll
                 for (int k = 0; k < RVM_MAX_LEVELS; k++)
                     if (k < nl) r += P.lw[k] * a[k];
@@ -969,13 +991,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 for (int k = 0; k < RVM_MAX_LEVELS; k++)
                     if (k < nl) r5 += P.lw5[k] * a[k];
                 r5 += P.lw5[nl] * vx;
-#pragma unroll
-                for (int k = 1; k < RVM_MAX_LEVELS; k++)
-                    if (k < nl) r4x += P.lw4x[k] * a[k];
-                r4x += P.lw4x[nl] * vx;
                 const double q = r5 - r_rv[e];
                 c5 += (q * q) / r_s2[e];
-                e5 += fabs((r5 - r4x) * (q + (r4x - r_rv[e]))) / r_s2[e];
                 dd += fabs((r5 - r) * (q + (r - r_rv[e]))) / r_s2[e];
                 if (rv_out != nullptr && wo < W) rv_out[(size_t)r_idx[e] * W + wo] = r5;
             }
@@ -991,7 +1008,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             } else if (!isfinite(c5)) {
                 chi2w = c5;  // (NONFINITE at the direction meeting)
                 need = false;
-            } else if (e5 <= RVM_EXT_TOL_FRAC * P.rtol_dir * P.npoints && dd <= RVM_EXT_GAIN_MAX * est0) {
+            } else if (dd <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
                 chi2w = c5;
                 need = false;
             }
@@ -1001,16 +1018,47 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // set by the caller, one barrier since): first the extension (the combiner waves, lr == 0),
     // then halving passes; the combiner lanes (cmb: level 0's wave, lane < WPB) update chi2w / enc /
     // need per pass; a walker leaves when its estimate drops to the bound or a finer pass meets an
-    // encounter, and is UNRESOLVED if still above after rmax passes.  est0: the main pass's estimate.
+    // encounter, and is UNRESOLVED if still above after rmax passes.
+    // Certain rejects (fused sampler launches only): after a halving pass, a proposal whose accept
+    // test fails even at logL_hi = -(c2 - d2) / npoints -- this direction's chi2 less the change the
+    // halving brought (a bound on the pass's own error: asymptotically that error is d2 / 255),
+    // the other direction's chi2 >= 0 left out -- is rejected whatever further passes would give:
+    // it stops refining and keeps this pass's value (never stored: rejected).  Counted in
+    // counters[4].
     auto refine_loop = [&](const int lr, const int gr, const int dr, const int gmask, const int eb, const bool cmb,
-                           bool& need, double& chi2w, int& enc, const double est0) {
+                           bool& need, double& chi2w, int& enc) {
+        // the combiner lane's accept inputs: 0 none, 1 stretch (emcee), 2 MH
+        int dmode = 0;
+        double dz = 0.0, du = 0.0, dl = 0.0;
+        if (cmb && need && P.ext_mult > 0) {
+            const int wo = w0 + lane;
+            if (stretch) {
+                int k2, wk2, j2, jp2;
+                double z2, zp2;
+                stretch_slot(sa, wo, k2, wk2, z2, j2, zp2, jp2);
+                if (k2 == 0) {
+                    dmode = 1;
+                    du = stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half);
+                    dl = sa.lnp[wo];
+                } else if (sa.lnp1 != nullptr) {  // half 1 of a speculative iteration (accepts later)
+                    dmode = 1;
+                    du = stretch_u3(sa.seed, (uint64_t)(sa.s1_begin + wk2), sa.iteration, 1u);
+                    dl = sa.lnp1[wk2];
+                }
+                dz = z2;
+            } else if (mh) {
+                dmode = 2;
+                du = mh_u(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration);
+                dl = sa.lnp[wo];
+            }
+        }
         if (P.ext_mult > 0) {
             const uint64_t gneed = s_need[gr];
             if (lr == 0 && gneed) {
                 if (lane == 0)
                     __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(gneed),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                extend_pass(gr, dr, gneed, need, chi2w, enc, est0);
+                extend_pass(gr, dr, gneed, need, chi2w, enc);
                 const uint64_t nb = ballot(need);
                 if (lane == 0) s_need[gr] = nb;
             }
@@ -1022,16 +1070,22 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (lr == 0 && lane == 0 && gneed)
                 __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(gneed),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            double c2, e2;
-            refine_pass(rf, lr, gr, dr, eb, gneed, c2, e2);
+            double c2, e2, d2;
+            refine_pass(rf, lr, gr, dr, eb, gneed, c2, e2, d2);
+            bool cut = false;
             if (cmb && need) {
                 int er = 0;
                 for (int k = 0; k < nl; k++) er |= s_enc_all[gr][k][lane];
                 chi2w = c2;
+                const double lp_hi = -(c2 - d2) / P.npoints;
                 if (er) {
                     enc |= er;
                     need = false;
                 } else if (!(e2 / P.npoints > P.rtol_dir)) {
+                    need = false;
+                } else if (dmode == 1 ? !stretch_accepts(sa.dim, dz, lp_hi, dl, du)
+                                      : (dmode == 2 && !mh_accepts(lp_hi, dl, du))) {
+                    cut = true;  // a certain reject
                     need = false;
                 } else if (rf == P.rmax) {
                     enc |= RVM_ENC_UNRESOLVED;
@@ -1040,7 +1094,13 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             }
             if (lr == 0) {
                 const uint64_t nb = ballot(need);
-                if (lane == 0) s_need[gr] = nb;
+                const uint64_t nc = ballot(cut);
+                if (lane == 0) {
+                    s_need[gr] = nb;
+                    if (nc)
+                        __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)__builtin_popcountll(nc),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             __syncthreads();
             if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) break;
@@ -1067,7 +1127,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 }
                 __syncthreads();
                 if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
-                    refine_loop(lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc, est);
+                    refine_loop(lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc);
             }
         }
         if (cmb && wo < W) {
@@ -1200,10 +1260,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 chi2w += (r * r) / l_s2[e];
                 est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
                 if (rv_out != nullptr && valid && pl_idx == 0) rv_out[(size_t)l_idx[e] * W + w] = rvx;
-                if (P.ext_mult > 0 && valid && pl_idx == 0) {  // the levels, for a later extension
+                if (P.ext_mult > 0 && valid && pl_idx == 0) {  // the levels and the RV, for a refinement
                     double* xo = P.lvx + ((size_t)(d * P.lvx_emax + e) * 4) * P.lvx_stride + w;
 #pragma unroll
                     for (int k = 0; k < 4; k++) xo[(size_t)k * P.lvx_stride] = v[k];
+                    P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = rvx;
                 }
                 if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 rr = rr + 1 == RING ? 0 : rr + 1;
@@ -1246,7 +1307,6 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 if (valid && pl_idx == 0) finish_recompute(w, chi2w, enc);
             } else if (valid && pl_idx == 0) {
                 s_fchi[ul][slot] = chi2w;
-                s_fest[ul][slot] = est;
                 s_fenc[ul][slot] = enc | (need ? 16 : 0);
             }
             if (lane == 0) __hip_atomic_store(s_vd + ul, refine ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1276,12 +1336,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         d = gr;  // (the finishing lanes meet the other direction as unit gr: finish() reads d)
         const bool cmb = lr == 0 && lane < WPB;
         const bool mine = (gr == 0 ? v0 : v1) == 2;
-        double chi2w = 0.0, est0 = 0.0;
+        double chi2w = 0.0;
         int enc = 0;
         bool need = false;
         if (cmb && mine) {
             chi2w = s_fchi[gr][lane];
-            est0 = s_fest[gr][lane];
             const int f = s_fenc[gr][lane];
             enc = f & 15;
             need = (f & 16) != 0 && w0 + lane < W;
@@ -1291,7 +1350,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (lane == 0) s_need[gr] = nb;
         }
         __syncthreads();
-        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, est0);
+        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc);
         if (cmb && mine && w0 + lane < W) finish_recompute(w0 + lane, chi2w, enc);
         return;
     }

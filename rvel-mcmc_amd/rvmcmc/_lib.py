@@ -80,7 +80,7 @@ SIGNATURES = {
                                   C.POINTER(C.c_double), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     "rvm_plan_destroy": (None, [C.c_void_p]),
     "rvm_plan_faults": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
-                                  C.POINTER(C.c_int64), C.POINTER(C.c_int64), _dp]),
+                                  C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64), _dp]),
     "rvm_plan_set_handoff_timeout": (C.c_int, [C.c_void_p, C.c_double]),
     "rvm_plan_extension": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rvm_plan_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
@@ -94,7 +94,7 @@ SIGNATURES = {
                                         _dp, C.c_int32, _dp, C.c_double, C.c_uint64, C.c_uint64, C.c_uint32,
                                         C.c_double, _dp, _dp, _dp, _dp]),
     "rvm_stretch_iteration_begin": (C.c_int, [C.c_void_p, C.POINTER(ParamMapC), C.c_int32, C.c_int32, C.c_int64,
-                                              C.c_int64, _dp, _dp, _dp, C.c_int32, _dp, _dp, C.c_double, C.c_uint64,
+                                              C.c_int64, _dp, _dp, _dp, _dp, C.c_int32, _dp, _dp, C.c_double, C.c_uint64,
                                               C.c_uint64, C.c_double, _dp, _dp, _dp, _dp, _dp]),
     "rvm_stretch_iteration_end": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int64, _dp, _dp, _dp, _dp, _dp,
                                             _dp, _dp, C.c_int32, _dp, _dp, _dp, _dp, C.c_double, C.c_uint64,

@@ -169,13 +169,13 @@ class LoglPlan:
 
     def faults(self, reset=False, stream=None) -> dict:
         """rvm_plan_faults: the plan's counters (synchronises the stream): hand-off timeouts, NONFINITE
-        and UNRESOLVED results, refined walker-directions; reset=True zeroes them and restores the
-        hand-off workspace."""
-        vals = [C.c_int64() for _ in range(4)]
+        and UNRESOLVED results, refinement passes, refinements cut short on a certain reject;
+        reset=True zeroes them and restores the hand-off workspace."""
+        vals = [C.c_int64() for _ in range(5)]
         _lib.check(self.lib.rvm_plan_faults(self._h, int(bool(reset)), *[C.byref(v) for v in vals],
                                             _lib.stream_handle(stream)), "rvm_plan_faults")
         return dict(handoff_timeouts=vals[0].value, nonfinite=vals[1].value, unresolved=vals[2].value,
-                    refined=vals[3].value)
+                    refined=vals[3].value, truncated=vals[4].value)
 
     def check_faults(self, what="plan", stream=None) -> dict:
         """Raise RvmError on hand-off timeouts or NONFINITE results since the last check (emcee
@@ -281,12 +281,13 @@ class LoglPlan:
         _lib.check(rc, "rvm_stretch_half_step")
 
     def stretch_iteration_begin(self, pmap, X0, lnp0, X1, c0_aos, c1_aos, s0_begin, s1_begin, a, seed, iteration,
-                                lnp_spec, status_spec, dec, hill_factor=1.0, accepted0=None, stream=None):
+                                lnp_spec, status_spec, dec, hill_factor=1.0, accepted0=None, stream=None, lnp1=None):
         """First launch of a speculative stretch iteration (rvm_stretch_iteration_begin): half 0's
         half-step (X0 [dim][n], lnp0 [n] updated in place, decisions to dec [n]) and half 1's
         proposals from X1 [dim][n] against both possible positions of their partners, logl of all
         3 n slots to lnp_spec / status_spec [3 n].  c0_aos / c1_aos: both halves walker-major
-        [n_half][dim] as at the start of the iteration (unchanged until the end call)."""
+        [n_half][dim] as at the start of the iteration (unchanged until the end call).  lnp1 [n]
+        (optional): half 1's log-probabilities, the accept inputs of its slots."""
         torch = _torch()
         for t in (X0, lnp0, X1, c0_aos, c1_aos, lnp_spec):
             if t.dtype != torch.float64 or t.device != self.device or not t.is_contiguous():
@@ -298,6 +299,9 @@ class LoglPlan:
             raise ValueError("shape mismatch between X0/X1 [dim][n], lnp0 [n] and c0_aos/c1_aos [n_half][dim]")
         if lnp_spec.shape != (3 * n,) or status_spec.shape != (3 * n,) or dec.shape != (n,):
             raise ValueError("lnp_spec / status_spec must be [3 n], dec [n]")
+        if lnp1 is not None and (lnp1.dtype != torch.float64 or lnp1.device != self.device or lnp1.shape != (n,)
+                                 or not lnp1.is_contiguous()):
+            raise ValueError("lnp1 must be a contiguous float64 [n] tensor on the plan's device")
         if status_spec.dtype != torch.int32 or dec.dtype != torch.int32:
             raise ValueError("status_spec and dec must be int32")
         if 3 * n > self.max_walkers:
@@ -305,7 +309,8 @@ class LoglPlan:
         with torch.cuda.device(self.device):
             rc = self.lib.rvm_stretch_iteration_begin(
                 self._h, C.byref(pmap.c_map()), dim, n, int(s0_begin), int(s1_begin), X0.data_ptr(), lnp0.data_ptr(),
-                X1.data_ptr(), n_half, c0_aos.data_ptr(), c1_aos.data_ptr(), float(a), int(seed), int(iteration),
+                X1.data_ptr(), lnp1.data_ptr() if lnp1 is not None else 0, n_half, c0_aos.data_ptr(), c1_aos.data_ptr(),
+                float(a), int(seed), int(iteration),
                 float(hill_factor), lnp_spec.data_ptr(), status_spec.data_ptr(), dec.data_ptr(),
                 accepted0.data_ptr() if accepted0 is not None else 0, _lib.stream_handle(stream))
         _lib.check(rc, "rvm_stretch_iteration_begin")

@@ -132,7 +132,7 @@ class DeviceOps:
             e0.record()
         self.plan.stretch_iteration_begin(s.pmap, s.pos[0], s.lnp[0], s.pos[1], c0, c1, s.global_begin(0),
                                           s.global_begin(1), s.a, s.seed, s.iteration, s._lnp_spec, s._st_spec,
-                                          s._dec, hill_factor=s.hill_factor, accepted0=s.naccepted[:n])
+                                          s._dec, hill_factor=s.hill_factor, accepted0=s.naccepted[:n], lnp1=s.lnp[1])
         if self.timing is not None:
             e1.record()
             self.timing.append((e0, e1, 3 * n))

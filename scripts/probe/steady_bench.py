@@ -1,0 +1,49 @@
+"""The bench's sampler at the steady state of its own chain: the bench setup (bench.py: 2-planet
+synthetic, 101 epochs, 4096 walkers) started from the ensemble after 2000 iterations
+(scripts/probe/ens_it2000.npy, from scripts/dump_bench_ensemble.py) instead of the initial ball;
+iterations/s and evaluations/s with the adaptive resolution off and on, and its counters."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, "rvel-mcmc_amd"), os.path.join(ROOT, "tests")]
+import torch  # noqa: E402
+
+from conftest import S2_PLANETS  # noqa: E402
+from rvmcmc import engine  # noqa: E402
+from rvmcmc.ensemble import EnsembleSampler  # noqa: E402
+from rvmcmc.observations import FakeObservation  # noqa: E402
+from rvmcmc.state import State  # noqa: E402
+
+
+def run(resolve_tol, iters=10, warm=3):
+    state = State(planets=[dict(p) for p in S2_PLANETS])
+    state.integrator = engine.IntegratorConfig(resolve_tol=resolve_tol)
+    np.random.seed(2017)
+    obs = FakeObservation(state, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+    X = np.load(os.path.join(ROOT, "scripts/probe/ens_it2000.npy"))
+    ens = EnsembleSampler(len(X), state, obs, seed=2017)
+    ens.set_positions(X)
+    ens.compute_lnprob()
+    for _ in range(warm):
+        ens.step()
+    torch.cuda.synchronize()
+    f0 = ens.check_faults()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        ens.step()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    f = ens.check_faults()
+    return dict(resolve_tol=resolve_tol, walkers=len(X), iterations=iters, ms_per_iteration=1e3 * dt / iters,
+                evals_per_s=len(X) * iters / dt, speculative=bool(ens.speculating()), faults=f,
+                faults_warm=f0)
+
+
+if __name__ == "__main__":
+    for tol in (0.0, 5e-7):
+        print(json.dumps(run(tol)), flush=True)

@@ -48,7 +48,7 @@ def test_argument_errors_do_not_touch_the_device():
     assert lib.rvm_logl_batch(None, 1, 0, 1.0, 0, 0, 0, 0) < 0
     m = _lib.ParamMapC()
     assert lib.rvm_stretch_half_step(None, C.byref(m), 10, 1, 0, 0, 0, 0, 1, 0, 2.0, 0, 0, 0, 1.0, 0, 0, 0, 0) < 0
-    assert lib.rvm_stretch_iteration_begin(None, C.byref(m), 10, 1, 0, 8, 0, 0, 0, 8, 0, 0, 2.0, 0, 0, 1.0, 0, 0, 0,
+    assert lib.rvm_stretch_iteration_begin(None, C.byref(m), 10, 1, 0, 8, 0, 0, 0, 0, 8, 0, 0, 2.0, 0, 0, 1.0, 0, 0, 0,
                                            0, 0) < 0
     # end: half 1's walker range must lie in the second half (s1_begin >= n_half)
     one = (C.c_double * 1)(0.0)
@@ -71,7 +71,7 @@ def test_argument_errors_do_not_touch_the_device():
     cfg3.resolve_tol, cfg3.resolve_max = 5e-7, 9
     rc = lib.rvm_plan_create(C.byref(cfg3), z, z, z, 1, 64, C.byref(h))
     assert rc < 0 and b"resolve_max" in lib.rvm_last_error()
-    assert lib.rvm_plan_faults(None, 0, None, None, None, None, 0) < 0
+    assert lib.rvm_plan_faults(None, 0, None, None, None, None, None, 0) < 0
     assert lib.rvm_plan_set_handoff_timeout(None, 1.0) < 0
     assert lib.rvm_plan_extension(None, None) < 0
     # workspace: per (chain, pair i >= j) and direction, 4 f64 partial sums and an int32 status

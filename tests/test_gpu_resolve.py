@@ -85,28 +85,43 @@ def _par(fn, P, nt=16):
     return [np.concatenate([p[k] for p in parts]) for k in range(len(parts[0]))]
 
 
+def _par_ix(fn, P, nt=16):
+    """_par for fn(P_chunk, index_chunk)."""
+    idx = np.array_split(np.arange(len(P)), nt)
+    with ThreadPoolExecutor(nt) as ex:
+        parts = list(ex.map(lambda ix: fn(P[ix], ix), idx))
+    return [np.concatenate([p[k] for p in parts]) for k in range(len(parts[0]))]
+
+
 def _adapt_oracle(P, obs, dt, mult, tol=TOL, rmax=RMAX):
     return _par(lambda p: O.logl_whx_adapt_batch(p, 2, obs, dt, mult, tol, rmax), P)
 
 
-def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX, has_inc=0):
+def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX, has_inc=0, ctx=None):
     """T1 of an adaptive-resolution launch against the oracle's restatement of the same rule
     (oracle.logl_whx_adapt_batch): statuses and logL, up to sensitivity.  Chaotic walkers (close
     approaches) and decisions at roundoff distance from their bound may legitimately go the other
     way in a second implementation: the oracle's own response to 1e-15 relative input nudges (of
     logL, of the status, of the stage reached and of the final estimate -- a difference of two
     extrapolations, which near a close approach moves by up to tens of percent under such a nudge),
-    and its closest approach to any decision's bound.  Returns (stages [W][2], sensitive [W])."""
+    and its closest approach to any decision's bound.  ctx: the sampler's accept inputs (the
+    certain-reject cut; oracle.logl_whx_adapt_batch).  Returns (stages [W][2], sensitive [W]) and,
+    with ctx, the oracle's cut [W][2]."""
     W = len(got)
-    fn = lambda p: O.logl_whx_adapt_batch(p, n_planets, obs, dt, mult, tol, rmax, has_inc=has_inc)
-    ref, st_ref, rf, est, margin = _par(fn, P)
+
+    def fn(p, ix=None):
+        c = None if ctx is None else dict(ctx, **{k: np.asarray(ctx[k])[ix] for k in ("mode", "z", "u", "lnp0")})
+        r = O.logl_whx_adapt_batch(p, n_planets, obs, dt, mult, tol, rmax, has_inc=has_inc, ctx=c)
+        return r if ctx is not None else r + (np.zeros((len(p), 2), dtype=np.int32),)
+
+    ref, st_ref, rf, est, margin, cut = _par_ix(fn, P)
     sens = np.zeros(W)
     flips = np.zeros(W, dtype=bool)
     for pl, par, sgn in [(0, 4, 1), (-1, 4, -1), (0, 1, 1)]:
         P2 = P.copy()
         P2[:, pl, par] *= 1 + sgn * 1e-15
-        r2, s2, rf2, est2, _ = _par(fn, P2)
-        flips |= (s2 != st_ref) | np.any(rf2 != rf, axis=1)
+        r2, s2, rf2, est2, _, cut2 = _par_ix(fn, P2)
+        flips |= (s2 != st_ref) | np.any(rf2 != rf, axis=1) | np.any(cut2 != cut, axis=1)
         with np.errstate(invalid="ignore"):  # (an estimate whose roundoff response is not small
             # against its distance from the bound)
             flips |= np.any(np.abs(est2 - est) > 0.02 * np.abs(est - 0.5 * tol), axis=1)
@@ -124,6 +139,8 @@ def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX,
     assert np.mean(err <= T1_REL) > 0.9
     # walkers the oracle leaves UNRESOLVED are UNRESOLVED on the device too (up to sensitivity)
     assert np.all(((st == 4) == (st_ref == 4)) | sensitive)
+    if ctx is not None:
+        return rf, sensitive, cut
     return rf, sensitive
 
 
@@ -157,7 +174,7 @@ def test_tight_ball_never_refines_and_keeps_the_bits():
     f = plan.faults()
     np.testing.assert_array_equal(st, st0)
     np.testing.assert_array_equal(got, got0)
-    assert f == dict(handoff_timeouts=0, nonfinite=0, unresolved=0, refined=0), f
+    assert f == dict(handoff_timeouts=0, nonfinite=0, unresolved=0, refined=0, truncated=0), f
 
 
 def test_flag_only_matches_oracle():
@@ -223,3 +240,48 @@ def test_level_split_encounter_on_the_last_lower_lane_stays_local():
     ref, st_ref, _, _, _ = _adapt_oracle(_oracle_P(X), obs, dt, mult)
     assert np.all(st_ref[hit] == 2) and np.all(np.delete(st_ref, hit) == 0)
     np.testing.assert_array_equal(st, st_ref)
+
+
+@pytest.mark.parametrize("W", [4096, 12288])  # halves of 2048 (LDS-coupled) / 6144 (level-split) walkers
+def test_certain_reject_cut_matches_oracle(W):
+    """A fused stretch half-step (the sampler's own launch) on a wide ensemble: refinements whose
+    proposal is rejected whatever further passes give stop early (rvm_plan_faults `truncated`);
+    every proposal's logL and status follow the oracle's restatement of the rule with the same
+    accept inputs (Philox draws restated, tests/philox_ref.py), and the decisions are the sampler's
+    emcee test on those values.  An accepted proposal is never cut: its value is fully resolved."""
+    torch = _torch()
+    import ias15_parity as IP
+    from philox_ref import stretch_uniforms
+    from rvmcmc.ensemble import EnsembleSampler
+    from rvmcmc.state import State
+
+    s = State(planets=[dict(p) for p in S2_PLANETS])
+    obs = s2_obs_oracle()
+    X0 = wide_walkers(W, ball=0.6, seed=13)
+    ens = EnsembleSampler(W, s, obs, seed=5)
+    ens.set_positions(X0)
+    ens.compute_lnprob()
+    n, it = ens.nloc, ens.iteration
+    before = ens.pos[0].t().cpu().numpy().copy()
+    c = ens.pos[1].t().cpu().numpy().copy()
+    lnp0 = ens.lnp[0].cpu().numpy().copy()
+    ens.plan.faults(reset=True)
+    ens.half_step(ens.pos[0], ens.lnp[0], ens.pos[1], 0)
+    torch.cuda.synchronize()
+    f = ens.plan.faults(reset=True)
+    got, st = ens._lnp_new.cpu().numpy(), ens._status.cpu().numpy()
+    after = ens.pos[0].t().cpu().numpy()
+    u1, u2, u3 = stretch_uniforms(ens.seed, ens.global_begin(0), n, it, 0)
+    q, z = IP.stretch_proposal(before, c, u1, u2, ens.a)
+    plan = ens.plan
+    ctx = dict(mode=np.ones(n, dtype=np.int32), dim=s.Nvars, z=z, u=u3, lnp0=lnp0)
+    rf, sensitive, cut = assert_t1_adaptive(got, st, IP.to_oracle(s.param_map(), q), 2, obs, plan.dt, plan.mult,
+                                            plan.resolve_tol, plan.resolve_max, ctx=ctx)
+    ncut = int(cut.sum())
+    print(f"W={W}: directions extended {int((rf == 1).sum())}, halved {int((rf >= 2).sum())}, cut {ncut} "
+          f"(oracle); kernel {f}")
+    assert ncut > 10 and abs(f["truncated"] - ncut) <= int(sensitive.sum())
+    with np.errstate(invalid="ignore"):
+        acc = (s.Nvars - 1.0) * np.log(z) + got - lnp0 > np.log(u3)
+    np.testing.assert_array_equal(np.any(after != before, axis=1), acc)
+    assert not np.any(acc & np.any(cut == 1, axis=1) & ~sensitive)
