@@ -1007,14 +1007,17 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /*   est > tol_dir; still above after rf_max: RVO_UNRESOLVED.                                   */
 /* Certain rejects (a sampler's accept inputs given: dmode 1 emcee stretch, 2 MH): after a       */
 /* halving pass whose estimate is still above the bound, the direction stops (status OK, this    */
-/* pass's chi2) when the accept test fails even at lp_hi = -(chi2 - d2) / npoints, d2 = the     */
-/* pass's change of chi2 from the previous pass (the main pass for rf = 1),                      */
-/*   d2 = sum |(r - o)^2 - (r_prev - o)^2| / s2.                                                */
+/* pass's chi2) when the accept test fails even at lp_hi = -(chi2 - min(d2, CUT_EST_FACTOR est)) */
+/* / npoints, d2 = the pass's change of chi2 from the previous pass (the main pass for rf = 1),  */
+/*   d2 = sum |(r - o)^2 - (r_prev - o)^2| / s2, est the pass's estimate (both before / npoints). */
 /* An encounter or non-finite RV ends the direction at once (no refinement).                    */
 /* ------------------------------------------------------------------------------------------ */
 enum { RVO_UNRESOLVED = 4 };
 #ifndef EXT_ACCEPT /* (overridable for studies of the rule: -DEXT_ACCEPT=...) */
 #define EXT_ACCEPT 2.0
+#endif
+#ifndef CUT_EST_FACTOR
+#define CUT_EST_FACTOR 100.0
 #endif
 
 
@@ -1074,11 +1077,12 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
             if (rf > 0) d2 += fabs((r - prev[i]) * ((r - ob[i]) + (prev[i] - ob[i]))) / s2[i];
             prev[i] = r;
         }
+        const double est_raw = est;
         est /= npoints;
         if (nl >= 2 && tol_dir < INFINITY && margin_of(est, tol_dir) < margin) margin = margin_of(est, tol_dir);
         if (nl < 2 || !(est > tol_dir)) break;
         if (rf > 0 && ext_mult > 0 && dc != NULL && dc->mode != 0) {
-            const double lp_hi = -(chi2 - d2) / npoints;
+            const double lp_hi = -(chi2 - fmin(d2, CUT_EST_FACTOR * est_raw)) / npoints;
             const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0
                                                  : lp_hi - dc->lnp0;
             const double lu = log(dc->u);

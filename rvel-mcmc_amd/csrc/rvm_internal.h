@@ -17,6 +17,10 @@ constexpr int RVM_INIT_DOUBLES = 8 * 64;
 // the extension's acceptance bound, in units of the direction's tolerance (rvm_logl.hip extend_pass;
 // oracle/rvoracle.c EXT_ACCEPT)
 constexpr double RVM_EXT_ACCEPT = 2.0;
+// the certain-reject cut's error bound after a halving pass: min(d2, this x the pass's estimate)
+// (rvm_logl.hip refine_loop; oracle/rvoracle.c CUT_EST_FACTOR; measured error / estimate <= 57 on
+// the main pass at the plan's step, smaller after a halving)
+constexpr double RVM_CUT_EST_FACTOR = 100.0;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {

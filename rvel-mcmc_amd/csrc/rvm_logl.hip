@@ -1020,11 +1020,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // need per pass; a walker leaves when its estimate drops to the bound or a finer pass meets an
     // encounter, and is UNRESOLVED if still above after rmax passes.
     // Certain rejects (fused sampler launches only): after a halving pass, a proposal whose accept
-    // test fails even at logL_hi = -(c2 - d2) / npoints -- this direction's chi2 less the change the
-    // halving brought (a bound on the pass's own error: asymptotically that error is d2 / 255),
-    // the other direction's chi2 >= 0 left out -- is rejected whatever further passes would give:
-    // it stops refining and keeps this pass's value (never stored: rejected).  Counted in
-    // counters[4].
+    // test fails even at logL_hi = -(c2 - min(d2, RVM_CUT_EST_FACTOR e2)) / npoints -- this
+    // direction's chi2 less a bound on the pass's own error (the change the halving brought,
+    // asymptotically 255x that error; or a large multiple of the pass's estimate), the other
+    // direction's chi2 >= 0 left out -- is rejected whatever further passes would give: it stops
+    // refining and keeps this pass's value (never stored: rejected).  Counted in counters[4].
     auto refine_loop = [&](const int lr, const int gr, const int dr, const int gmask, const int eb, const bool cmb,
                            bool& need, double& chi2w, int& enc) {
         // the combiner lane's accept inputs: 0 none, 1 stretch (emcee), 2 MH
@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 int er = 0;
                 for (int k = 0; k < nl; k++) er |= s_enc_all[gr][k][lane];
                 chi2w = c2;
-                const double lp_hi = -(c2 - d2) / P.npoints;
+                const double lp_hi = -(c2 - fmin(d2, RVM_CUT_EST_FACTOR * e2)) / P.npoints;
                 if (er) {
                     enc |= er;
                     need = false;

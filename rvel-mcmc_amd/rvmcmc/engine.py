@@ -377,6 +377,19 @@ def periodic_fault_check(sampler, plan):
 PLAN_CACHE_SIZE = 32  # plans kept per observation set
 
 
+def check_stream(plan, what="sampler"):
+    """A sampler's plan came from plan_for on the stream current at its construction, and a plan's
+    workspace (direction slots, hand-off slots) is single-stream: stepping the sampler from
+    another stream could share that workspace with a concurrent launch.  Raise instead."""
+    want = getattr(plan, "stream", None)
+    if want is None or plan.device.type != "cuda":
+        return
+    cur = _torch().cuda.current_stream(plan.device).cuda_stream
+    if int(cur) != want:
+        raise RuntimeError(f"{what}: stepped on another stream than the one it was built on (its plan's "
+                           f"workspace is single-stream, include/rvmcmc.h); build one sampler per stream")
+
+
 def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0.0, inclined=False,
              resolve=(0.0, 0)) -> LoglPlan:
     """Cached LoglPlan on an Observation object (keyed by device, the caller's current stream and
@@ -393,6 +406,7 @@ def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0
         t, rv, er = obs_arrays(obs)
         cap = max(int(max_walkers), plan.max_walkers * 2 if plan else 0, 64)
         plan = LoglPlan(t, rv, er, obs.Npoints, n_planets, dt, mult, cap, dev, period_hint, inclined, resolve)
+        plan.stream = int(stream)
     cache[key] = plan  # most recently used last
     while len(cache) > PLAN_CACHE_SIZE:  # bounded: the least recently used plan is dropped (freed
         cache.pop(next(iter(cache)))      # when no sampler holds it any more)

@@ -324,7 +324,9 @@ class EnsembleSampler:
         return self._spec_pays
 
     def step(self):
-        """One emcee iteration (both half-steps) over this rank's walkers."""
+        """One emcee iteration (both half-steps) over this rank's walkers (on the stream the sampler
+        was built on: engine.check_stream)."""
+        engine.check_stream(self.plan, "EnsembleSampler.step")
         if self.lnp[0] is None:
             self.compute_lnprob()
         if self.speculating():

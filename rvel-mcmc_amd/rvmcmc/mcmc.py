@@ -261,8 +261,11 @@ class MhChains:
         propose / likelihood / accept launches; bit-identical for the same draws.  In the
         level-split layout every level wave of a walker forms its proposal in its prologue; the
         walker's planet lanes share the Box-Muller draws (rvm_logl.hip), and the fused launch is
-        ahead (4096 chains: 15.3-15.6M vs 14.8-15.1M chain-steps/s, profiles/r02h_configs.jsonl)."""
+        ahead (4096 chains: 15.3-15.6M vs 14.8-15.1M chain-steps/s, profiles/r02h_configs.jsonl).
+        On the stream the chains were built on (engine.check_stream)."""
         import torch
+
+        engine.check_stream(self.plan, "MhChains.step")
 
         st = _lib.stream_handle()
         if fused and draws_propose is None and draws_accept is None:

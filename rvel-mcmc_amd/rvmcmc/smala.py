@@ -201,7 +201,8 @@ class SmalaChains:
         (rvm_smala_stencil_logl; exact: rvm_logl_derivs) and rvm_smala_derive_accept
         (rvm_smala_metric_accept); fused=False runs the separate fd / logl / derive / accept
         launches (bit-identical; 256 chains: 523k vs 485k chain-steps/s fused vs separate,
-        profiles/r02h_configs.jsonl)."""
+        profiles/r02h_configs.jsonl).  The plan is looked up per step for the current stream
+        (State._plan -> engine.plan_for), so any stream is safe."""
         st_h = _lib.stream_handle()
         zp = 0
         if z is not None:

@@ -11,4 +11,9 @@ rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed|W=" gpurun_out/${TAG}_pytest.log |
 timeout -k 10 200 python scripts/probe/resolve_cost.py scripts/probe/slots_it23.npz scripts/probe/slots_it2000.npz 2>&1 | grep -v amdgpu.ids | tee gpurun_out/${TAG}_cost.jsonl || exit 1
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --ess-iters 0 --no-cpu > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json
-timeout -k 10 300 python scripts/probe/steady_bench.py 2>&1 | grep -v amdgpu.ids | tee gpurun_out/${TAG}_steady.jsonl || exit 1
+timeout -k 10 400 python scripts/probe/steady_bench.py ${STEADY:-} 2>&1 | grep -v amdgpu.ids | tee gpurun_out/${TAG}_steady.jsonl || exit 1
+for spec in ${BENCH_VARIANTS:-}; do  # "LEVELS:TOL" variants of the bench line
+  lv=${spec%%:*}; tol=${spec##*:}
+  timeout -k 10 300 python bench.py --steps 20 --warmup 3 --ess-iters 0 --no-cpu --levels $lv --resolve-tol $tol > gpurun_out/${TAG}_bench_${lv}_${tol}.json 2>> gpurun_out/${TAG}_bench.err || exit 1
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], round(d['value']/1e6,3), 'M', d['ms_per_step'], d['resolve'])" gpurun_out/${TAG}_bench_${lv}_${tol}.json
+done

@@ -20,9 +20,9 @@ from rvmcmc.observations import FakeObservation  # noqa: E402
 from rvmcmc.state import State  # noqa: E402
 
 
-def run(resolve_tol, iters=10, warm=3):
+def run(resolve_tol, levels=(4, 5, 6, 7), resolve_max=4, iters=10, warm=3):
     state = State(planets=[dict(p) for p in S2_PLANETS])
-    state.integrator = engine.IntegratorConfig(resolve_tol=resolve_tol)
+    state.integrator = engine.IntegratorConfig(resolve_tol=resolve_tol, levels=tuple(levels), resolve_max=resolve_max)
     np.random.seed(2017)
     obs = FakeObservation(state, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
     X = np.load(os.path.join(ROOT, "scripts/probe/ens_it2000.npy"))
@@ -39,11 +39,15 @@ def run(resolve_tol, iters=10, warm=3):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     f = ens.check_faults()
-    return dict(resolve_tol=resolve_tol, walkers=len(X), iterations=iters, ms_per_iteration=1e3 * dt / iters,
+    return dict(resolve_tol=resolve_tol, resolve_max=resolve_max, levels=list(levels), walkers=len(X), iterations=iters, ms_per_iteration=1e3 * dt / iters,
                 evals_per_s=len(X) * iters / dt, speculative=bool(ens.speculating()), faults=f,
                 faults_warm=f0)
 
 
 if __name__ == "__main__":
-    for tol in (0.0, 5e-7):
-        print(json.dumps(run(tol)), flush=True)
+    # specs "LEVELS:TOL[:RMAX]", e.g. 4,5,6,7:5e-7:4 (default: the bench's levels, resolution off / on)
+    specs = sys.argv[1:] or ["4,5,6,7:0", "4,5,6,7:5e-7"]
+    for sp in specs:
+        f = sp.split(":")
+        print(json.dumps(run(float(f[1]), tuple(int(v) for v in f[0].split(",")), int(f[2]) if len(f) > 2 else 4)),
+              flush=True)

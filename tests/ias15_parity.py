@@ -77,6 +77,8 @@ def ias15_roundoff(P, n_planets, obs, ref, hill=1.0, has_inc=0):
 
 def to_oracle(pm, X):
     """Free-parameter rows X [W][dim] of a State's ParamMap -> oracle layout [W][np][7]."""
+    if len(X) == 0:
+        return np.zeros((0, pm.n_planets, 7))
     K = np.stack([pm.vector_to_kernel_np(x) for x in np.asarray(X, dtype=np.float64)], 1)  # [rows][W]
     rows = 7 if pm.inclined else 5
     W = K.shape[1]
@@ -118,10 +120,13 @@ class Tally:
         self.beyond_margin_not_roundoff = 0
 
     def add(self, acc_dev, acc_ref, margin, st_dev, st_ref, lnq_dev=None, lnq_ref=None, idx_offset=0,
-            roundoff=None):
+            roundoff=None, current_differs=None):
         """margin: |lnpdiff_ias15 - ln u| per decision.  roundoff (optional): the IAS15 logL's own
         roundoff sensitivity per proposal (ias15_roundoff); proposals above ROUNDOFF_REL are
-        exempt from the decision and T2 checks (counted separately)."""
+        exempt from the decision and T2 checks (counted separately).  current_differs (optional):
+        walkers whose CURRENT position has a logL status the two chains disagree on (one finite,
+        the other -inf: a status disagreement counted when that position was proposed or set),
+        whose decision then compares against different lnp0."""
         acc_dev = np.asarray(acc_dev, bool)
         acc_ref = np.asarray(acc_ref, bool)
         st_dev = np.asarray(st_dev)
@@ -129,6 +134,10 @@ class Tally:
         near = margin < MARGIN
         sdiff = st_dev != st_ref
         exempt = near | sdiff
+        if current_differs is not None:
+            cd = np.asarray(current_differs, bool) & ~exempt
+            self.exempt_current = getattr(self, "exempt_current", 0) + int(cd.sum())
+            exempt = exempt | cd
         chaotic = np.zeros(len(acc_dev), bool)
         if roundoff is not None:
             chaotic = np.asarray(roundoff) > ROUNDOFF_REL
@@ -163,6 +172,7 @@ class Tally:
 
     def report(self, **extra):
         d = {"test": self.name, "decisions": self.n, "identical": self.agree,
+             "exempt_current_status_disagreement": getattr(self, "exempt_current", 0),
              "exempt_near_margin": self.exempt_margin, "exempt_status_disagreement": self.exempt_status,
              "status_pairs_device/ias15": self.status_pairs, "differing_but_exempt": self.disagree_exempt,
              "mismatches_not_exempt": len(self.mismatch), "accepted_ias15": self.accepted_ref,

@@ -119,7 +119,9 @@ def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, roundoff=F
             # the device sampler itself is exact: its decisions follow its own logL bit for bit
             np.testing.assert_array_equal(acc_dev, d_dev > np.log(u3))
             np.testing.assert_array_equal(after[h][acc_dev], q[acc_dev])
-            tally.add(acc_dev, acc_ref, margin, sq_dev, sq_ref, lq_dev, lq_ref, idx_offset=h * hk, roundoff=sens)
+            cur = np.isneginf(lnp_dev[h]) != np.isneginf(lnp_ref[h])  # (e.g. UNRESOLVED vs OK)
+            tally.add(acc_dev, acc_ref, margin, sq_dev, sq_ref, lq_dev, lq_ref, idx_offset=h * hk, roundoff=sens,
+                      current_differs=cur)
             lnp_ref[h] = np.where(acc_dev, lq_ref, lnp_ref[h])  # follow the device chain
     return tally, dict(walkers=W, ball=ball, iterations=iterations, warm_iterations=warm, speculative=bool(spec))
 
@@ -149,6 +151,7 @@ def test_stretch_vs_ias15_wide_ball_encounters():
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
     assert rep["encounters_ias15"] > 20 and rep["prior_rejections"] > 20
     assert rep["exempt_status_disagreement"] <= max(4, rep["decisions"] // 100)
+    assert rep["exempt_current_status_disagreement"] <= max(4, rep["decisions"] // 100)
     assert rep["ok_proposals_dlogl_above_margin_not_roundoff"] == 0
     assert rep["max_abs_dlogl_ok_proposals_not_roundoff"] <= T2_ABS
     assert rep["exempt_ias15_roundoff_sensitive"] <= rep["decisions"] // 100
