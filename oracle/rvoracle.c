@@ -1001,7 +1001,7 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /*   the stored levels: r5 = Richardson over all nl + 1 levels.  Accepted (chi2 from r5) when    */
 /*     sum |(r5 - o)^2 - (r - o)^2| / s2 <= EXT_ACCEPT * tol_dir * npoints                        */
 /*   -- the change of chi2 the extension brought, an estimate of the main pass's own error (and  */
-/*   a conservative one of r5's: measured, r5's error stays below 0.5 tol_dir wherever this      */
+/*   a conservative one of r5's: measured, r5's error stays below 2.6 tol_dir wherever this      */
 /*   holds);                                                                        */
 /*  stages 2..: every step halved (level k: mult 2^rf steps per base step, rf = 1..rf_max) while  */
 /*   est > tol_dir; still above after rf_max: RVO_UNRESOLVED.                                   */
@@ -1010,7 +1010,8 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /* pass's chi2) when the accept test fails even at lp_hi = -(chi2 - min(d2, CUT_EST_FACTOR est)) */
 /* / npoints, d2 = the pass's change of chi2 from the previous pass (the main pass for rf = 1),  */
 /*   d2 = sum |(r - o)^2 - (r_prev - o)^2| / s2, est the pass's estimate (both before / npoints). */
-/* An encounter or non-finite RV ends the direction at once (no refinement).                    */
+/* An encounter ends the direction at once; a non-finite RV (the fixed step blowing up on an    */
+/* extreme orbit) counts as above the bound and refines on (UNRESOLVED if it never settles).    */
 /* ------------------------------------------------------------------------------------------ */
 enum { RVO_UNRESOLVED = 4 };
 #ifndef EXT_ACCEPT /* (overridable for studies of the rule: -DEXT_ACCEPT=...) */
@@ -1058,64 +1059,81 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
     int st = RVO_OK, stage = 0;
     *cut_out = 0;
     double chi2 = 0.0, est = 0.0, margin = INFINITY;
+    const int adaptive = nl >= 2 && tol_dir < INFINITY;
     for (int rf = 0; rf <= rf_max; rf++) {
         st = RVO_OK;
         for (int k = 0; k < nl; k++) {
             const int s = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, mult[k] << rf, lv + (size_t)k * cnt);
             if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
         }
-        if (st != RVO_OK) break;
-        chi2 = 0.0;
-        est = 0.0;
-        double d2 = 0.0;
-        for (int i = 0; i < cnt; i++) {
-            double r = 0.0, r3 = 0.0;
-            for (int k = 0; k < nl; k++) r += w[k] * lv[(size_t)k * cnt + i];
-            for (int k = 1; k < nl; k++) r3 += w3[k] * lv[(size_t)k * cnt + i];
-            chi2 += (r - ob[i]) * (r - ob[i]) / s2[i];
-            est += fabs((r - r3) * ((r - ob[i]) + (r3 - ob[i]))) / s2[i];
-            if (rf > 0) d2 += fabs((r - prev[i]) * ((r - ob[i]) + (prev[i] - ob[i]))) / s2[i];
-            prev[i] = r;
-        }
-        const double est_raw = est;
-        est /= npoints;
-        if (nl >= 2 && tol_dir < INFINITY && margin_of(est, tol_dir) < margin) margin = margin_of(est, tol_dir);
-        if (nl < 2 || !(est > tol_dir)) break;
-        if (rf > 0 && ext_mult > 0 && dc != NULL && dc->mode != 0) {
-            const double lp_hi = -(chi2 - fmin(d2, CUT_EST_FACTOR * est_raw)) / npoints;
-            const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0
-                                                 : lp_hi - dc->lnp0;
-            const double lu = log(dc->u);
-            const double mg = fabs(lnpdiff - lu) / (1.0 + fabs(lu));
-            if (mg < margin) margin = mg;
-            if (!decide_accepts(dc, lp_hi)) { /* a certain reject: keep this pass */
-                *cut_out = 1;
-                break;
+        if (st == RVO_ENCOUNTER || (st != RVO_OK && !adaptive)) break;
+        /* a non-finite pass (the fixed step blowing up on an extreme orbit) refines on */
+        const int bad = st != RVO_OK;
+        st = RVO_OK;
+        if (!bad) {
+            chi2 = 0.0;
+            est = 0.0;
+            double d2 = 0.0;
+            for (int i = 0; i < cnt; i++) {
+                double r = 0.0, r3 = 0.0;
+                for (int k = 0; k < nl; k++) r += w[k] * lv[(size_t)k * cnt + i];
+                for (int k = 1; k < nl; k++) r3 += w3[k] * lv[(size_t)k * cnt + i];
+                chi2 += (r - ob[i]) * (r - ob[i]) / s2[i];
+                est += fabs((r - r3) * ((r - ob[i]) + (r3 - ob[i]))) / s2[i];
+                if (rf > 0) d2 += fabs((r - prev[i]) * ((r - ob[i]) + (prev[i] - ob[i]))) / s2[i];
+                prev[i] = r;
             }
+            const double est_raw = est;
+            est /= npoints;
+            if (nl >= 2 && tol_dir < INFINITY && margin_of(est, tol_dir) < margin) margin = margin_of(est, tol_dir);
+            if (nl < 2 || !(est > tol_dir)) break;
+            if (rf > 0 && ext_mult > 0 && dc != NULL && dc->mode != 0) {
+                const double lp_hi = -(chi2 - fmin(d2, CUT_EST_FACTOR * est_raw)) / npoints;
+                if (isfinite(lp_hi)) {
+                    const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0
+                                                         : lp_hi - dc->lnp0;
+                    const double lu = log(dc->u);
+                    const double mg = fabs(lnpdiff - lu) / (1.0 + fabs(lu));
+                    if (mg < margin) margin = mg;
+                    if (!decide_accepts(dc, lp_hi)) { /* a certain reject: keep this pass */
+                        *cut_out = 1;
+                        break;
+                    }
+                }
+            }
+        } else {
+            chi2 = NAN;
+            est = NAN;
+            for (int i = 0; i < cnt; i++) prev[i] = NAN;
         }
         if (rf == 0 && ext) {
             /* stage 1: the extension level over the main pass's stored levels */
             stage = 1;
             memcpy(lv0, lv, sizeof(double) * (size_t)nl * cnt);
             double* lx = lv + (size_t)nl * cnt;
-            st = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, ext_mult, lx);
-            if (st != RVO_OK) break;
-            double c5 = 0.0, dd = 0.0;
-            for (int i = 0; i < cnt; i++) {
-                double r = 0.0, r5 = 0.0;
-                for (int k = 0; k < nl; k++) r += w[k] * lv0[(size_t)k * cnt + i];
-                for (int k = 0; k < nl; k++) r5 += w5[k] * lv0[(size_t)k * cnt + i];
-                r5 += w5[nl] * lx[i];
-                const double q = r5 - ob[i];
-                c5 += (q * q) / s2[i];
-                dd += fabs((r5 - r) * (q + (r - ob[i]))) / s2[i];
-            }
-            const double bx = EXT_ACCEPT * tol_dir * npoints;
-            if (margin_of(dd, bx) < margin) margin = margin_of(dd, bx);
-            if (dd <= bx) {
-                chi2 = c5;
-                est = dd / npoints;
+            const int sx = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, ext_mult, lx);
+            if (sx == RVO_ENCOUNTER) {
+                st = sx;
                 break;
+            }
+            if (sx == RVO_OK && !bad) {
+                double c5 = 0.0, dd = 0.0;
+                for (int i = 0; i < cnt; i++) {
+                    double r = 0.0, r5 = 0.0;
+                    for (int k = 0; k < nl; k++) r += w[k] * lv0[(size_t)k * cnt + i];
+                    for (int k = 0; k < nl; k++) r5 += w5[k] * lv0[(size_t)k * cnt + i];
+                    r5 += w5[nl] * lx[i];
+                    const double q = r5 - ob[i];
+                    c5 += (q * q) / s2[i];
+                    dd += fabs((r5 - r) * (q + (r - ob[i]))) / s2[i];
+                }
+                const double bx = EXT_ACCEPT * tol_dir * npoints;
+                if (margin_of(dd, bx) < margin) margin = margin_of(dd, bx);
+                if (dd <= bx) {
+                    chi2 = c5;
+                    est = dd / npoints;
+                    break;
+                }
             }
         }
         if (rf == rf_max) {

@@ -465,12 +465,15 @@ __device__ __forceinline__ constexpr double halley_tol() {
 
 template <int NT>
 __device__ __forceinline__ bool halley_ok(double q, double x) {
-    return !(fabs(q) > halley_tol<NT>() * fabs(x));
+    // (false for a NaN correction: a Halley step from a guess far outside the series' range can
+    // give one, and the lane must then take the general solver -- found when a walker near a
+    // parabolic pericentre came out NONFINITE where the oracle's solver reports the encounter)
+    return fabs(q) <= halley_tol<NT>() * fabs(x);
 }
 
-// general form (any z) for the rare solver
+// general form (any z) for the rare solver (false for NaN: the bracketed solve takes over)
 __device__ __forceinline__ bool halley_done(double q, double z, double x3) {
-    return !(fabs((q * q) * (q * z)) > 3e-17 * fabs(x3));
+    return fabs((q * q) * (q * z)) <= 3e-17 * fabs(x3);
 }
 
 // Universal-Kepler solve for the rare lanes: Halley with the full Stumpff evaluation (any z)

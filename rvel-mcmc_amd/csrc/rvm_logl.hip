@@ -1005,10 +1005,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 enc |= 1;
                 chi2w = c5;
                 need = false;
-            } else if (!isfinite(c5)) {
-                chi2w = c5;  // (NONFINITE at the direction meeting)
-                need = false;
-            } else if (dd <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
+            } else if (dd <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {  // (false for a non-finite one)
                 chi2w = c5;
                 need = false;
             }
@@ -1078,13 +1075,15 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 for (int k = 0; k < nl; k++) er |= s_enc_all[gr][k][lane];
                 chi2w = c2;
                 const double lp_hi = -(c2 - fmin(d2, RVM_CUT_EST_FACTOR * e2)) / P.npoints;
+                const bool fin = isfinite(c2) && isfinite(e2);  // (a non-finite pass refines on)
                 if (er) {
                     enc |= er;
                     need = false;
-                } else if (!(e2 / P.npoints > P.rtol_dir)) {
+                } else if (fin && !(e2 / P.npoints > P.rtol_dir)) {
                     need = false;
-                } else if (dmode == 1 ? !stretch_accepts(sa.dim, dz, lp_hi, dl, du)
-                                      : (dmode == 2 && !mh_accepts(lp_hi, dl, du))) {
+                } else if (fin && isfinite(lp_hi) &&
+                           (dmode == 1 ? !stretch_accepts(sa.dim, dz, lp_hi, dl, du)
+                                       : (dmode == 2 && !mh_accepts(lp_hi, dl, du)))) {
                     cut = true;  // a certain reject
                     need = false;
                 } else if (rf == P.rmax) {
@@ -1117,7 +1116,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
         double chi2w = chi2;
         if (P.rtol_dir < INFINITY) {  // (kernel argument: uniform)
-            bool need = cmb && wo < W && enc == 0 && est / P.npoints > P.rtol_dir;
+            // (a non-finite chi2 -- the fixed step blowing up on an extreme orbit -- refines too)
+            bool need = cmb && wo < W && enc == 0 && (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est));
             if (P.rmax == 0) {
                 if (need) enc |= RVM_ENC_UNRESOLVED;
             } else {
@@ -1297,7 +1297,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             const unsigned long long rt_arr = __builtin_amdgcn_s_memrealtime();
 #endif
             // adaptive resolution: finish now, or leave the unit to the refinement team
-            bool need = P.rtol_dir < INFINITY && valid && pl_idx == 0 && enc == 0 && est / P.npoints > P.rtol_dir;
+            bool need = P.rtol_dir < INFINITY && valid && pl_idx == 0 && enc == 0 &&
+                        (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est));
             if (need && P.rmax == 0) {
                 enc |= RVM_ENC_UNRESOLVED;
                 need = false;

@@ -10,7 +10,7 @@ R=$PWD
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+  RVM_PARITY_REPORT=gpurun_out/parity_ias15.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
   tail -2 gpurun_out/pytest_gpu.log
   timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
 fi

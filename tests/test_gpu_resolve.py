@@ -285,3 +285,40 @@ def test_certain_reject_cut_matches_oracle(W):
         acc = (s.Nvars - 1.0) * np.log(z) + got - lnp0 > np.log(u3)
     np.testing.assert_array_equal(np.any(after != before, axis=1), acc)
     assert not np.any(acc & np.any(cut == 1, axis=1) & ~sensitive)
+
+
+def test_near_parabolic_pericentre_reports_the_encounter():
+    """Regression (found when the samplers began raising on NONFINITE, HD155358 posterior run):
+    two affine proposals whose outer planet has e = 0.98 / 0.93 (pericentre inside the inner
+    planet's orbit, within exit_min_distance of the star) came out NONFINITE: a Halley step from a
+    guess far outside the Stumpff series' range gave a NaN correction, which the acceptance test
+    let through.  The oracle's solver, and IAS15, report the encounter; so must the kernel, with the
+    adaptive resolution off and on."""
+    from conftest import hd_obs_oracle
+    from rvmcmc import engine
+
+    obs = hd_obs_oracle()
+    # free parameters a, h, k, m, l per planet ((Ex)HD155358.ipynb order)
+    Q = np.array([[0.6657403462735857, -0.03598508261780334, -0.22616251032911833, 0.001067427963625652,
+                   4.809278256084164, 1.0225890089859921, 0.5008569502269338, 0.839486028623608,
+                   0.000508558297134821, 1.813555010417457],
+                  [0.6674899135343648, -0.09193415567815766, 0.3058258300122595, 0.000628834189154814,
+                   5.562596065758877, 1.0267865106849083, -0.8167984417091974, 0.45176536412785595,
+                   0.0008402837623474788, 1.4987361800115173]])
+    P = np.zeros((len(Q), 2, 7))
+    for p in range(2):
+        a, h, k, m, l = Q[:, 5 * p:5 * p + 5].T
+        P[:, p, :5] = np.stack([m, a, h, k, l], 1)
+    sol = [{"m": 8.84031737e-04, "a": 6.57730330e-01, "h": -9.72263877e-02, "k": -7.82798396e-02, "l": 4.42804990},
+           {"m": 8.30379710e-04, "a": 1.04404207, "h": -2.05622789e-02, "k": -1.08797961e-01, "l": 1.49919861}]
+    dt, mult, hint = engine.IntegratorConfig().plan_args(sol)
+    t, rv, er = engine.obs_arrays(obs)
+    _, st_ref = O.logl_whx_batch(P, 2, obs, dt, mult)
+    _, st_ias = O.logl_ias15_batch(P, 2, obs)
+    assert st_ref.tolist() == [2, 2] and st_ias.tolist() == [2, 2]
+    K = np.concatenate([P[:, p, :5].T for p in range(2)], 0)
+    for res in [(0.0, 0), engine.IntegratorConfig().resolve()]:
+        plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, 64, period_hint=hint, resolve=res)
+        _, st = _run(plan, K.T)
+        assert st.tolist() == [2, 2], (res, st)
+        assert plan.faults()["nonfinite"] == 0
