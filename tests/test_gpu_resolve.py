@@ -287,17 +287,16 @@ def test_certain_reject_cut_matches_oracle(W):
     assert not np.any(acc & np.any(cut == 1, axis=1) & ~sensitive)
 
 
-def test_near_parabolic_pericentre_reports_the_encounter():
+def test_near_parabolic_pericentre_reports_the_encounter(hd_obs_oracle):
     """Regression (found when the samplers began raising on NONFINITE, HD155358 posterior run):
     two affine proposals whose outer planet has e = 0.98 / 0.93 (pericentre inside the inner
     planet's orbit, within exit_min_distance of the star) came out NONFINITE: a Halley step from a
     guess far outside the Stumpff series' range gave a NaN correction, which the acceptance test
     let through.  The oracle's solver, and IAS15, report the encounter; so must the kernel, with the
     adaptive resolution off and on."""
-    from conftest import hd_obs_oracle
     from rvmcmc import engine
 
-    obs = hd_obs_oracle()
+    obs = hd_obs_oracle
     # free parameters a, h, k, m, l per planet ((Ex)HD155358.ipynb order)
     Q = np.array([[0.6657403462735857, -0.03598508261780334, -0.22616251032911833, 0.001067427963625652,
                    4.809278256084164, 1.0225890089859921, 0.5008569502269338, 0.839486028623608,
