@@ -109,8 +109,9 @@ int rvm_plan_info(const rvm_plan* plan, int32_t* steps_fwd, int32_t* steps_bwd, 
                   int32_t* epochs_bwd);
 /* The adaptive resolution's extension level of a plan: *ext_mult = its steps per base step
  * (max(level_mult) + 1), or 0 when the plan has none -- resolution off or flag-only, n_levels < 2 or
- * = RVM_MAX_LEVELS, or its stored levels (8 * n_levels * 2 * max(epochs per direction) * max_walkers
- * bytes of device memory, written by every launch) above RVM_EXT_MAX_BYTES. */
+ * = RVM_MAX_LEVELS, or its stored main-pass values (2 doubles per direction, epoch and walker:
+ * 32 * max(epochs per direction) * max_walkers bytes of device memory, written by every launch)
+ * above RVM_EXT_MAX_BYTES. */
 #define RVM_EXT_MAX_BYTES (4ull << 30)
 int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult);
 

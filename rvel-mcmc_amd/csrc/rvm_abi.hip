@@ -344,8 +344,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     if (P.rmax > 0 && cfg->n_levels >= 2 && cfg->n_levels < RVM_MAX_LEVELS) {
         const int nl = cfg->n_levels;
         const size_t emax = std::max<size_t>(std::max(nf, nb), 1);
-        const size_t bl = 2 * emax * (size_t)nl * (size_t)max_walkers * sizeof(double);  // levels
-        const size_t bx = bl + 2 * emax * (size_t)max_walkers * sizeof(double);         // + last RV
+        const size_t bl = 2 * emax * (size_t)max_walkers * sizeof(double);  // partial sums
+        const size_t bx = 2 * bl;                                           // + last RV
         if (bx <= RVM_EXT_MAX_BYTES) {
             if (hipMalloc(&plan->xmem, bx) != hipSuccess) {
                 plan->xmem = nullptr;

@@ -53,9 +53,10 @@ struct DevPlan {
     double rtol_dir;   // +inf: no estimate check
     int32_t rmax;
     // the extension (stage 1, rvm_logl.hip extend_pass): one more level of ext_mult steps per base
-    // step (0: none) joined to the main pass's levels, which every launch stores in lvx
-    // [2][lvx_emax][n_levels][lvx_stride]; lw5 = the weights of all n_levels + 1 levels.  rvp
-    // [2][lvx_emax][lvx_stride]: the last pass's extrapolated RV (main pass, then each halving pass)
+    // step (0: none) joined to the main pass's levels; lw5 = the weights of all n_levels + 1 levels.
+    // Every launch keeps, per direction, epoch and walker ([2][lvx_emax][lvx_stride]), lvx = the
+    // main pass's partial sum sum_k lw5[k] rv_k and rvp = its extrapolated RV (then each halving
+    // pass's, the previous pass of the next)
     int32_t ext_mult, ext_nt, ext_spec;
     double inv_ext;
     double lw5[RVM_MAX_LEVELS + 1];

@@ -738,10 +738,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
             const int wo = w0 + lane;
             if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[e] * W + wo] = rvx;
-            if (P.ext_mult > 0 && wo < W) {  // the levels and the RV, for a later refinement
-                double* xo = P.lvx + ((size_t)(d * P.lvx_emax + e) * nl) * P.lvx_stride + wo;
-                for (int k = 0; k < nl; k++) xo[(size_t)k * P.lvx_stride] = s_rv[e & 1][k][lane];
-                P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + wo] = rvx;
+            if (P.ext_mult > 0 && wo < W) {  // the RV and the extension's partial sum, for a refinement
+                double s5 = 0.0;
+                for (int k = 0; k < nl; k++) s5 += P.lw5[k] * s_rv[e & 1][k][lane];
+                const size_t xi = (size_t)(d * P.lvx_emax + e) * P.lvx_stride + wo;
+                P.lvx[xi] = s5;
+                P.rvp[xi] = rvx;
             }
         }
         n1 = n1_next;
@@ -910,8 +912,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // ---- adaptive resolution, stage 1: the extension level ----------------------------------
     // One wave per group / unit -- its combiner wave -- integrates one more level (P.ext_mult steps
     // per base step) of direction dr from t = 0 and joins it, epoch by epoch, to the main pass's
-    // levels stored in P.lvx: r5 = all nl + 1 levels (lw5).  A marked walker (combiner lane `lane`,
-    // its bit in need_m) is settled -- chi2 from r5 -- when the extension changed chi2 by at most
+    // levels: r5 = all nl + 1 levels (lw5), formed from the main pass's partial sum over its own
+    // levels (P.lvx, sum_k lw5[k] rv_k, kept by every launch) and its RV r (P.rvp) -- two numbers per
+    // epoch and walker, the same bits as summing the levels here.  A marked walker (combiner lane
+    // `lane`, its bit in need_m) is settled -- chi2 from r5 -- when the extension changed chi2 by at most
     // sum |(r5-o)^2 - (r-o)^2| / s2 <= RVM_EXT_ACCEPT rtol_dir npoints (r = the main pass's RV); an
     // encounter of the extension ends it ENCOUNTER, a non-finite one NONFINITE; otherwise the
     // halving passes follow.  One wave, no barrier: each epoch's value
@@ -946,18 +950,16 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const int cs = lane & (WPB - 1);  // combiner lane -> walker slot
         const bool cl = lane < WPB && ((need_m >> lane) & 1);
         const int wo = w0 + cs;
-        const double* xs = P.lvx + (size_t)dr * P.lvx_emax * nl * P.lvx_stride + (cl ? wo : 0);
-        double a[RVM_MAX_LEVELS];
-#pragma unroll
-        for (int k = 0; k < RVM_MAX_LEVELS; k++) a[k] = cl && k < nl && Er > 0 ? xs[(size_t)k * P.lvx_stride] : 0.0;
+        const size_t xb = (size_t)dr * P.lvx_emax * P.lvx_stride + (cl ? wo : 0);
+        const double* xs = P.lvx + xb;
+        const double* xr = P.rvp + xb;
+        double a5 = cl && Er > 0 ? xs[0] : 0.0, a4 = cl && Er > 0 ? xr[0] : 0.0;
         double c5 = 0.0, dd = 0.0;
         int x_off = 0, x_bo = 4;  // speculation back-off (as the main pass's spec_off / spec_bo)
         for (int e = 0; e < Er; e++) {
-            double b[RVM_MAX_LEVELS];
             const bool nx = cl && e + 1 < Er;
-#pragma unroll
-            for (int k = 0; k < RVM_MAX_LEVELS; k++)
-                b[k] = nx && k < nl ? xs[((size_t)(e + 1) * nl + k) * P.lvx_stride] : 0.0;
+            const double b5 = nx ? xs[(size_t)(e + 1) * P.lvx_stride] : 0.0;
+            const double b4 = nx ? xr[(size_t)(e + 1) * P.lvx_stride] : 0.0;
             const int ns = r_n[e] * mx;
             if (ns > 0) {
                 const double h = r_len[e] * ix;
@@ -983,21 +985,15 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             const double v = star_vx<NP, L>(s);
             const double vx = __shfl(v, cs * L);
             if (cl) {
-                double r = 0.0, r5 = 0.0;
-#pragma unroll
-                for (int k = 0; k < RVM_MAX_LEVELS; k++)
-                    if (k < nl) r += P.lw[k] * a[k];
-#pragma unroll
-                for (int k = 0; k < RVM_MAX_LEVELS; k++)
-                    if (k < nl) r5 += P.lw5[k] * a[k];
-                r5 += P.lw5[nl] * vx;
+                const double r = a4;
+                const double r5 = a5 + P.lw5[nl] * vx;
                 const double q = r5 - r_rv[e];
                 c5 += (q * q) / r_s2[e];
                 dd += fabs((r5 - r) * (q + (r - r_rv[e]))) / r_s2[e];
                 if (rv_out != nullptr && wo < W) rv_out[(size_t)r_idx[e] * W + wo] = r5;
             }
-#pragma unroll
-            for (int k = 0; k < RVM_MAX_LEVELS; k++) a[k] = b[k];
+            a5 = b5;
+            a4 = b4;
         }
         const bool xenc = ((s.encm >> (cs * L)) & kick_enc_bits<NP>()) != 0;
         if (cl && need) {
@@ -1260,11 +1256,13 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 chi2w += (r * r) / l_s2[e];
                 est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
                 if (rv_out != nullptr && valid && pl_idx == 0) rv_out[(size_t)l_idx[e] * W + w] = rvx;
-                if (P.ext_mult > 0 && valid && pl_idx == 0) {  // the levels and the RV, for a refinement
-                    double* xo = P.lvx + ((size_t)(d * P.lvx_emax + e) * 4) * P.lvx_stride + w;
+                if (P.ext_mult > 0 && valid && pl_idx == 0) {  // the RV and the extension's partial sum
+                    double s5 = 0.0;
 #pragma unroll
-                    for (int k = 0; k < 4; k++) xo[(size_t)k * P.lvx_stride] = v[k];
-                    P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = rvx;
+                    for (int k = 0; k < 4; k++) s5 += P.lw5[k] * v[k];
+                    const size_t xi = (size_t)(d * P.lvx_emax + e) * P.lvx_stride + w;
+                    P.lvx[xi] = s5;
+                    P.rvp[xi] = rvx;
                 }
                 if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 rr = rr + 1 == RING ? 0 : rr + 1;

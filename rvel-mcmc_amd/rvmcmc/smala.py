@@ -49,7 +49,18 @@ def fd_logp_grad_metric(state, obs, X, rel_step=FD_REL_STEP, pmap=None, hill_fac
     stencil = torch.empty((P, S * C_), dtype=torch.float64, device=X.device)
     _lib.check(lib.rvm_fd_params(P, C_, X.contiguous().data_ptr(), float(rel_step), fl.data_ptr(),
                                  stencil.data_ptr(), _lib.stream_handle()), "rvm_fd_params")
-    lp, st, rv = state.get_logp_batch(obs, stencil, hill_factor=hill_factor, want_rv=True, pmap=pmap)
+    # the stencil on the fixed-step plan (every point of a chain with the same steps:
+    # SmalaChains._fixed_plan), the centres' logp from the adaptive one
+    it = state.integrator
+    dt, mult, hint = it.plan_args(state.planets)
+    plan = engine.plan_for(obs, len(state.planets), dt, mult, S * C_, X.device, hint, engine.is_inclined(state.planets),
+                           (0.0, 0))
+    hf = state.hillRadiusFactor if hill_factor is None else hill_factor
+    lp, st, rv = plan.logl(pmap.to_kernel(stencil), hill_factor=hf, want_rv=True)
+    if it.resolve()[0] > 0.0:
+        lpc, stc, _ = state.get_logp_batch(obs, X.contiguous(), hill_factor=hill_factor, pmap=pmap)
+        lp[:C_].copy_(lpc)
+        st[:C_].copy_(stc)
     lp = lp.view(S, C_)
     st = st.view(S, C_)
     rv = rv.view(-1, S, C_)
@@ -132,17 +143,42 @@ class SmalaChains:
         d["_c"] = _lib.SmalaCache(*[d[k].data_ptr() for k in ("lp", "grad", "mu", "L", "G", "logdet", "ok")])
         return d
 
+    def _fixed_plan(self, max_walkers):
+        """The plan of the stencil's neighbour points: the state's integrator with the adaptive
+        resolution off.  Finite differences need every point of a chain's stencil integrated with
+        the same steps -- a refinement of some points but not others (per-walker decisions) would
+        put the resolution's change, up to the bound, into the difference quotient -- and the
+        gradient and metric only shape the proposal (the MH test keeps the target exact); the
+        chain's logp itself comes from the adaptive plan (_center_logl)."""
+        it = self.state.integrator
+        dt, mult, hint = it.plan_args(self.state.planets)
+        return engine.plan_for(self.obs, len(self.state.planets), dt, mult, max_walkers, self.device, hint,
+                               engine.is_inclined(self.state.planets), (0.0, 0))
+
+    def _center_logl(self, X, lp, st):
+        """Overwrite the stencil centres' logp / status (walkers 0 .. C-1) with the adaptive plan's
+        (T2: the value the accept test uses)."""
+        if self.state.integrator.resolve()[0] <= 0.0:
+            return
+        lpc, stc, _ = self.state.get_logp_batch(self.obs, X, hill_factor=1.0, pmap=self.pmap)
+        lp[:self.n].copy_(lpc)
+        st[:self.n].copy_(stc)
+
     def _stencil_logl(self, X, fused=True):
         """logp, status [(2P+1) C] and model RVs [n_obs][(2P+1) C] over the central-difference
         stencil of X: one launch that forms the stencil in the likelihood kernel's prologue
-        (rvm_smala_stencil_logl), or rvm_fd_params + rvm_logl_batch (fused=False; same bits)."""
+        (rvm_smala_stencil_logl), or rvm_fd_params + rvm_logl_batch (fused=False; same bits), both
+        on the fixed-step plan (_fixed_plan); the centres' logp then from the adaptive plan."""
         torch = _torch()
+        S = 2 * self.P + 1
+        plan = self._fixed_plan(S * self.n)
         if not fused:
             _lib.check(self.lib.rvm_fd_params(self.P, self.n, X.data_ptr(), self.rel_step, self.floor.data_ptr(),
                                               self.stencil.data_ptr(), _lib.stream_handle()), "rvm_fd_params")
-            return self.state.get_logp_batch(self.obs, self.stencil, hill_factor=1.0, want_rv=True, pmap=self.pmap)
-        S = 2 * self.P + 1
-        plan = self.state._plan(self.obs, max_walkers=S * self.n, device=self.device)
+            lp, st, rv = plan.logl(self.pmap.to_kernel(self.stencil), hill_factor=1.0, want_rv=True)
+            self._plan_keep = plan
+            self._center_logl(X, lp, st)
+            return lp, st, rv
         if getattr(self, "_st_bufs", None) is None:
             self._st_bufs = (torch.empty(S * self.n, dtype=torch.float64, device=self.device),
                              torch.empty(S * self.n, dtype=torch.int32, device=self.device),
@@ -154,12 +190,14 @@ class SmalaChains:
                                                        lp.data_ptr(), st.data_ptr(), rv.data_ptr(),
                                                        _lib.stream_handle()), "rvm_smala_stencil_logl")
         self._plan_keep = plan  # the launch's plan stays alive with the sampler
+        self._center_logl(X, lp, st)
         return lp, st, rv
 
     def _derive_into(self, X, cache, fused=True):
         st_h = _lib.stream_handle()
         if self.hessian == "exact":
             lp, g, H, st = self.state.get_logp_d_dd_batch(self.obs, X, hill_factor=1.0, pmap=self.pmap)
+            self._center_logl(X, lp, st)
             _lib.check(self.lib.rvm_smala_metric(self.P, self.n, X.data_ptr(), lp.data_ptr(), st.data_ptr(),
                                                  g.data_ptr(), H.data_ptr(), self.alpha, self.eps,
                                                  C.byref(cache["_c"]), st_h), "rvm_smala_metric")
@@ -218,6 +256,7 @@ class SmalaChains:
         cur, prop = C.byref(self.cache["_c"]), C.byref(self.prop["_c"])
         if fused and self.hessian == "exact":
             lp, g, H, st = self.state.get_logp_d_dd_batch(self.obs, self.Xs, hill_factor=1.0, pmap=self.pmap)
+            self._center_logl(self.Xs, lp, st)  # (the logp the accept uses: adaptive resolution)
             _lib.check(self.lib.rvm_smala_metric_accept(self.P, self.n, 0, self.X.data_ptr(), self.Xs.data_ptr(),
                                                         lp.data_ptr(), st.data_ptr(), g.data_ptr(), H.data_ptr(),
                                                         self.alpha, self.eps, cur, prop, self.seed, self.iteration,
@@ -225,7 +264,7 @@ class SmalaChains:
                                                         st_h), "rvm_smala_metric_accept")
             self._keep = (lp, g, H, st)
             self.iteration += 1
-            engine.periodic_fault_check(self, self._fault_plan())
+            self._periodic_faults()
             return
         if fused:
             lp, st, rv = self._stencil_logl(self.Xs)
@@ -235,7 +274,7 @@ class SmalaChains:
                 float(self.obs.Npoints), self.alpha, self.eps, cur, prop, self.seed, self.iteration, up,
                 self.accepted.data_ptr(), self.failures.data_ptr(), st_h), "rvm_smala_derive_accept")
             self.iteration += 1
-            engine.periodic_fault_check(self, self._fault_plan())
+            self._periodic_faults()
             return
         self._derive_into(self.Xs, self.prop, fused=False)
         _lib.check(self.lib.rvm_smala_accept(self.P, self.n, 0, self.X.data_ptr(), C.byref(self.cache["_c"]),
@@ -243,13 +282,20 @@ class SmalaChains:
                                              self.iteration, up, self.accepted.data_ptr(), self.failures.data_ptr(),
                                              st_h), "rvm_smala_accept")
         self.iteration += 1
-        engine.periodic_fault_check(self, self._fault_plan())
+        self._periodic_faults()
 
     def _fault_plan(self):
         return self.state._plan(self.obs, max_walkers=(2 * self.P + 1) * self.n, device=self.device)
 
+    def _periodic_faults(self):  # (engine.periodic_fault_check over both plans)
+        every = getattr(self, "fault_check_every", engine.FAULT_CHECK_EVERY)
+        if every and self.iteration % every == 0:
+            self.check_faults()
+
     def check_faults(self):
-        """rvm_plan_faults of the chains' plan: raises on hand-off timeouts / NONFINITE results."""
+        """rvm_plan_faults of the chains' plans (adaptive, and the stencil's fixed-step one): raises on
+        hand-off timeouts / NONFINITE results; returns the adaptive plan's counters."""
+        self._fixed_plan((2 * self.P + 1) * self.n).check_faults(type(self).__name__)
         self.last_faults = self._fault_plan().check_faults(type(self).__name__)
         return self.last_faults
 
