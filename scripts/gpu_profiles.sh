@@ -24,7 +24,7 @@ cat gpurun_out/bench.json
 # the N > 1 flow of bench.py (2 ranks on this one GPU over gloo: correctness, not scaling)
 bash scripts/gpu_rehearse_dist.sh > /dev/null
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 --ess-iters 0 --no-cpu > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 10 --warmup 2 --ess-iters 0 --no-cpu --no-fixed-step-ref > "$R/gpurun_out/prof_bench.json" 2> "$R/gpurun_out/prof_bench.err"
 cd "$R"
 find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats.csv \;
 cat gpurun_out/kernel_stats.csv | cut -c1-200

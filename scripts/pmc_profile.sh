@@ -18,7 +18,7 @@ TARGET=${PMC_TARGET:-bench}
 for grp in "${GRPS[@]}"; do
   i=$((i+1))
   if [ "$TARGET" = "bench" ]; then
-    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc/p$i" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --ess-iters 0 --kernel-iters 0 --no-cpu > "$R/gpurun_out/pmc/p$i.log" 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc/p$i" -o run --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --ess-iters 0 --kernel-iters 0 --no-cpu --no-fixed-step-ref > "$R/gpurun_out/pmc/p$i.log" 2>&1
   else
     timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp -d "$R/gpurun_out/pmc/p$i" -o run --output-format csv -- python3 "$R/scripts/kbench.py" ${PMC_W:-2048} > "$R/gpurun_out/pmc/p$i.log" 2>&1
   fi
