@@ -36,9 +36,16 @@ ST_OK, ST_PRIOR, ST_ENC = 0, 1, 2
 def n_threads():
     """The CPUs this process may run on (the GPU box's share; os.cpu_count() is the whole machine)."""
     try:
-        return max(1, len(os.sched_getaffinity(0)))
+        n = max(1, len(os.sched_getaffinity(0)))
     except (AttributeError, OSError):
-        return max(1, os.cpu_count() or 1)
+        n = max(1, os.cpu_count() or 1)
+    # the GPU box exports its CPU share as OMP_NUM_THREADS (16 per GPU) while the affinity mask
+    # covers the whole machine: the smaller of the two
+    try:
+        n = min(n, max(1, int(os.environ.get("OMP_NUM_THREADS", n))))
+    except ValueError:
+        pass
+    return n
 
 
 def ias15_logl(P, n_planets, obs, hill=1.0, has_inc=0):
