@@ -114,6 +114,11 @@ int rvm_plan_info(const rvm_plan* plan, int32_t* steps_fwd, int32_t* steps_bwd, 
  * above RVM_EXT_MAX_BYTES. */
 #define RVM_EXT_MAX_BYTES (4ull << 30)
 int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult);
+/* Eccentricity guard of the adaptive resolution (plans with an extension level): a walker with a
+ * planet of eccentricity above e counts as above the bound after the main pass whatever its
+ * estimate, so the extension verifies it -- the estimate under-reads on orbits whose pericentre
+ * passage is much quicker than the plan's reference orbit.  e <= 0: off (default). */
+int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e);
 
 /* Counters of a plan since its creation or the last reset, read in order on `stream` (the call
  * synchronises that stream; any output pointer may be NULL):

@@ -73,7 +73,7 @@ def lib():
                                              C.POINTER(C.c_int32)]
         L.rvo_logl_whx_adapt_batch.argtypes = [C.c_int, C.c_int, dp, C.c_int, C.c_int, C.c_double, dp, dp, dp,
                                                C.c_int, C.c_double, C.c_double, C.c_int, ip, C.c_int, C.c_double, C.c_int,
-                                               C.POINTER(C.c_int32), C.c_int, dp, dp, dp,
+                                               C.POINTER(C.c_int32), C.c_int, dp, dp, dp, C.c_double,
                                                dp, C.POINTER(C.c_int32), C.POINTER(C.c_int32), dp,
                                                C.POINTER(C.c_int32)]
         _LIB = L
@@ -251,7 +251,7 @@ def ext_multiplier(mult, rf_max):
 
 
 def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.0, has_hk=1, has_inc=0, ext=None,
-                         ctx=None):
+                         ctx=None, ecc_guard=0.0):
     """The kernel's algorithm with adaptive resolution (rvm_config.resolve_tol / resolve_max):
     a direction whose extrapolation-error estimate exceeds tol / 2 gets the extension level (ext
     steps per base step; default ext_multiplier) and, if that does not settle it, passes with every
@@ -261,7 +261,9 @@ def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.
     closest any decision came to its bound, min |x/bound - 1| (a decision at roundoff distance may
     go the other way in a second implementation).  tol = 0 is the plain rvo_whx algorithm.
     ctx = dict(mode [W] (0 none, 1 emcee stretch, 2 MH), dim, z [W], u [W], lnp0 [W]): the sampler's
-    accept inputs of each walker, for the certain-reject cut; then a sixth result, cut [W][2]."""
+    accept inputs of each walker, for the certain-reject cut; then a sixth result, cut [W][2].
+    ecc_guard > 0: walkers with a planet of eccentricity above it always get the extension
+    (rvm_plan_set_verify_eccentricity)."""
     pl = _f64(params)
     W = pl.shape[0]
     t = _f64(np.concatenate([obs.tf, obs.tb]))
@@ -284,7 +286,8 @@ def logl_whx_adapt_batch(params, np_, obs, dt, mult, tol, rf_max, hill_factor=1.
         cargs = (None, 0, None, None, None)
     lib().rvo_logl_whx_adapt_batch(W, np_, _p(pl), has_hk, has_inc, float(hill_factor), _p(t), _p(rv), _p(er),
                                    len(t), float(obs.Npoints), float(dt), len(m), mp, ext, tol_dir, int(rf_max),
-                                   *cargs, _p(out), st.ctypes.data_as(ip32), rf.ctypes.data_as(ip32), _p(est),
+                                   *cargs, float(ecc_guard), _p(out), st.ctypes.data_as(ip32),
+                                   rf.ctypes.data_as(ip32), _p(est),
                                    cut.ctypes.data_as(ip32))
     if ctx is not None:
         return out, st, rf, est[:, :2], est[:, 2:], cut

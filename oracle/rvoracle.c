@@ -1010,6 +1010,8 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /* pass's chi2) when the accept test fails even at lp_hi = -(chi2 - min(d2, CUT_EST_FACTOR est)) */
 /* / npoints, d2 = the pass's change of chi2 from the previous pass (the main pass for rf = 1),  */
 /*   d2 = sum |(r - o)^2 - (r_prev - o)^2| / s2, est the pass's estimate (both before / npoints). */
+/* ecc_guard > 0: a walker with a planet of e > ecc_guard counts as above the bound after the    */
+/* main pass whatever its estimate (it gets the extension; the estimate under-reads there).     */
 /* An encounter ends the direction at once; a non-finite RV (the fixed step blowing up on an    */
 /* extreme orbit) counts as above the bound and refines on (UNRESOLVED if it never settles).    */
 /* ------------------------------------------------------------------------------------------ */
@@ -1040,8 +1042,8 @@ static int decide_accepts(const rvo_decide* dc, double lp) {
 
 static int whx_direction_adapt(int np, const double* pl, double hill_factor, const double* at, const double* ob,
                                const double* s2, int cnt, double sign, double dt, int nl, const int* mult, int ext_mult,
-                               double tol_dir, int rf_max, double npoints, const rvo_decide* dc, double* chi2_out,
-                               int* stage_out, double* est_out, double* margin_out, int* cut_out) {
+                               double tol_dir, int rf_max, double npoints, const rvo_decide* dc, double ecc_guard,
+                               double* chi2_out, int* stage_out, double* est_out, double* margin_out, int* cut_out) {
     double w[8], w3[8], w5[9];
     rvo_richardson_weights_seq(nl, mult, w);
     w3[0] = 0.0;
@@ -1086,7 +1088,19 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
             const double est_raw = est;
             est /= npoints;
             if (nl >= 2 && tol_dir < INFINITY && margin_of(est, tol_dir) < margin) margin = margin_of(est, tol_dir);
-            if (nl < 2 || !(est > tol_dir)) break;
+            /* the eccentricity guard: an orbit whose pericentre passage is much quicker than the
+             * plan's reference orbit always gets the extension (the estimate can miss there) */
+            int eflag = 0;
+            if (rf == 0 && ext && ecc_guard > 0.0) {
+                double e2 = 0.0;
+                for (int p = 0; p < np; p++) {
+                    const double h = pl[p * RVO_PSTRIDE + 2], k = pl[p * RVO_PSTRIDE + 3];
+                    if (h * h + k * k > e2) e2 = h * h + k * k;
+                }
+                eflag = e2 > ecc_guard * ecc_guard;
+                if (margin_of(e2, ecc_guard * ecc_guard) < margin) margin = margin_of(e2, ecc_guard * ecc_guard);
+            }
+            if (nl < 2 || (!(est > tol_dir) && !eflag)) break;
             if (rf > 0 && ext_mult > 0 && dc != NULL && dc->mode != 0) {
                 const double lp_hi = -(chi2 - fmin(d2, CUT_EST_FACTOR * est_raw)) / npoints;
                 if (isfinite(lp_hi)) {
@@ -1161,7 +1175,7 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
 int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
                        const double* rvobs, const double* err, int n, double npoints, double dt, int nl,
                        const int* mult, int ext_mult, double tol_dir, int rf_max, const rvo_decide* dc,
-                       double* logl, int32_t* rf_used, double* est, int32_t* cut) {
+                       double ecc_guard, double* logl, int32_t* rf_used, double* est, int32_t* cut) {
     rf_used[0] = rf_used[1] = 0;
     cut[0] = cut[1] = 0;
     est[0] = est[1] = 0.0;
@@ -1198,7 +1212,8 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
         double e = 0.0, mg = INFINITY;
         if (cnt)
             sd[dir] = whx_direction_adapt(np, pl, hill_factor, at, ob, s2, cnt, dir == 0 ? 1.0 : -1.0, dt, nl, mult,
-                                          ext_mult, tol_dir, rf_max, npoints, dc, &chi2[dir], &rf, &e, &mg, &ct);
+                                          ext_mult, tol_dir, rf_max, npoints, dc, ecc_guard, &chi2[dir], &rf, &e, &mg,
+                                          &ct);
         cut[dir] = ct;
         rf_used[dir] = rf;
         est[dir] = e;
@@ -1217,11 +1232,12 @@ void rvo_logl_whx_adapt_batch(int W, int np, const double* pl, int has_hk, int h
                               const double* t, const double* rvobs, const double* err, int n, double npoints,
                               double dt, int nl, const int* mult, int ext_mult, double tol_dir, int rf_max,
                               const int32_t* dmode, int dim, const double* dz, const double* du, const double* dlnp0,
-                              double* logl, int32_t* status, int32_t* rf_used, double* est, int32_t* cut) {
+                              double ecc_guard, double* logl, int32_t* status, int32_t* rf_used, double* est,
+                              int32_t* cut) {
     for (int w = 0; w < W; w++) {
         rvo_decide dc = {dmode ? dmode[w] : 0, dim, dz ? dz[w] : 1.0, du ? du[w] : 0.5, dlnp0 ? dlnp0[w] : 0.0};
         status[w] = rvo_logl_whx_adapt(np, pl + (size_t)w * np * RVO_PSTRIDE, has_hk, has_inc, hill_factor, t, rvobs,
-                                       err, n, npoints, dt, nl, mult, ext_mult, tol_dir, rf_max, &dc, logl + w,
+                                       err, n, npoints, dt, nl, mult, ext_mult, tol_dir, rf_max, &dc, ecc_guard, logl + w,
                                        rf_used + 2 * w, est + 4 * w, cut + 2 * w);
     }
 }

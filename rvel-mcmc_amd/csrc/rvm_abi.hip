@@ -337,6 +337,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.inv_ext = 1.0;
     P.lvx = nullptr;
     P.rvp = nullptr;
+    P.e2_guard = INFINITY;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
     P.ext_spec = 0;
@@ -393,6 +394,13 @@ void rvm_plan_destroy(rvm_plan* plan) {
     if (plan->xmem) (void)hipFree(plan->xmem);
     if (plan->dmem) (void)hipFree(plan->dmem);
     delete plan;
+}
+
+int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e) {
+    if (!plan) return fail(-1, "rvm_plan_set_verify_eccentricity: null plan");
+    if (std::isnan(e) || e >= 1.0) return fail(-1, "rvm_plan_set_verify_eccentricity: e must be < 1 (<= 0: off)");
+    plan->dev.e2_guard = e > 0.0 ? e * e : INFINITY;
+    return 0;
 }
 
 int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult) {

@@ -62,6 +62,9 @@ struct DevPlan {
     double lw5[RVM_MAX_LEVELS + 1];
     double* lvx;
     double* rvp;
+    // eccentricity guard (rvm_plan_set_verify_eccentricity; +inf: off): a walker with a planet of
+    // e^2 above it counts as above the bound after the main pass (it gets the extension)
+    double e2_guard;
     int32_t lvx_emax, lvx_stride;
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,

@@ -400,6 +400,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         if constexpr (D3) bad = bad || !(pix[p] * pix[p] + piy[p] * piy[p] < 4.0);  // state.py:311-313
         if (bad) status = RVM_STATUS_PRIOR;
     }
+    // the adaptive resolution's eccentricity guard (P.e2_guard): the walker's largest e^2
+    double e2w = 0.0;
+#pragma unroll
+    for (int p = 0; p < NP; p++) e2w = fmax(e2w, ph[p] * ph[p] + pk[p] * pk[p]);
     PROF_T(t_p1);  // parameters read, prior checked
     if (status != RVM_STATUS_OK) {  // keep the lane numerically benign; its result is discarded
 #pragma unroll
@@ -1112,8 +1116,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
         double chi2w = chi2;
         if (P.rtol_dir < INFINITY) {  // (kernel argument: uniform)
-            // (a non-finite chi2 -- the fixed step blowing up on an extreme orbit -- refines too)
-            bool need = cmb && wo < W && enc == 0 && (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est));
+            // (a non-finite chi2 -- the fixed step blowing up on an extreme orbit -- refines too, and
+            // so does a walker past the eccentricity guard: its e^2 from the walker's first lane)
+            const double e2c = __shfl(e2w, (lane & (WPB - 1)) * L);
+            bool need = cmb && wo < W && enc == 0 &&
+                        (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est) ||
+                         (P.ext_mult > 0 && e2c > P.e2_guard));
             if (P.rmax == 0) {
                 if (need) enc |= RVM_ENC_UNRESOLVED;
             } else {
@@ -1296,7 +1304,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #endif
             // adaptive resolution: finish now, or leave the unit to the refinement team
             bool need = P.rtol_dir < INFINITY && valid && pl_idx == 0 && enc == 0 &&
-                        (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est));
+                        (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est) ||
+                         (P.ext_mult > 0 && e2w > P.e2_guard));
             if (need && P.rmax == 0) {
                 enc |= RVM_ENC_UNRESOLVED;
                 need = false;

@@ -83,6 +83,7 @@ SIGNATURES = {
                                   C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64), _dp]),
     "rvm_plan_set_handoff_timeout": (C.c_int, [C.c_void_p, C.c_double]),
     "rvm_plan_extension": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    "rvm_plan_set_verify_eccentricity": (C.c_int, [C.c_void_p, C.c_double]),
     "rvm_plan_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                 C.POINTER(C.c_int32)]),
     "rvm_logl_batch": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_double, _dp, _dp, _dp, _dp]),

@@ -65,6 +65,12 @@ class IntegratorConfig:
     # off (the round-2 fixed-step algorithm).
     resolve_tol: float = 5e-7
     resolve_max: int = 4
+    # eccentricity guard (rvm_plan_set_verify_eccentricity): walkers whose pericentre passage is more
+    # than this factor quicker than the plan's reference orbit's always get the extension -- the
+    # estimate under-read on such orbits (all three T2 misses it left at the bench chain's steady
+    # state had e >= 0.295 against the reference's 0.218; the guard at 1.1 -> e > 0.266 removes them,
+    # DESIGN.md §3).  0: off.
+    verify_speedup: float = 1.1
 
     @property
     def mult(self) -> tuple:
@@ -84,9 +90,19 @@ class IntegratorConfig:
         raw = min_period(planets) / float(self.steps_per_orbit)
         return 2.0 ** (round(math.log2(raw) * DT_GRID) / DT_GRID)
 
-    def resolve(self) -> tuple:
-        """(resolve_tol, resolve_max) for plan_for / LoglPlan."""
-        return float(self.resolve_tol), int(self.resolve_max)
+    def resolve(self, planets=None) -> tuple:
+        """(resolve_tol, resolve_max, eccentricity guard) for plan_for / LoglPlan; the guard (0: off)
+        from the plan's reference planets: the eccentricity whose pericentre passage is
+        verify_speedup times quicker, (1 - e)^-3/2 = verify_speedup (1 - e_ref)^-3/2."""
+        return float(self.resolve_tol), int(self.resolve_max), self.ecc_guard(planets)
+
+    def ecc_guard(self, planets) -> float:
+        if not planets or not (self.verify_speedup > 0.0) or not (self.resolve_tol > 0.0):
+            return 0.0
+        e_ref = max(float(np.hypot(p.get("h", 0.0), p.get("k", 0.0))) for p in planets)
+        if not e_ref < 1.0:
+            return 0.0
+        return float(1.0 - (self.verify_speedup * (1.0 - e_ref) ** -1.5) ** (-2.0 / 3.0))
 
     def plan_args(self, planets):
         """(dt, level multipliers, period hint) for plan_for / LoglPlan; the hint (Stumpff series
@@ -154,6 +170,7 @@ class LoglPlan:
         self.npoints = float(npoints)
         self.max_walkers = int(max_walkers)
         self.resolve_tol, self.resolve_max = float(resolve[0]), int(resolve[1])
+        self.ecc_guard = float(resolve[2]) if len(resolve) > 2 else 0.0
         lm = (C.c_int32 * _lib.RVM_MAX_LEVELS)(*self.mult)
         cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints, lm, self.period_hint,
                              int(self.inclined), self.resolve_tol, self.resolve_max)
@@ -167,6 +184,9 @@ class LoglPlan:
         ext = C.c_int32()
         _lib.check(self.lib.rvm_plan_extension(self._h, C.byref(ext)), "rvm_plan_extension")
         self.ext_mult = ext.value  # the adaptive resolution's extension level (0: none)
+        if self.ecc_guard > 0.0:
+            _lib.check(self.lib.rvm_plan_set_verify_eccentricity(self._h, self.ecc_guard),
+                       "rvm_plan_set_verify_eccentricity")
 
     def faults(self, reset=False, stream=None) -> dict:
         """rvm_plan_faults: the plan's counters (synchronises the stream): hand-off timeouts, NONFINITE
@@ -400,7 +420,7 @@ def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0
     cache = obs.__dict__.setdefault("_rvm_plans", {})
     mult = level_multipliers(levels)
     stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
-    resolve = (float(resolve[0]), int(resolve[1]))
+    resolve = (float(resolve[0]), int(resolve[1]), float(resolve[2]) if len(resolve) > 2 else 0.0)
     key = (str(dev), int(stream), int(n_planets), float(dt), mult, float(period_hint), bool(inclined), resolve)
     plan = cache.pop(key, None)
     if plan is None or plan.max_walkers < max_walkers:

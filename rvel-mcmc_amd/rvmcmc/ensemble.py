@@ -49,7 +49,7 @@ class DeviceOps:
         dt, mult, hint = st.integrator.plan_args(st.planets)
         # room for the 3 n walker slots of a speculative iteration (iteration_begin)
         self.plan = engine.plan_for(sampler.obs, sampler.pmap.n_planets, dt, mult, 3 * sampler.nloc,
-                                    sampler.device, hint, sampler.pmap.inclined, st.integrator.resolve())
+                                    sampler.device, hint, sampler.pmap.inclined, st.integrator.resolve(st.planets))
         self.timing = None  # set to [] to collect (start_event, end_event, n_walkers) per logL launch
         self.track_status = False  # set True to histogram per-walker statuses (costs a small kernel)
         self.status_counts = torch.zeros(4, dtype=torch.int64, device=sampler.device)

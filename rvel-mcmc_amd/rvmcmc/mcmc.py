@@ -227,7 +227,7 @@ class MhChains:
         self.pmap = self.state.param_map()
         dt, mult, hint = self.state.integrator.plan_args(self.state.planets)
         self.plan = engine.plan_for(obs, self.pmap.n_planets, dt, mult, self.n, self.device, hint, self.pmap.inclined,
-                                    self.state.integrator.resolve())
+                                    self.state.integrator.resolve(self.state.planets))
         self.scales = torch.as_tensor(_scales_vector(self.state, scales), device=self.device)
         if X0 is None:
             X0 = np.tile(self.state.get_params()[:, None], (1, self.n))

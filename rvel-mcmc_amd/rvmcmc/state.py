@@ -168,7 +168,7 @@ class State(object):
     def _plan(self, obs, max_walkers=1, device=None):
         dt, mult, hint = self.integrator.plan_args(self.planets)
         return engine.plan_for(obs, len(self.planets), dt, mult, max_walkers, device, hint,
-                               engine.is_inclined(self.planets), self.integrator.resolve())
+                               engine.is_inclined(self.planets), self.integrator.resolve(self.planets))
 
     def get_rv(self, times):
         """state.py:61-73: model RV (star barycentric vx) at `times`; raises Encounter."""

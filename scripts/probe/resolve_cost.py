@@ -28,7 +28,7 @@ def main():
         cfg = engine.IntegratorConfig()
         dt, mult, hint = cfg.plan_args(S2_PLANETS)
         K = torch.as_tensor(np.ascontiguousarray(X.T), device="cuda")
-        for res in [(0.0, 0), cfg.resolve()]:
+        for res in [(0.0, 0), cfg.resolve(S2_PLANETS)]:
             plan = engine.LoglPlan(t, rv, er, 100, 2, dt, mult, W, period_hint=hint, resolve=res)
             lp, st, _ = plan.logl(K)
             torch.cuda.synchronize()

@@ -65,7 +65,7 @@ def test_config5_shard_8192_walkers():
     plan = ens.plan  # (the default IntegratorConfig: adaptive resolution on)
     assert plan.resolve_tol > 0 and plan.ext_mult == O.ext_multiplier(plan.mult, plan.resolve_max)
     rf, _ = assert_t1_adaptive(lnp[idx], st_all.cpu().numpy()[idx], P, 3, obs, plan.dt, plan.mult, plan.resolve_tol,
-                               plan.resolve_max)
+                               plan.resolve_max, ecc_guard=plan.ecc_guard)
     ias, st_ias = IP.ias15_logl(P, 3, obs, ens.hill_factor)
     assert (st_ias == 0).all()
     d2 = np.abs(lnp[idx] - ias)

@@ -97,7 +97,7 @@ def _adapt_oracle(P, obs, dt, mult, tol=TOL, rmax=RMAX):
     return _par(lambda p: O.logl_whx_adapt_batch(p, 2, obs, dt, mult, tol, rmax), P)
 
 
-def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX, has_inc=0, ctx=None):
+def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX, has_inc=0, ctx=None, ecc_guard=0.0):
     """T1 of an adaptive-resolution launch against the oracle's restatement of the same rule
     (oracle.logl_whx_adapt_batch): statuses and logL, up to sensitivity.  Chaotic walkers (close
     approaches) and decisions at roundoff distance from their bound may legitimately go the other
@@ -111,7 +111,7 @@ def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX,
 
     def fn(p, ix=None):
         c = None if ctx is None else dict(ctx, **{k: np.asarray(ctx[k])[ix] for k in ("mode", "z", "u", "lnp0")})
-        r = O.logl_whx_adapt_batch(p, n_planets, obs, dt, mult, tol, rmax, has_inc=has_inc, ctx=c)
+        r = O.logl_whx_adapt_batch(p, n_planets, obs, dt, mult, tol, rmax, has_inc=has_inc, ctx=c, ecc_guard=ecc_guard)
         return r if ctx is not None else r + (np.zeros((len(p), 2), dtype=np.int32),)
 
     ref, st_ref, rf, est, margin, cut = _par_ix(fn, P)
@@ -275,8 +275,9 @@ def test_certain_reject_cut_matches_oracle(W):
     q, z = IP.stretch_proposal(before, c, u1, u2, ens.a)
     plan = ens.plan
     ctx = dict(mode=np.ones(n, dtype=np.int32), dim=s.Nvars, z=z, u=u3, lnp0=lnp0)
+    assert plan.ecc_guard > 0.0  # (the sampler's plan carries the eccentricity guard)
     rf, sensitive, cut = assert_t1_adaptive(got, st, IP.to_oracle(s.param_map(), q), 2, obs, plan.dt, plan.mult,
-                                            plan.resolve_tol, plan.resolve_max, ctx=ctx)
+                                            plan.resolve_tol, plan.resolve_max, ctx=ctx, ecc_guard=plan.ecc_guard)
     ncut = int(cut.sum())
     print(f"W={W}: directions extended {int((rf == 1).sum())}, halved {int((rf >= 2).sum())}, cut {ncut} "
           f"(oracle); kernel {f}")
@@ -321,3 +322,25 @@ def test_near_parabolic_pericentre_reports_the_encounter(hd_obs_oracle):
         _, st = _run(plan, K.T)
         assert st.tolist() == [2, 2], (res, st)
         assert plan.faults()["nonfinite"] == 0
+
+
+@pytest.mark.parametrize("W", [512, 6144])
+def test_t1_eccentricity_guard(W):
+    """rvm_plan_set_verify_eccentricity: walkers with a planet above the guard get the extension
+    whatever their estimate (IntegratorConfig.verify_speedup; the sampler plans carry it).  Both
+    layouts against the oracle's restatement of the same rule; the guard must add extensions."""
+    from rvmcmc import engine
+
+    obs = s2_obs_oracle()
+    guard = engine.IntegratorConfig().ecc_guard(S2_PLANETS)
+    assert 0.26 < guard < 0.27
+    dt, mult, hint = engine.IntegratorConfig().plan_args(S2_PLANETS)
+    t, rv, er = engine.obs_arrays(obs)
+    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint, resolve=(TOL, RMAX, guard))
+    assert plan.ecc_guard == guard
+    X = wide_walkers(W, ball=0.3, seed=21)
+    got, st = _run(plan, X)
+    rf, _ = assert_t1_adaptive(got, st, _oracle_P(X), 2, obs, dt, mult, ecc_guard=guard)
+    rf0 = O.logl_whx_adapt_batch(_oracle_P(X), 2, obs, dt, mult, TOL, RMAX)[2]
+    print(f"W={W}: directions extended {int((rf == 1).sum())} with the guard, {int((rf0 == 1).sum())} without")
+    assert (rf >= 1).sum() > (rf0 >= 1).sum()
