@@ -378,6 +378,12 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             P.ext_nt = P.nt[fin];
             P.ext_spec = P.spec[fin];  // (a finer step than the finest level's: speculate where it does)
             P.inv_ext = 1.0 / m5[nl];
+            // and as plan level slot nl (lw[nl] = 0): the concurrent extension wave of the
+            // LDS-coupled layout integrates it like any level (rvm_logl.hip, cx)
+            P.mult[nl] = P.ext_mult;
+            P.nt[nl] = P.ext_nt;
+            P.spec[nl] = P.ext_spec;
+            P.inv_mult[nl] = P.inv_ext;
             P.lvx = reinterpret_cast<double*>(plan->xmem);
             P.rvp = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(plan->xmem) + bl);
             P.lvx_emax = (int32_t)emax;

@@ -267,12 +267,22 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         d = unit & 1;
         w0 = (unit >> 1) * WPB;
     } else {
-        grp = wv >= nl ? 1 : 0;
-        lvl = grp ? 2 * nl - 1 - wv : wv;  // wave-uniform extrapolation level
-        G = (blockDim.x >> 6) / nl;
+        // (cx: one group per block plus a wave for the extension level, nl + 1 waves)
+        const bool cxw = (int)(blockDim.x >> 6) == nl + 1;
+        grp = !cxw && wv >= nl ? 1 : 0;
+        lvl = grp ? 2 * nl - 1 - wv : wv;  // wave-uniform extrapolation level (nl: the extension)
+        G = cxw ? 1 : (blockDim.x >> 6) / nl;
         d = blockIdx.y;
         w0 = (blockIdx.x * G + grp) * WPB;  // first walker of the group
     }
+    // Concurrent extension (LDS-coupled layout with one group per block, launch_logl): when the
+    // blocks leave SIMDs with room (at most one block per CU), the adaptive resolution's extension
+    // level (P.ext_mult steps per base step, plan slot nl) runs as an extra wave of the main pass
+    // from t = 0 -- on SIMD 0 beside level 0, the lightest -- instead of after it.  The combiner
+    // forms r5 and its acceptance sums at every epoch; the flagged walkers then take the
+    // extension's verdict at once (the same bits as extend_pass: the same integration, the same
+    // sums), and only the halving passes remain.
+    const bool cx = !dec && (int)(blockDim.x >> 6) == nl + 1;
     const bool live = w0 < W && !idle;  // level-split: waves past the last unit only help stage the schedule
     const bool comb = dec && idle;       // level-split: this unit's combiner from the start
     const int lane = threadIdx.x & 63;
@@ -596,6 +606,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                        // keeps needing the general solver), back to 4 after a clean segment
     double chi2 = 0.0;
     double est = 0.0;  // adaptive resolution: sum_e |(rv - o)^2 - (rv3 - o)^2| / s2 (combiner lanes)
+    double c5x = 0.0, ddx = 0.0;  // the concurrent extension's chi2 and acceptance sum (cx)
     // level-split hand-off: level 1's column of P.lv_rv (one epoch row per epoch); the other levels'
     // slot in the block's LDS ring ([unit ul][local level ks][RING][WPB] doubles after the schedule)
     const int ul = wv & 1;
@@ -746,7 +757,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 double s5 = 0.0;
                 for (int k = 0; k < nl; k++) s5 += P.lw5[k] * s_rv[e & 1][k][lane];
                 const size_t xi = (size_t)(d * P.lvx_emax + e) * P.lvx_stride + wo;
-                P.lvx[xi] = s5;
+                if (cx) {  // (extend_pass's sums, from the extension wave's value of this epoch)
+                    const double r5 = s5 + P.lw5[nl] * s_rv[e & 1][nl][lane];
+                    const double q = r5 - l_rv[e];
+                    c5x += (q * q) / l_s2[e];
+                    ddx += fabs((r5 - rvx) * (q + (rvx - l_rv[e]))) / l_s2[e];
+                } else {
+                    P.lvx[xi] = s5;
+                }
                 P.rvp[xi] = rvx;
             }
         }
@@ -1023,7 +1041,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // direction's chi2 >= 0 left out -- is rejected whatever further passes would give: it stops
     // refining and keeps this pass's value (never stored: rejected).  Counted in counters[4].
     auto refine_loop = [&](const int lr, const int gr, const int dr, const int gmask, const int eb, const bool cmb,
-                           bool& need, double& chi2w, int& enc) {
+                           bool& need, double& chi2w, int& enc, const bool ext_done) {
         // the combiner lane's accept inputs: 0 none, 1 stretch (emcee), 2 MH
         int dmode = 0;
         double dz = 0.0, du = 0.0, dl = 0.0;
@@ -1049,7 +1067,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 dl = sa.lnp[wo];
             }
         }
-        if (P.ext_mult > 0) {
+        if (P.ext_mult > 0 && !ext_done) {
             const uint64_t gneed = s_need[gr];
             if (lr == 0 && gneed) {
                 if (lane == 0)
@@ -1125,13 +1143,30 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (P.rmax == 0) {
                 if (need) enc |= RVM_ENC_UNRESOLVED;
             } else {
+                if (cx && lvl == 0) {
+                    // the concurrent extension's verdict (extend_pass's rule on the same sums)
+                    const uint64_t nx = ballot(need);
+                    if (lane == 0 && nx)
+                        __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(nx),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (need) {
+                        if (s_enc[nl][lane] & 1) {
+                            enc |= 1;
+                            chi2w = c5x;
+                            need = false;
+                        } else if (ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
+                            chi2w = c5x;
+                            need = false;
+                        }
+                    }
+                }
                 if (lvl == 0) {
                     const uint64_t nb = ballot(need);
                     if (lane == 0) s_need[grp] = nb;
                 }
                 __syncthreads();
                 if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
-                    refine_loop(lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc);
+                    refine_loop(cx ? (lvl < nl ? lvl : -1) : lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc, cx);
             }
         }
         if (cmb && wo < W) {
@@ -1358,7 +1393,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (lane == 0) s_need[gr] = nb;
         }
         __syncthreads();
-        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc);
+        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, false);
         if (cmb && mine && w0 + lane < W) finish_recompute(w0 + lane, chi2w, enc);
         return;
     }
@@ -1426,7 +1461,10 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     // the heaviest level with the lightest on each SIMD (logl_kernel)
     const int G = (P.n_cu > 0 && 2 * groups > P.n_cu && 2 * P.n_levels * 64 <= 512) ? 2 : 1;
     dim3 grid((groups + G - 1) / G, 2);
-    dim3 block(64 * P.n_levels * G);
+    // one group per block (the blocks fit one per CU): the extension level as an extra wave
+    // (logl_kernel, cx) when the plan has one and no model RVs are asked for
+    const bool cx = G == 1 && P.ext_mult > 0 && rv_out == nullptr;
+    dim3 block(64 * (P.n_levels + (cx ? 1 : 0)) * G);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t rows = (size_t)(D3V ? 7 : 5) * NPV;
     const bool fused = sa.c != nullptr || sa.mh_scale != nullptr;
