@@ -79,7 +79,7 @@ struct DevPlan {
     // level-split layout (launch_logl, rvm_logl.hip): level 1 of a walker group runs in another
     // workgroup than its levels 3, 2, 0 and the unit's combiner, and hands its star velocities over
     // through HBM.  Null when the plan cannot use it.  All-ones / -1 between launches.
-    double* lv_rv;     // [2][lv_emax][lv_stride] level 1's star vx per direction, epoch, walker
+    double* lv_rv;     // [2][lv_emax][lv_stride] the HBM-handed level's (1; 2 with lsx) star vx per direction, epoch, walker
     int32_t* lv_enc;   // [2][lv_stride] level 1's encounter / prior flags
     int32_t lv_emax, lv_stride;
     DirSched fwd, bwd;

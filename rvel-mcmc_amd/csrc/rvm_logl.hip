@@ -240,16 +240,24 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     //     from the start (10, 7) when a direction has more epochs than the ring holds
     //   type B, tB = 8 units of level 1 per block: waves 0..7 one each (2 m1 per SIMD); or tB = 6
     //     (all CUs in use): waves 0..3 whole, 4 / 5 head / tail of unit 4, 6 / 7 of unit 5 (1.5 m1)
+    //   with the extension level (lsx, an adaptive plan whose directions fit the ring): type A, units
+    //     2b + (wv & 1), waves 0, 1 the extension (plan slot nl = 4, P.ext_mult steps per base step),
+    //     2, 3 level 3, 4, 5 level 0 -- then the units' combiners --, 6, 7 level 1: SIMD loads
+    //     m_x + m0 and m3 + m1; type B level 2 of tB = 8 units (2 m2), handed over through HBM
     const int tB = lsm & 0xFF;
-    const bool splitA = (lsm >> 8) != 0;  // (needs the whole direction in the ring: E <= RVM_LS_RING)
+    const bool splitA = ((lsm >> 8) & 1) != 0;  // (needs the whole direction in the ring: E <= RVM_LS_RING)
+    const bool lsx = dec && ((lsm >> 9) & 1) != 0;
+    const int hl = lsx ? 2 : 1;   // the level handed over through HBM (type-B blocks)
+    const int NK = lsx ? 4 : 3;   // levels per unit in the type-A ring
     const int tsk = wv < 4 || tB == 8 ? wv : (wv < 6 ? 4 : 5);  // type-B task of this wave
     auto unit_of = [&]() { return bid < nA ? 2 * bid + (wv & 1) : tB * (bid - nA) + tsk; };
     int part = 0, hs = 0;
     if (dec) {
         const int b = bid;
         const int unit = __builtin_amdgcn_readfirstlane(unit_of());  // wave-uniform (SGPRs)
-        lvl = __builtin_amdgcn_readfirstlane(b < nA ? (wv < 2 ? 3 : (wv < 4 ? 2 : 0)) : 1);
-        idle = b < nA && !splitA && (wv == 4 || wv == 5);  // the combiners (no integration)
+        lvl = __builtin_amdgcn_readfirstlane(
+            b < nA ? (lsx ? (wv < 2 ? nl : (wv < 4 ? 3 : (wv < 6 ? 0 : 1))) : (wv < 2 ? 3 : (wv < 4 ? 2 : 0))) : hl);
+        idle = b < nA && !splitA && !lsx && (wv == 4 || wv == 5);  // the combiners (no integration)
         if (b < nA) {
             part = splitA ? (wv >= 6 ? 1 : (wv >= 4 ? 2 : 0)) : 0;
             hs = wv & 1;
@@ -296,9 +304,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // level-split hand-off inside a type-A block (unit ul = wv & 1; local level slot ks = 0, 1, 2
     // for levels 3, 2, 0): epochs published per level, epochs consumed by the combiner, the levels'
     // encounter / prior flags; the RVs themselves sit in the ring after the schedule (s_sched)
-    __shared__ int s_lvp[2][3];
+    __shared__ int s_lvp[2][4];
     __shared__ int s_cprog[2];
-    __shared__ int s_encl[2][3][64];
+    __shared__ int s_encl[2][4][64];
     // head -> tail hand-off of a split level (slot hs): the lanes' dynamic state, the wave's
     // encounter mask and speculation state, and the ready flag
     __shared__ double s_hos[2][8][64];
@@ -509,7 +517,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // schedule and the stretch staging (LDS-coupled: [group][8][64]) or after the level-split ring
     // ([unit][8][64]; the unit's level-3 wave keeps it)
     const int ring_sz = emax2 < RVM_LS_RING ? emax2 : RVM_LS_RING;
-    double* l_init = dec ? s_sched + (size_t)8 * emax2 + (size_t)6 * ring_sz * WPB
+    double* l_init = dec ? s_sched + (size_t)8 * emax2 + (size_t)2 * NK * ring_sz * WPB
                          : s_sched + (size_t)4 * emax2 + (fused ? (size_t)(R + 3) * GW : 0);
     if (P.rmax > 0 && (dec ? (bid < nA && wv < 2) : lvl == 0)) {
         double* o = l_init + (size_t)(dec ? wv : grp) * RVM_INIT_DOUBLES + lane;
@@ -545,7 +553,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             l_idx[i] = S.obs_idx[i];
         }
     } else {
-        if (threadIdx.x < 6) (&s_lvp[0][0])[threadIdx.x] = 0;
+        if (threadIdx.x < 8) (&s_lvp[0][0])[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_cprog[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_hof[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_vd[threadIdx.x] = 0;
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // level-split hand-off: level 1's column of P.lv_rv (one epoch row per epoch); the other levels'
     // slot in the block's LDS ring ([unit ul][local level ks][RING][WPB] doubles after the schedule)
     const int ul = wv & 1;
-    const int ks = lvl == 3 ? 0 : (lvl == 2 ? 1 : 2);
+    const int ks = lsx ? (lvl == 3 ? 0 : (lvl == 1 ? 1 : (lvl == 0 ? 2 : 3))) : (lvl == 3 ? 0 : (lvl == 2 ? 1 : 2));
     const int RING = emax2 < RVM_LS_RING ? emax2 : RVM_LS_RING;
     double* ring = s_sched + (size_t)8 * emax2;
     gu64* lv1p = dec ? (gu64*)(P.lv_rv + ((size_t)d * P.lv_emax + e_lo) * P.lv_stride + wl) : nullptr;
@@ -711,7 +719,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 __builtin_amdgcn_s_setprio(2);
             else
                 __builtin_amdgcn_s_setprio(1);
-            if (lvl == 1) {
+            if (lvl == hl) {
                 if (pl_idx == 0 && valid) {
                     unsigned long long bits = (unsigned long long)__double_as_longlong(v0);
                     if (bits == RVM_LV_EMPTY) bits = 0x7FF8000000000000ULL;  // (still a NaN)
@@ -736,7 +744,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                         __builtin_amdgcn_s_sleep(4);
                     }
                 }
-                if (pl_idx == 0) ring[((ul * 3 + ks) * RING + rslot) * WPB + slot] = v0;
+                if (pl_idx == 0) ring[((ul * NK + ks) * RING + rslot) * WPB + slot] = v0;
                 if (lane == 0) __hip_atomic_store(&s_lvp[ul][ks], e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 rslot = rslot + 1 == RING ? 0 : rslot + 1;
             }
@@ -1239,7 +1247,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         }
         if (!comb && part != 1) {
             // a level wave: publish this level's encounter / prior flags (type B: and leave)
-            if (lvl == 1) {
+            if (lvl == hl) {
                 if (pl_idx == 0 && valid)
                     __hip_atomic_store((gi32*)(P.lv_enc + (size_t)d * P.lv_stride + w), encflag, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
@@ -1251,10 +1259,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             prof_dec(__builtin_amdgcn_s_memrealtime(), lvl);
 #endif
             if (bid >= nA) return;
-        } else {
-            // the unit's combiner: consume epoch e once the three local levels have published it
-            // (LDS counters) and level 1's values have landed (every lane's slot off the sentinel);
-            // lowest issue priority (it shares a SIMD with a level-3 or level-2 wave).  A plan whose
+        }
+        // (lsx: level 0's wave, its integration done, combines its unit -- the ring holds every epoch)
+        if (comb || part == 1 || (lsx && lvl == 0)) {
+            // the unit's combiner: consume epoch e once the local levels have published it (LDS
+            // counters) and the HBM-handed level's values have landed (every lane's slot off the
+            // sentinel); lowest issue priority (it shares a SIMD with a level wave).  A plan whose
             // hand-off workspace is dirty from an earlier give-up (counters[0] != 0, until
             // rvm_plan_faults resets it) reports every walker NONFINITE without waiting.
             __builtin_amdgcn_s_setprio(0);
@@ -1262,13 +1272,16 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             hung = __builtin_amdgcn_readfirstlane((int)hung) != 0;
             const bool dirty = hung;
             auto local_published = [&]() {
-                const int p0 = __hip_atomic_load(&s_lvp[ul][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int p1 = __hip_atomic_load(&s_lvp[ul][1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                const int p2 = __hip_atomic_load(&s_lvp[ul][2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                return __builtin_amdgcn_readfirstlane(p0 < p1 ? (p0 < p2 ? p0 : p2) : (p1 < p2 ? p1 : p2));
+                int p = __hip_atomic_load(&s_lvp[ul][0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int k = 1; k < NK; k++) {
+                    const int pk = __hip_atomic_load(&s_lvp[ul][k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    p = pk < p ? pk : p;
+                }
+                return __builtin_amdgcn_readfirstlane(p);
             };
             gu64* l1 = (gu64*)(P.lv_rv + (size_t)d * P.lv_emax * P.lv_stride + wl);
             double chi2w = 0.0;
+            double c5x = 0.0, ddx = 0.0;  // lsx: the extension's chi2 and acceptance sum (as extend_pass)
             int rr = 0;
             clk.restart();
             for (int e = 0; e < E; e++) {
@@ -1288,8 +1301,20 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 clk.restart();  // (an epoch arrived: progress)
                 // levels in order 0..3 (same arithmetic as the LDS-coupled path)
                 const double* rg = ring + (size_t)rr * WPB + slot;
-                const double v[4] = {rg[(ul * 3 + 2) * RING * WPB], __longlong_as_double((long long)b1),
-                                     rg[(ul * 3 + 1) * RING * WPB], rg[(ul * 3 + 0) * RING * WPB]};
+                const size_t rs = (size_t)RING * WPB;
+                const double vh = __longlong_as_double((long long)b1);
+                double v[4];
+                if (lsx) {
+                    v[0] = rg[(ul * 4 + 2) * rs];
+                    v[1] = rg[(ul * 4 + 1) * rs];
+                    v[2] = vh;
+                    v[3] = rg[(ul * 4 + 0) * rs];
+                } else {
+                    v[0] = rg[(ul * 3 + 2) * rs];
+                    v[1] = vh;
+                    v[2] = rg[(ul * 3 + 1) * rs];
+                    v[3] = rg[(ul * 3 + 0) * rs];
+                }
                 double rvx = 0.0, rv3 = 0.0;
 #pragma unroll
                 for (int k = 0; k < 4; k++) rvx += P.lw[k] * v[k];
@@ -1304,7 +1329,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #pragma unroll
                     for (int k = 0; k < 4; k++) s5 += P.lw5[k] * v[k];
                     const size_t xi = (size_t)(d * P.lvx_emax + e) * P.lvx_stride + w;
-                    P.lvx[xi] = s5;
+                    if (lsx) {  // (extend_pass's sums, from the extension wave's value of this epoch)
+                        const double r5 = s5 + P.lw5[nl] * rg[(ul * 4 + 3) * rs];
+                        const double q = r5 - l_rv[e];
+                        c5x += (q * q) / l_s2[e];
+                        ddx += fabs((r5 - rvx) * (q + (rvx - l_rv[e]))) / l_s2[e];
+                    } else {
+                        P.lvx[xi] = s5;
+                    }
                     P.rvp[xi] = rvx;
                 }
                 if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1315,7 +1347,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 __builtin_amdgcn_s_sleep(2);
                 hung = clk.expired(P.spin_ticks);
             }
-            int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];
+            int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];  // (lsx: [3] the extension)
             {
                 gi32* e1p = (gi32*)(P.lv_enc + (size_t)d * P.lv_stride + wl);
                 int f1;
@@ -1344,6 +1376,22 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (need && P.rmax == 0) {
                 enc |= RVM_ENC_UNRESOLVED;
                 need = false;
+            }
+            if (lsx) {  // the concurrent extension's verdict (extend_pass's rule on the same sums)
+                const uint64_t nx = ballot(need);
+                if (lane == 0 && nx)
+                    __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(nx),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (need) {
+                    if (s_encl[ul][3][slot] & 1) {
+                        enc |= 1;
+                        chi2w = c5x;
+                        need = false;
+                    } else if (ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
+                        chi2w = c5x;
+                        need = false;
+                    }
+                }
             }
             const bool refine = ballot(need) != 0;
             if (!refine) {
@@ -1393,7 +1441,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (lane == 0) s_need[gr] = nb;
         }
         __syncthreads();
-        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, false);
+        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, lsx);
         if (cmb && mine && w0 + lane < W) finish_recompute(w0 + lane, chi2w, enc);
         return;
     }
@@ -1473,8 +1521,25 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     // level-split layout (logl_kernel) when it lowers the heaviest SIMD's load: in steps per base
     // step, max(m3, m2 + m0, 2 m1) for one round of <= n_cu blocks, against m3 per round of
     // single-group blocks or max_i(m_i + m_{n-1-i}) per round of two-group blocks
-    int nA = 0, tB = 8, splitA = 0;
-    if (P.lv_rv != nullptr && W <= P.lv_stride && P.n_levels == 4 && P.n_cu > 0) {
+    int nA = 0, tB = 8, splitA = 0, lsx = 0;
+    // with the adaptive resolution's extension level: where two groups would share a block (no
+    // room for the concurrent extension wave), the level-split layout carries the extension as a
+    // fifth level of the main pass (logl_kernel, lsx) -- the ring then holds whole directions
+    if (P.lv_rv != nullptr && W <= P.lv_stride && P.n_levels == 4 && P.n_cu > 0 && P.ext_mult > 0 &&
+        rv_out == nullptr && G == 2 && emax <= RVM_LS_RING) {
+        const int units = 2 * groups;
+        const int na = groups, nb = (units + 7) / 8;
+        const size_t smem_x = (size_t)emax * 8 * sizeof(double) + (size_t)8 * emax * wpb * sizeof(double) + 2 * init;
+        if (na + nb <= P.n_cu && smem_x <= lds_budget<NPV, D3V, true>()) {
+            nA = na;
+            tB = 8;
+            lsx = 1;
+            grid = dim3(na + nb, 1);
+            block = dim3(8 * 64);
+            smem = smem_x;
+        }
+    }
+    if (nA == 0 && P.lv_rv != nullptr && W <= P.lv_stride && P.n_levels == 4 && P.n_cu > 0) {
         const int* m = P.mult;
         const int units = 2 * groups;
         // type-B blocks carry 6 units' level 1 (two of them split head / tail) when the CUs allow,
@@ -1500,7 +1565,7 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     }
     if (nA > 0) {
         logl_kernel<NPV, D3V, true><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, logl,
-                                                                   status, sa, nA, tB | (splitA << 8));
+                                                                   status, sa, nA, tB | (splitA << 8) | (lsx << 9));
     } else {
         if (smem > lds_budget<NPV, D3V, false>()) return hipErrorInvalidConfiguration;
         logl_kernel<NPV, D3V, false><<<grid, block, smem, stream>>>(P, W, params, hill_factor, slots, rv_out, logl,
