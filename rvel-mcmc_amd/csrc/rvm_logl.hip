@@ -1283,23 +1283,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             double chi2w = 0.0;
             double c5x = 0.0, ddx = 0.0;  // lsx: the extension's chi2 and acceptance sum (as extend_pass)
             int rr = 0;
-            clk.restart();
-            for (int e = 0; e < E; e++) {
-                while (!hung && local_published() <= e) {
-                    __builtin_amdgcn_s_sleep(2);
-                    hung = clk.expired(P.spin_ticks);
-                }
-                unsigned long long b1;
-                for (;;) {
-                    b1 = valid ? __hip_atomic_load(l1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ULL;
-                    if (ballot(b1 == RVM_LV_EMPTY) == 0 || hung) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    hung = clk.expired(P.spin_ticks);
-                }
-                if (valid && pl_idx == 0) __hip_atomic_store(l1, RVM_LV_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                l1 += P.lv_stride;
-                clk.restart();  // (an epoch arrived: progress)
-                // levels in order 0..3 (same arithmetic as the LDS-coupled path)
+            // one epoch: the levels in order 0..3 (same arithmetic as the LDS-coupled path), b1 the
+            // HBM-handed level's bits
+            auto consume = [&](const int e, const unsigned long long b1) {
                 const double* rg = ring + (size_t)rr * WPB + slot;
                 const size_t rs = (size_t)RING * WPB;
                 const double vh = __longlong_as_double((long long)b1);
@@ -1339,9 +1325,66 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                     }
                     P.rvp[xi] = rvx;
                 }
-                if (lane == 0) __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // (the levels wait on it only when the ring wraps; a release store also waits for
+                // every load in flight, the prefetched HBM values included)
+                if (E > RING && lane == 0)
+                    __hip_atomic_store(s_cprog + ul, e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 rr = rr + 1 == RING ? 0 : rr + 1;
+            };
+            // The HBM-handed level's values are loaded PF epochs ahead, each into the register its
+            // epoch's value just left (the loop is unrolled by PF: no register moves, which would
+            // wait for the loads in flight): an lsx combiner starts when its own level is done and
+            // finds most values landed -- one HBM latency per PF epochs.  A value still at the
+            // sentinel is polled again when its epoch comes.  The hang clock restarts when a wait
+            // begins (a wait's limit is time without progress).
+            // The loads are unconditional (a lane past W reads walker W - 1's slot, an epoch past the
+            // last re-reads the last; the values are masked afterwards): a load the compiler can
+            // branch around leaves it unsure how many are in flight, and it then waits for all.
+            constexpr int PF = 8;
+            const int el = E > 0 ? E - 1 : 0;
+            unsigned long long bq[PF];
+#pragma unroll
+            for (int j = 0; j < PF; j++)
+                bq[j] = __hip_atomic_load(l1 + (size_t)(j < el ? j : el) * P.lv_stride, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+            gi32* e1p = (gi32*)(P.lv_enc + (size_t)d * P.lv_stride + wl);
+            int f1 = __hip_atomic_load(e1p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (early too)
+            int pub = 0;  // the local levels' published epochs, as last read
+            for (int e0 = 0; e0 < E; e0 += PF) {
+#pragma unroll
+                for (int j = 0; j < PF; j++) {
+                    const int e = e0 + j;
+                    if (e < E) {
+                        if (pub <= e) {
+                            pub = local_published();
+                            if (pub <= e) clk.restart();
+                            while (!hung && pub <= e) {
+                                __builtin_amdgcn_s_sleep(2);
+                                hung = clk.expired(P.spin_ticks);
+                                pub = local_published();
+                            }
+                        }
+                        gu64* le = l1 + (size_t)e * P.lv_stride;
+                        unsigned long long b1 = valid ? bq[j] : 0ULL;
+                        // (the test of the prefetched value in straight-line code, the poll as a
+                        // bottom-tested loop: a loop header that reads b1 makes the compiler wait
+                        // for every load in flight, vmcnt(0), at each epoch)
+                        if (ballot(b1 == RVM_LV_EMPTY) != 0 && !hung) {
+                            clk.restart();
+                            do {
+                                __builtin_amdgcn_s_sleep(2);
+                                hung = clk.expired(P.spin_ticks);
+                                b1 = valid ? __hip_atomic_load(le, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ULL;
+                            } while (ballot(b1 == RVM_LV_EMPTY) != 0 && !hung);
+                        }
+                        bq[j] = __hip_atomic_load(l1 + (size_t)(e + PF < el ? e + PF : el) * P.lv_stride,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (valid && pl_idx == 0) __hip_atomic_store(le, RVM_LV_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        consume(e, b1);
+                    }
+                }
             }
+            clk.restart();
             // the levels' flags: local ones after their last counter step (E + 1), level 1's from HBM
             while (!hung && local_published() <= E) {
                 __builtin_amdgcn_s_sleep(2);
@@ -1349,13 +1392,13 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             }
             int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];  // (lsx: [3] the extension)
             {
-                gi32* e1p = (gi32*)(P.lv_enc + (size_t)d * P.lv_stride + wl);
-                int f1;
-                for (;;) {
-                    f1 = valid ? __hip_atomic_load(e1p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-                    if (ballot(f1 < 0) == 0 || hung) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    hung = clk.expired(P.spin_ticks);
+                f1 = valid ? f1 : 0;
+                if (ballot(f1 < 0) != 0 && !hung) {
+                    do {
+                        __builtin_amdgcn_s_sleep(2);
+                        hung = clk.expired(P.spin_ticks);
+                        f1 = valid ? __hip_atomic_load(e1p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                    } while (ballot(f1 < 0) != 0 && !hung);
                 }
                 if (valid && pl_idx == 0) __hip_atomic_store(e1p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 enc |= f1 > 0 ? f1 : 0;

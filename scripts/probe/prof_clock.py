@@ -5,7 +5,7 @@ Each wave records s_memtime (shader cycles) and s_memrealtime (100 MHz) at its s
 cycles / realtime is the clock the wave actually ran at, and segment cycles / (mult x base steps)
 is the cost of one step on that level.  Answers: is a launch issue-bound (cycles per step grow
 when two waves share a SIMD) or clock-bound (the clock drops under full-chip fp64 load)?
-Usage: python scripts/probe/prof_clock.py W [W ...]   (S2 workload, default integrator)"""
+Usage: [RESOLVE=5e-7,4] [BALL=1e-3] python scripts/probe/prof_clock.py W [W ...]   (S2 workload)"""
 import ctypes as C
 import json
 import os
@@ -32,7 +32,11 @@ def run(lib, W):
     obs = s2_obs_oracle()
     dt, mult, hint = engine.IntegratorConfig().plan_args(S2_PLANETS)
     t, rv, er = engine.obs_arrays(obs)
-    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint)
+    # RESOLVE="tol,max": an adaptive plan (its extension level runs as a fifth level of the split
+    # layout, or as a concurrent wave of the one-group-per-block layout)
+    rs = os.environ.get("RESOLVE")
+    resolve = (float(rs.split(",")[0]), int(rs.split(",")[1])) if rs else (0.0, 0)
+    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint, resolve=resolve)
     info = plan.info()
     nbase = [info["steps_fwd"], info["steps_bwd"]]
     rng = np.random.default_rng(0)
@@ -64,7 +68,7 @@ def run(lib, W):
            "clock_ghz": pct(cyc[ok] / rt_us[ok] / 1e3), "span_us": float((b[:, 6].max() - b[:, 5].min()) / 100.0)}
     # placement from HW_REG_HW_ID (simd [5:4]): which wave slots of a block share a SIMD
     simd = (b[:, 10] >> 4) & 3
-    wpb = 8 if W > 4096 else 4
+    wpb = 8 if W > 4096 else (5 if rs else 4)
     blk, wv = gw // wpb, gw % wpb
     pairs = {}
     for bk in np.unique(blk):
@@ -87,6 +91,28 @@ def run(lib, W):
                             "rest_kcyc": pct((cyc[s] - (b[s, 1] - b[s, 0]) - b[s, 2] - b[s, 3]) / 1e3),
                             "start_us": pct((b[s, 5] - t0) / 100.0), "end_us": pct((b[s, 6] - t0) / 100.0),
                             "redo": int(b[s, 8].sum())}
+        # level-split waves: the end of the integration (o[11]) and a combiner's arrival (o[12]:
+        # every epoch consumed, verdict next)
+        if np.any(b[s, 11] != 0):
+            out[f"level{k}"]["integ_end_us"] = pct((b[s, 11] - t0) / 100.0)
+        if np.any(b[s, 12] != 0):
+            out[f"level{k}"]["comb_arrival_us"] = pct((b[s, 12] - t0) / 100.0)
+    # level-split: per unit, the combiner's arrival against the last of its levels' integration
+    # ends (o[13] >> 8 = unit): the time the combiner needs after its last input
+    if np.any(b[:, 11] != 0):
+        unit = (b[:, 13] >> 8) & 0xFFFF
+        t0 = b[:, 5].min()
+        lag, own = [], []
+        for u in np.unique(unit[b[:, 12] != 0]):
+            su = unit == u
+            cmb = su & (lvl == 0)
+            if not np.any(cmb):
+                continue
+            last = b[su, 11].max()
+            lag.append((b[cmb, 12].max() - last) / 100.0)
+            own.append((b[cmb, 12].max() - b[cmb, 11].max()) / 100.0)
+        out["comb_after_last_level_us"] = pct(np.array(lag))
+        out["comb_after_own_level_us"] = pct(np.array(own))
     return out
 
 
