@@ -21,6 +21,9 @@ constexpr double RVM_EXT_ACCEPT = 2.0;
 // (rvm_logl.hip refine_loop; oracle/rvoracle.c CUT_EST_FACTOR; measured error / estimate <= 57 on
 // the main pass at the plan's step, smaller after a halving)
 constexpr double RVM_CUT_EST_FACTOR = 100.0;
+// launches of fewer walkers than this run the extension after the main pass (only when a walker is
+// flagged) instead of as a concurrent fifth wave of the one-group-per-block layout (launch_logl_t)
+constexpr int RVM_CX_MIN_WALKERS = 32;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {

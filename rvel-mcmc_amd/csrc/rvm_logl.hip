@@ -1553,8 +1553,13 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     const int G = (P.n_cu > 0 && 2 * groups > P.n_cu && 2 * P.n_levels * 64 <= 512) ? 2 : 1;
     dim3 grid((groups + G - 1) / G, 2);
     // one group per block (the blocks fit one per CU): the extension level as an extra wave
-    // (logl_kernel, cx) when the plan has one and no model RVs are asked for
-    const bool cx = G == 1 && P.ext_mult > 0 && rv_out == nullptr;
+    // (logl_kernel, cx) when the plan has one and no model RVs are asked for.  The fifth wave shares
+    // SIMD 0 with level 0 (4 + 8 steps per base step against level 3's 7 alone), which costs every
+    // launch ~60 % (config 1's one-walker launch 0.335 -> 0.538 ms with nothing flagged,
+    // scripts/probe/config1_probe.py): worth it only where a launch almost surely holds a flagged
+    // walker.  Launches of a few walkers (the reference API's single-state calls) run the extension
+    // after the main pass, only when flagged -- the same bits either way.
+    const bool cx = G == 1 && P.ext_mult > 0 && rv_out == nullptr && W >= RVM_CX_MIN_WALKERS;
     dim3 block(64 * (P.n_levels + (cx ? 1 : 0)) * G);
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t rows = (size_t)(D3V ? 7 : 5) * NPV;

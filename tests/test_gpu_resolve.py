@@ -144,7 +144,9 @@ def assert_t1_adaptive(got, st, P, n_planets, obs, dt, mult, tol=TOL, rmax=RMAX,
     return rf, sensitive
 
 
-@pytest.mark.parametrize("W", [512, 6144])  # LDS-coupled layout / level-split layout (bench shape)
+# a few walkers: the extension after the main pass (RVM_CX_MIN_WALKERS); 512: its concurrent wave in the
+# LDS-coupled layout; 6144: the level-split layout with the extension as a fifth level (bench shape)
+@pytest.mark.parametrize("W", [24, 512, 6144])
 def test_t1_adaptive_wide_ball(W):
     obs = s2_obs_oracle()
     plan, dt, mult = _plan(obs, W)
@@ -155,7 +157,8 @@ def test_t1_adaptive_wide_ball(W):
     rf, sensitive = assert_t1_adaptive(got, st, _oracle_P(X), 2, obs, dt, mult)
     print(f"W={W}: oracle walker-directions at the extension {int((rf == 1).sum())}, halved {int((rf >= 2).sum())}; "
           f"kernel counters {f}, statuses {np.bincount(st, minlength=5).tolist()}, sensitive {int(sensitive.sum())}")
-    assert (rf == 1).sum() > W // 20 and (rf >= 2).sum() > W // 20, "the wide ball must exercise both stages"
+    assert (rf == 1).sum() >= max(1, W // 20) and (rf >= 2).sum() >= max(1, W // 20), \
+        "the wide ball must exercise both stages"
     assert f["refined"] > 0 and f["handoff_timeouts"] == 0
     assert f["unresolved"] == int((st == 4).sum())
 
