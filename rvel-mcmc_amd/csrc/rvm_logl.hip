@@ -278,7 +278,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         // (cx: one group per block plus a wave for the extension level, nl + 1 waves)
         const bool cxw = (int)(blockDim.x >> 6) == nl + 1;
         grp = !cxw && wv >= nl ? 1 : 0;
-        lvl = grp ? 2 * nl - 1 - wv : wv;  // wave-uniform extrapolation level (nl: the extension)
+        // wave-uniform extrapolation level (nl: the extension).  cx with four levels: waves 0..4 take
+        // levels 1, 3, 2, the extension, 0 -- wave i runs on SIMD i % 4, so the fifth wave's SIMD
+        // carries levels 0 + 1 (9 steps per base step) and the extension (8) has a SIMD of its own,
+        // instead of extension + level 0 = 12 beside level 3 alone
+        lvl = grp ? 2 * nl - 1 - wv : (cxw && nl == 4 ? (0x04231 >> (4 * wv)) & 15 : wv);
         G = cxw ? 1 : (blockDim.x >> 6) / nl;
         d = blockIdx.y;
         w0 = (blockIdx.x * G + grp) * WPB;  // first walker of the group
@@ -286,7 +290,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // Concurrent extension (LDS-coupled layout with one group per block, launch_logl): when the
     // blocks leave SIMDs with room (at most one block per CU), the adaptive resolution's extension
     // level (P.ext_mult steps per base step, plan slot nl) runs as an extra wave of the main pass
-    // from t = 0 -- on SIMD 0 beside level 0, the lightest -- instead of after it.  The combiner
+    // from t = 0 -- on a SIMD of its own, levels 0 and 1 sharing one -- instead of after it.  The combiner
     // forms r5 and its acceptance sums at every epoch; the flagged walkers then take the
     // extension's verdict at once (the same bits as extend_pass: the same integration, the same
     // sums), and only the halving passes remain.
