@@ -1148,6 +1148,16 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
                     est = dd / npoints;
                     break;
                 }
+#ifdef EARLY_CUT /* (study: the certain-reject test right after the extension) */
+                if (dc != NULL && dc->mode != 0) {
+                    const double lp_hi = -(c5 - fmin(dd, CUT_EST_FACTOR * est * npoints)) / npoints;
+                    if (isfinite(lp_hi) && !decide_accepts(dc, lp_hi)) {
+                        chi2 = c5;
+                        *cut_out = 1;
+                        break;
+                    }
+                }
+#endif
             }
         }
         if (rf == rf_max) {
