@@ -1,3 +1,7 @@
+#!/bin/bash
+# Every BASELINE config (scripts/configs_bench.py), then rocprofv3 --kernel-trace --stats over the
+# bench's own window (--steps 20 --warmup 3, as the default bench line): per-launch durations of the
+# timed iterations.  Each GPU step has its own time limit; the chain stops at the first failure.
 set -euo pipefail
 R=$PWD
 export TMPDIR=/tmp
