@@ -1005,7 +1005,9 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /*   holds);                                                                        */
 /*  stages 2..: every step halved (level k: mult 2^rf steps per base step, rf = 1..rf_max) while  */
 /*   est > tol_dir; still above after rf_max: RVO_UNRESOLVED.                                   */
-/* Certain rejects (a sampler's accept inputs given: dmode 1 emcee stretch, 2 MH): after a       */
+/* Certain rejects (a sampler's accept inputs given: dmode 1 emcee stretch, 2 MH): after an      */
+/* extension that does not settle the direction (with its chi2, d2 = the extension's change and  */
+/* est the main pass's), and after a                                                            */
 /* halving pass whose estimate is still above the bound, the direction stops (status OK, this    */
 /* pass's chi2) when the accept test fails even at lp_hi = -(chi2 - min(d2, CUT_EST_FACTOR est)) */
 /* / npoints, d2 = the pass's change of chi2 from the previous pass (the main pass for rf = 1),  */
@@ -1148,16 +1150,24 @@ static int whx_direction_adapt(int np, const double* pl, double hill_factor, con
                     est = dd / npoints;
                     break;
                 }
-#ifdef EARLY_CUT /* (study: the certain-reject test right after the extension) */
+                /* a certain reject already after the extension: the accept test fails even at
+                 * lp_hi = -(c5 - min(dd, CUT_EST_FACTOR est)) / npoints (dd: the change the
+                 * extension brought, est: the main pass's estimate) -- keep the extension's chi2 */
                 if (dc != NULL && dc->mode != 0) {
                     const double lp_hi = -(c5 - fmin(dd, CUT_EST_FACTOR * est * npoints)) / npoints;
-                    if (isfinite(lp_hi) && !decide_accepts(dc, lp_hi)) {
-                        chi2 = c5;
-                        *cut_out = 1;
-                        break;
+                    if (isfinite(lp_hi)) {
+                        const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0
+                                                             : lp_hi - dc->lnp0;
+                        const double lu = log(dc->u);
+                        const double mg = fabs(lnpdiff - lu) / (1.0 + fabs(lu));
+                        if (mg < margin) margin = mg;
+                        if (!decide_accepts(dc, lp_hi)) {
+                            chi2 = c5;
+                            *cut_out = 1;
+                            break;
+                        }
                     }
                 }
-#endif
             }
         }
         if (rf == rf_max) {

@@ -324,6 +324,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     __shared__ int s_vd[2];
     __shared__ double s_fchi[2][64];
     __shared__ int s_fenc[2][64];
+    // (the early certain-reject test of the refinement team: the main pass's estimate and the
+    // concurrent extension's chi2 and change, per unit and walker slot)
+    __shared__ double s_fx[3][2][64];
     double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
     // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
@@ -955,7 +958,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // halving passes follow.  One wave, no barrier: each epoch's value
     // moves from the walker's first lane to its combiner lane by a shuffle, and the stored levels
     // of the next epoch load while this one integrates.
-    auto extend_pass = [&](const int gr, const int dr, const uint64_t need_m, bool& need, double& chi2w, int& enc) {
+    auto extend_pass = [&](const int gr, const int dr, const uint64_t need_m, bool& need, double& chi2w, int& enc,
+                           double& c5o, double& ddo) {
         const DirSched& SR = dr ? P.bwd : P.fwd;
         const int Er = SR.n_epochs;
         const double* r_dir = dec ? s_sched + (size_t)dr * 4 * emax2 : l_dir;
@@ -1030,6 +1034,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             a4 = b4;
         }
         const bool xenc = ((s.encm >> (cs * L)) & kick_enc_bits<NP>()) != 0;
+        if (cl) {
+            c5o = c5;
+            ddo = dd;
+        }
         if (cl && need) {
             if (xenc) {
                 enc |= 1;
@@ -1052,8 +1060,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // asymptotically 255x that error; or a large multiple of the pass's estimate), the other
     // direction's chi2 >= 0 left out -- is rejected whatever further passes would give: it stops
     // refining and keeps this pass's value (never stored: rejected).  Counted in counters[4].
+    // xest: the combiner lane's main-pass estimate (raw sum); xc5, xdd: the concurrent extension's chi2
+    // and change (ext_done), else set by extend_pass here.
     auto refine_loop = [&](const int lr, const int gr, const int dr, const int gmask, const int eb, const bool cmb,
-                           bool& need, double& chi2w, int& enc, const bool ext_done) {
+                           bool& need, double& chi2w, int& enc, const bool ext_done, const double xest, double xc5,
+                           double xdd) {
         // the combiner lane's accept inputs: 0 none, 1 stretch (emcee), 2 MH
         int dmode = 0;
         double dz = 0.0, du = 0.0, dl = 0.0;
@@ -1085,9 +1096,37 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 if (lane == 0)
                     __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(gneed),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                extend_pass(gr, dr, gneed, need, chi2w, enc);
+                extend_pass(gr, dr, gneed, need, chi2w, enc, xc5, xdd);
                 const uint64_t nb = ballot(need);
                 if (lane == 0) s_need[gr] = nb;
+            }
+            __syncthreads();
+            if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) return;
+        }
+        // a certain reject already after the extension (rvoracle.c whx_direction_adapt): a proposal
+        // whose accept test fails even at lp_hi = -(c5 - min(d, RVM_CUT_EST_FACTOR est)) / npoints
+        // -- the extension's chi2 less the change it brought (or a large multiple of the main
+        // pass's estimate) -- starts no halving pass and keeps the extension's chi2 (counters[4])
+        if (P.ext_mult > 0) {
+            bool cut = false;
+            if (cmb && need && dmode != 0) {
+                const double lp_hi = -(xc5 - fmin(xdd, RVM_CUT_EST_FACTOR * xest)) / P.npoints;
+                if (isfinite(lp_hi) && (dmode == 1 ? !stretch_accepts(sa.dim, dz, lp_hi, dl, du)
+                                                   : !mh_accepts(lp_hi, dl, du))) {
+                    cut = true;
+                    need = false;
+                    chi2w = xc5;
+                }
+            }
+            if (lr == 0) {
+                const uint64_t nb = ballot(need);
+                const uint64_t nc = ballot(cut);
+                if (lane == 0) {
+                    s_need[gr] = nb;
+                    if (nc)
+                        __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)__builtin_popcountll(nc),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             __syncthreads();
             if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) return;
@@ -1178,7 +1217,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 }
                 __syncthreads();
                 if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
-                    refine_loop(cx ? (lvl < nl ? lvl : -1) : lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc, cx);
+                    refine_loop(cx ? (lvl < nl ? lvl : -1) : lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc, cx,
+                                est, c5x, ddx);
             }
         }
         if (cmb && wo < W) {
@@ -1446,6 +1486,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             } else if (valid && pl_idx == 0) {
                 s_fchi[ul][slot] = chi2w;
                 s_fenc[ul][slot] = enc | (need ? 16 : 0);
+                s_fx[0][ul][slot] = est;
+                s_fx[1][ul][slot] = c5x;
+                s_fx[2][ul][slot] = ddx;
             }
             if (lane == 0) __hip_atomic_store(s_vd + ul, refine ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef RVM_PROFILE
@@ -1488,7 +1531,9 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             if (lane == 0) s_need[gr] = nb;
         }
         __syncthreads();
-        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, lsx);
+        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, lsx,
+                    cmb && mine ? s_fx[0][gr][lane] : 0.0, cmb && mine ? s_fx[1][gr][lane] : 0.0,
+                    cmb && mine ? s_fx[2][gr][lane] : 0.0);
         if (cmb && mine && w0 + lane < W) finish_recompute(w0 + lane, chi2w, enc);
         return;
     }
