@@ -60,9 +60,11 @@ class IntegratorConfig:
     # and, if that does not settle it, passes with every step halved, up to resolve_max times -- the
     # plan's step is fixed from the sampler's initial state, the reference's IAS15 adapts to every
     # proposal.  Measured against IAS15 on the bench chain's own proposals (iteration 23 / 2000) and
-    # a 0.6-wide ball: max |dlogL| 1.8e-7 / 1.7e-6 / 3.3e-7 (3 of 6144 steady-state proposals above
-    # 1e-6, the fixed step: 668), at about twice the bench's launch time.  resolve_tol = 0 turns it
-    # off (the round-2 fixed-step algorithm).
+    # a 0.6-wide ball: max |dlogL| 1.8e-7 / 7.0e-7 / 3.3e-7 with the eccentricity guard below (the
+    # fixed step: 668 of 6144 steady-state proposals above 1e-6).  Cost on the bench (the extension
+    # as a fifth level, certain rejects cut after it): 0.53 ms per iteration against 0.375 with the
+    # fixed step; at the chain's steady state 6.2 ms against 0.69.  resolve_tol = 0
+    # turns it off (the round-2 fixed-step algorithm).
     resolve_tol: float = 5e-7
     resolve_max: int = 4
     # eccentricity guard (rvm_plan_set_verify_eccentricity): walkers whose pericentre passage is more
