@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 10
+#define RVM_ABI_VERSION 11
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
@@ -66,6 +66,7 @@ extern "C" {
 #define RVM_MAX_LEVELS 6
 #define RVM_MAX_EPOCHS_PER_DIRECTION 1700 /* epochs with t >= 0, and with t < 0, per plan */
 #define RVM_SMALA_MAX_PARAMS 20           /* free parameters per SMALA chain                 */
+#define RVM_RESOLVE_MAX_LIMIT 12          /* rvm_config.resolve_max                          */
 
 /* Integrator configuration of a plan. */
 typedef struct {
@@ -87,10 +88,14 @@ typedef struct {
                               when the coarsest level is dropped -- split evenly over its two
                               directions.  A direction above its half first gets one extra level
                               (the extension, rvm_plan_extension) joined to its stored levels; if
-                              that does not settle it, it is integrated again with every step
-                              halved, up to resolve_max times (the reference's IAS15 adapts its
-                              step to the orbit; a fixed plan step does not).  <= 0: off            */
-    int32_t resolve_max;   /* 0..8 refinements; 0 with resolve_tol > 0: flag (UNRESOLVED) only      */
+                              that does not settle it, the walker's open directions are integrated
+                              again together with every step halved, up to resolve_max times (the
+                              reference's IAS15 adapts its step to the orbit; a fixed plan step
+                              does not).  The halving passes run in a second kernel on the launch's
+                              stream; every launch function of an adaptive plan
+                              enqueues both.  <= 0: off                                            */
+    int32_t resolve_max;   /* 0..RVM_RESOLVE_MAX_LIMIT halvings; 0 with resolve_tol > 0: flag
+                              (UNRESOLVED) only                                                    */
 } rvm_config;
 
 typedef struct rvm_plan rvm_plan;
@@ -128,14 +133,22 @@ int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e);
  *   nonfinite         walkers finished with RVM_STATUS_NONFINITE (any launch on the plan)
  *   unresolved        walkers finished with RVM_STATUS_UNRESOLVED
  *   refined           walker-direction passes of the adaptive resolution (extension + halvings)
- *   truncated         refinements cut short because the proposal's accept test fails whatever
- *                     further passes give (fused sampler launches): such a proposal
- *                     is rejected and keeps the last pass's logL
+ *   truncated         walker-directions whose refinement stopped because the proposal's accept
+ *                     test fails even at the upper bound on its logL both directions give
+ *                     (fused sampler launches): such a proposal is rejected and
+ *                     reports that upper bound
  * reset != 0: zero the counters and restore the hand-off workspace, after the stream's earlier work.
  * The samplers (rvmcmc) check this and raise on timeouts / non-finite results (mcmc.py:28-35: emcee
  * refuses NaN log-probabilities) rather than treating them as ordinary rejections. */
 int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
                     int64_t* unresolved, int64_t* refined, int64_t* truncated, void* stream);
+/* Kernel timing (benchmarks): the plan's next max_launches likelihood evaluations (any entry point)
+ * record HIP events on their stream around the likelihood kernel and around the refinement kernel
+ * that follows it (0..4096; 0 stops).  rvm_plan_kernel_times waits for those events and returns
+ * each evaluation's two kernel durations in ms (logl_ms[i], refine_ms[i]; either may be NULL; up
+ * to max of them, *n_out = how many), then stops timing. */
+int rvm_plan_time_kernels(rvm_plan* plan, int32_t max_launches);
+int rvm_plan_kernel_times(rvm_plan* plan, float* logl_ms, float* refine_ms, int32_t max, int32_t* n_out);
 /* Level-split hand-off waits give up after `seconds` without progress (default 2 s; > 0). */
 int rvm_plan_set_handoff_timeout(rvm_plan* plan, double seconds);
 

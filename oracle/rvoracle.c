@@ -991,31 +991,37 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* Adaptive resolution: restatement of the kernel's per-direction refinement (rvm_logl.hip,    */
-/* DESIGN.md §3).  A direction is integrated with the plan's step; its extrapolation error is   */
-/* estimated by the change of chi2 when the coarsest level is dropped,                          */
+/* Adaptive resolution: restatement of the kernel's per-walker refinement (rvm_logl.hip         */
+/* main pass + extension, rvm_refine.hip halving passes).  Each direction is      */
+/* integrated with the plan's step; its extrapolation error is estimated by the change of chi2   */
+/* when the coarsest level is dropped,                                                          */
 /*   est = sum_i |(r_i - o_i)^2 - (r3_i - o_i)^2| / sigma_i^2 / npoints,                        */
 /* r = all levels' Richardson RV, r3 = the finer nl - 1 levels' (their own Lagrange weights).   */
-/* Above the bound (est > tol_dir):                                                             */
+/* A direction above the bound (est > tol_dir, a non-finite pass, or past the eccentricity      */
+/* guard) is OPEN:                                                                              */
 /*  stage 1, the extension (ext_mult > 0): one more level, ext_mult steps per base step, joins  */
-/*   the stored levels: r5 = Richardson over all nl + 1 levels.  Accepted (chi2 from r5) when    */
-/*     sum |(r5 - o)^2 - (r - o)^2| / s2 <= EXT_ACCEPT * tol_dir * npoints                        */
+/*   the stored levels: r5 = Richardson over all nl + 1 levels.  Settled (chi2 from r5) when     */
+/*     dd = sum |(r5 - o)^2 - (r - o)^2| / s2 <= EXT_ACCEPT * tol_dir * npoints                   */
 /*   -- the change of chi2 the extension brought, an estimate of the main pass's own error (and  */
 /*   a conservative one of r5's: measured, r5's error stays below 2.6 tol_dir wherever this      */
 /*   holds);                                                                        */
-/*  stages 2..: every step halved (level k: mult 2^rf steps per base step, rf = 1..rf_max) while  */
-/*   est > tol_dir; still above after rf_max: RVO_UNRESOLVED.                                   */
-/* Certain rejects (a sampler's accept inputs given: dmode 1 emcee stretch, 2 MH): after an      */
-/* extension that does not settle the direction (with its chi2, d2 = the extension's change and  */
-/* est the main pass's), and after a                                                            */
-/* halving pass whose estimate is still above the bound, the direction stops (status OK, this    */
-/* pass's chi2) when the accept test fails even at lp_hi = -(chi2 - min(d2, CUT_EST_FACTOR est)) */
-/* / npoints, d2 = the pass's change of chi2 from the previous pass (the main pass for rf = 1),  */
-/*   d2 = sum |(r - o)^2 - (r_prev - o)^2| / s2, est the pass's estimate (both before / npoints). */
-/* ecc_guard > 0: a walker with a planet of e > ecc_guard counts as above the bound after the    */
-/* main pass whatever its estimate (it gets the extension; the estimate under-reads there).     */
-/* An encounter ends the direction at once; a non-finite RV (the fixed step blowing up on an    */
-/* extreme orbit) counts as above the bound and refines on (UNRESOLVED if it never settles).    */
+/*  stages 2..: passes with every step halved (level k: mult 2^rf steps per base step, rf = 1..  */
+/*   rf_max) over every direction still open, until est <= tol_dir; still open after rf_max:     */
+/*   RVO_UNRESOLVED.                                                                             */
+/* The walker's two directions advance through the stages together (round 4): an encounter in   */
+/* either ends the walker (ENCOUNTER), and the certain-reject test (a sampler's accept inputs    */
+/* given: dmode 1 emcee stretch, 2 MH) runs on the WALKER after the extension stage and after    */
+/* each halving stage while a direction is open: with each direction's lower bound on its chi2   */
+/*   lb = max(0, chi2 - min(d, CUT_EST_FACTOR est_raw))                                          */
+/* of an OPEN direction (chi2 of its last stage; d = the change that stage brought: the          */
+/* extension's dd, a halving pass's step-doubling change from the previous pass's RV, none for   */
+/* the main pass; est_raw = that stage's estimate -- the main pass's for the extension; lb = 0    */
+/* after a non-finite pass) and lb = chi2 of a settled one, the walker stops when               */
+/* its accept test fails even at lp_hi = -(lb_f + lb_b) / npoints and reports lp_hi (each        */
+/* direction's chi2 := its lb): rejected whatever further passes would give.                    */
+/* ecc_guard > 0: a walker with a planet of e > ecc_guard counts as open after the main pass     */
+/* whatever its estimate (it gets the extension; the estimate under-reads there).               */
+/* A non-finite pass (the fixed step blowing up on an extreme orbit) counts as open (lb 0).     */
 /* ------------------------------------------------------------------------------------------ */
 enum { RVO_UNRESOLVED = 4 };
 #ifndef EXT_ACCEPT /* (overridable for studies of the rule: -DEXT_ACCEPT=...) */
@@ -1042,156 +1048,188 @@ static int decide_accepts(const rvo_decide* dc, double lp) {
     return exp(lp - dc->lnp0) > dc->u;
 }
 
-static int whx_direction_adapt(int np, const double* pl, double hill_factor, const double* at, const double* ob,
-                               const double* s2, int cnt, double sign, double dt, int nl, const int* mult, int ext_mult,
-                               double tol_dir, int rf_max, double npoints, const rvo_decide* dc, double ecc_guard,
-                               double* chi2_out, int* stage_out, double* est_out, double* margin_out, int* cut_out) {
+/* the plan shared by both directions of a walker */
+typedef struct {
+    int np;
+    const double* pl;
+    double hill_factor, dt, tol_dir, npoints, ecc_guard;
+    int nl, ext_mult, rf_max, adaptive, ext;
+    const int* mult;
     double w[8], w3[8], w5[9];
-    rvo_richardson_weights_seq(nl, mult, w);
-    w3[0] = 0.0;
-    if (nl >= 2) rvo_richardson_weights_seq(nl - 1, mult + 1, w3 + 1);
-    const int ext = ext_mult > 0 && rf_max > 0 && nl >= 2 && nl < 8;
-    if (ext) {
-        int m5[9];
-        for (int k = 0; k < nl; k++) m5[k] = mult[k];
-        m5[nl] = ext_mult;
-        rvo_richardson_weights_seq(nl + 1, m5, w5);
-    }
-    double* lv = (double*)malloc(sizeof(double) * (size_t)(9 * cnt + 1));
-    double* lv0 = (double*)malloc(sizeof(double) * (size_t)(8 * cnt + 1)); /* the main pass's levels */
-    double* prev = (double*)malloc(sizeof(double) * (size_t)(cnt + 1));   /* the last pass's RV */
-    int st = RVO_OK, stage = 0;
-    *cut_out = 0;
-    double chi2 = 0.0, est = 0.0, margin = INFINITY;
-    const int adaptive = nl >= 2 && tol_dir < INFINITY;
-    for (int rf = 0; rf <= rf_max; rf++) {
-        st = RVO_OK;
-        for (int k = 0; k < nl; k++) {
-            const int s = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, mult[k] << rf, lv + (size_t)k * cnt);
-            if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
-        }
-        if (st == RVO_ENCOUNTER || (st != RVO_OK && !adaptive)) break;
-        /* a non-finite pass (the fixed step blowing up on an extreme orbit) refines on */
-        const int bad = st != RVO_OK;
-        st = RVO_OK;
-        if (!bad) {
-            chi2 = 0.0;
-            est = 0.0;
-            double d2 = 0.0;
-            for (int i = 0; i < cnt; i++) {
-                double r = 0.0, r3 = 0.0;
-                for (int k = 0; k < nl; k++) r += w[k] * lv[(size_t)k * cnt + i];
-                for (int k = 1; k < nl; k++) r3 += w3[k] * lv[(size_t)k * cnt + i];
-                chi2 += (r - ob[i]) * (r - ob[i]) / s2[i];
-                est += fabs((r - r3) * ((r - ob[i]) + (r3 - ob[i]))) / s2[i];
-                if (rf > 0) d2 += fabs((r - prev[i]) * ((r - ob[i]) + (prev[i] - ob[i]))) / s2[i];
-                prev[i] = r;
-            }
-            const double est_raw = est;
-            est /= npoints;
-            if (nl >= 2 && tol_dir < INFINITY && margin_of(est, tol_dir) < margin) margin = margin_of(est, tol_dir);
-            /* the eccentricity guard: an orbit whose pericentre passage is much quicker than the
-             * plan's reference orbit always gets the extension (the estimate can miss there) */
-            int eflag = 0;
-            if (rf == 0 && ext && ecc_guard > 0.0) {
-                double e2 = 0.0;
-                for (int p = 0; p < np; p++) {
-                    const double h = pl[p * RVO_PSTRIDE + 2], k = pl[p * RVO_PSTRIDE + 3];
-                    if (h * h + k * k > e2) e2 = h * h + k * k;
-                }
-                eflag = e2 > ecc_guard * ecc_guard;
-                if (margin_of(e2, ecc_guard * ecc_guard) < margin) margin = margin_of(e2, ecc_guard * ecc_guard);
-            }
-            if (nl < 2 || (!(est > tol_dir) && !eflag)) break;
-            if (rf > 0 && ext_mult > 0 && dc != NULL && dc->mode != 0) {
-                const double lp_hi = -(chi2 - fmin(d2, CUT_EST_FACTOR * est_raw)) / npoints;
-                if (isfinite(lp_hi)) {
-                    const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0
-                                                         : lp_hi - dc->lnp0;
-                    const double lu = log(dc->u);
-                    const double mg = fabs(lnpdiff - lu) / (1.0 + fabs(lu));
-                    if (mg < margin) margin = mg;
-                    if (!decide_accepts(dc, lp_hi)) { /* a certain reject: keep this pass */
-                        *cut_out = 1;
-                        break;
-                    }
-                }
-            }
-        } else {
-            chi2 = NAN;
-            est = NAN;
-            for (int i = 0; i < cnt; i++) prev[i] = NAN;
-        }
-        if (rf == 0 && ext) {
-            /* stage 1: the extension level over the main pass's stored levels */
-            stage = 1;
-            memcpy(lv0, lv, sizeof(double) * (size_t)nl * cnt);
-            double* lx = lv + (size_t)nl * cnt;
-            const int sx = wh_direction(np, pl, hill_factor, at, cnt, sign, dt, ext_mult, lx);
-            if (sx == RVO_ENCOUNTER) {
-                st = sx;
-                break;
-            }
-            if (sx == RVO_OK && !bad) {
-                double c5 = 0.0, dd = 0.0;
-                for (int i = 0; i < cnt; i++) {
-                    double r = 0.0, r5 = 0.0;
-                    for (int k = 0; k < nl; k++) r += w[k] * lv0[(size_t)k * cnt + i];
-                    for (int k = 0; k < nl; k++) r5 += w5[k] * lv0[(size_t)k * cnt + i];
-                    r5 += w5[nl] * lx[i];
-                    const double q = r5 - ob[i];
-                    c5 += (q * q) / s2[i];
-                    dd += fabs((r5 - r) * (q + (r - ob[i]))) / s2[i];
-                }
-                const double bx = EXT_ACCEPT * tol_dir * npoints;
-                if (margin_of(dd, bx) < margin) margin = margin_of(dd, bx);
-                if (dd <= bx) {
-                    chi2 = c5;
-                    est = dd / npoints;
-                    break;
-                }
-                /* a certain reject already after the extension: the accept test fails even at
-                 * lp_hi = -(c5 - min(dd, CUT_EST_FACTOR est)) / npoints (dd: the change the
-                 * extension brought, est: the main pass's estimate) -- keep the extension's chi2 */
-                if (dc != NULL && dc->mode != 0) {
-                    const double lp_hi = -(c5 - fmin(dd, CUT_EST_FACTOR * est * npoints)) / npoints;
-                    if (isfinite(lp_hi)) {
-                        const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0
-                                                             : lp_hi - dc->lnp0;
-                        const double lu = log(dc->u);
-                        const double mg = fabs(lnpdiff - lu) / (1.0 + fabs(lu));
-                        if (mg < margin) margin = mg;
-                        if (!decide_accepts(dc, lp_hi)) {
-                            chi2 = c5;
-                            *cut_out = 1;
-                            break;
-                        }
-                    }
-                }
-            }
-        }
-        if (rf == rf_max) {
-            st = RVO_UNRESOLVED;
-            break;
-        }
-        stage = (ext ? 2 : 1) + rf;
-    }
-    free(lv);
-    free(lv0);
-    free(prev);
-    *chi2_out = chi2;
-    *stage_out = stage;
-    *est_out = est;
-    *margin_out = margin;
-    return st;
+} rvo_plan_ctx;
+
+/* one direction's inputs, scratch and refinement state */
+typedef struct {
+    const double *at, *ob, *s2;
+    int cnt;
+    double sign;
+    double *lv0, *lv, *prev; /* main pass's levels (+ the extension), a halving pass's, the last RV */
+    int st, open, bad, stage, cut;
+    double chi2, lb, est, est_raw, margin;
+} rvo_dir;
+
+static double lb_of(double chi2, double d, double est_raw) {
+    const double b = chi2 - fmin(d, CUT_EST_FACTOR * est_raw);
+    return b > 0.0 ? b : 0.0;
 }
+
+/* stage 0: the plan's step */
+static void dir_main(const rvo_plan_ctx* X, rvo_dir* D) {
+    int st = RVO_OK;
+    for (int k = 0; k < X->nl; k++) {
+        const int s = wh_direction(X->np, X->pl, X->hill_factor, D->at, D->cnt, D->sign, X->dt, X->mult[k],
+                                   D->lv0 + (size_t)k * D->cnt);
+        if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
+    }
+    if (st == RVO_ENCOUNTER || (st != RVO_OK && !X->adaptive)) {
+        D->st = st;
+        return;
+    }
+    D->bad = st != RVO_OK;
+    if (D->bad) {
+        D->chi2 = D->est = D->est_raw = NAN;
+        D->lb = 0.0;
+        for (int i = 0; i < D->cnt; i++) D->prev[i] = NAN;
+        D->open = 1;
+        return;
+    }
+    double chi2 = 0.0, est = 0.0;
+    for (int i = 0; i < D->cnt; i++) {
+        double r = 0.0, r3 = 0.0;
+        for (int k = 0; k < X->nl; k++) r += X->w[k] * D->lv0[(size_t)k * D->cnt + i];
+        for (int k = 1; k < X->nl; k++) r3 += X->w3[k] * D->lv0[(size_t)k * D->cnt + i];
+        chi2 += (r - D->ob[i]) * (r - D->ob[i]) / D->s2[i];
+        est += fabs((r - r3) * ((r - D->ob[i]) + (r3 - D->ob[i]))) / D->s2[i];
+        D->prev[i] = r;
+    }
+    D->chi2 = chi2;
+    D->est_raw = est;
+    D->est = est / X->npoints;
+    D->lb = chi2;
+    if (!X->adaptive) return;
+    if (margin_of(D->est, X->tol_dir) < D->margin) D->margin = margin_of(D->est, X->tol_dir);
+    /* the eccentricity guard: an orbit whose pericentre passage is much quicker than the plan's
+     * reference orbit always gets the extension (the estimate can miss there) */
+    int eflag = 0;
+    if (X->ext && X->ecc_guard > 0.0) {
+        double e2 = 0.0;
+        for (int p = 0; p < X->np; p++) {
+            const double h = X->pl[p * RVO_PSTRIDE + 2], k = X->pl[p * RVO_PSTRIDE + 3];
+            if (h * h + k * k > e2) e2 = h * h + k * k;
+        }
+        eflag = e2 > X->ecc_guard * X->ecc_guard;
+        const double mg = margin_of(e2, X->ecc_guard * X->ecc_guard);
+        if (mg < D->margin) D->margin = mg;
+    }
+    D->open = D->est > X->tol_dir || eflag;
+    if (D->open) D->lb = lb_of(chi2, INFINITY, est);
+}
+
+/* stage 1: the extension level joined to the main pass's levels */
+static void dir_extend(const rvo_plan_ctx* X, rvo_dir* D) {
+    D->stage = 1;
+    double* lx = D->lv0 + (size_t)X->nl * D->cnt;
+    const int sx = wh_direction(X->np, X->pl, X->hill_factor, D->at, D->cnt, D->sign, X->dt, X->ext_mult, lx);
+    if (sx == RVO_ENCOUNTER) {
+        D->st = sx;
+        D->open = 0;
+        return;
+    }
+    if (sx != RVO_OK || D->bad) return; /* (refines on; lb as the main pass left it) */
+    double c5 = 0.0, dd = 0.0;
+    for (int i = 0; i < D->cnt; i++) {
+        double r = 0.0, r5 = 0.0;
+        for (int k = 0; k < X->nl; k++) r += X->w[k] * D->lv0[(size_t)k * D->cnt + i];
+        for (int k = 0; k < X->nl; k++) r5 += X->w5[k] * D->lv0[(size_t)k * D->cnt + i];
+        r5 += X->w5[X->nl] * lx[i];
+        const double q = r5 - D->ob[i];
+        c5 += (q * q) / D->s2[i];
+        dd += fabs((r5 - r) * (q + (r - D->ob[i]))) / D->s2[i];
+    }
+    if (!isfinite(c5) || !isfinite(dd)) return; /* (refines on; lb as the main pass left it) */
+    const double bx = EXT_ACCEPT * X->tol_dir * X->npoints;
+    if (margin_of(dd, bx) < D->margin) D->margin = margin_of(dd, bx);
+    D->chi2 = c5;
+    if (dd <= bx) {
+        D->est = dd / X->npoints;
+        D->open = 0;
+        D->lb = c5;
+    } else {
+        D->lb = lb_of(c5, dd, D->est_raw);
+    }
+}
+
+/* stage 1 + rf: every step halved rf times */
+static void dir_halve(const rvo_plan_ctx* X, rvo_dir* D, int rf) {
+    D->stage = (X->ext ? 1 : 0) + rf;
+    int st = RVO_OK;
+    for (int k = 0; k < X->nl; k++) {
+        const int s = wh_direction(X->np, X->pl, X->hill_factor, D->at, D->cnt, D->sign, X->dt, X->mult[k] << rf,
+                                   D->lv + (size_t)k * D->cnt);
+        if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
+    }
+    if (st == RVO_ENCOUNTER) {
+        D->st = st;
+        D->open = 0;
+        return;
+    }
+    if (st != RVO_OK) { /* a non-finite pass refines on */
+        D->chi2 = D->est = D->est_raw = NAN;
+        D->lb = 0.0;
+        for (int i = 0; i < D->cnt; i++) D->prev[i] = NAN;
+        return;
+    }
+    double c2 = 0.0, e2 = 0.0, d2 = 0.0;
+    for (int i = 0; i < D->cnt; i++) {
+        double r = 0.0, r3 = 0.0;
+        for (int k = 0; k < X->nl; k++) r += X->w[k] * D->lv[(size_t)k * D->cnt + i];
+        for (int k = 1; k < X->nl; k++) r3 += X->w3[k] * D->lv[(size_t)k * D->cnt + i];
+        c2 += (r - D->ob[i]) * (r - D->ob[i]) / D->s2[i];
+        e2 += fabs((r - r3) * ((r - D->ob[i]) + (r3 - D->ob[i]))) / D->s2[i];
+        d2 += fabs((r - D->prev[i]) * ((r - D->ob[i]) + (D->prev[i] - D->ob[i]))) / D->s2[i];
+        D->prev[i] = r;
+    }
+    D->chi2 = c2;
+    D->est_raw = e2;
+    D->est = e2 / X->npoints;
+    if (margin_of(D->est, X->tol_dir) < D->margin) D->margin = margin_of(D->est, X->tol_dir);
+    if (!(D->est > X->tol_dir)) {
+        D->open = 0;
+        D->lb = c2;
+    } else {
+        D->lb = lb_of(c2, d2, e2); /* (d2 NaN after a non-finite pass: fmin takes the estimate) */
+    }
+}
+
+/* the walker's certain-reject test; returns 1 (and stops every direction) on a cut */
+static int walker_cut(const rvo_plan_ctx* X, rvo_dir* D, const rvo_decide* dc) {
+    if (dc == NULL || dc->mode == 0 || X->ext_mult <= 0) return 0;
+    const double lp_hi = -((D[0].lb + D[1].lb) / X->npoints);
+    if (!isfinite(lp_hi)) return 0;
+    const double lnpdiff = dc->mode == 1 ? (double)(dc->dim - 1) * log(dc->z) + lp_hi - dc->lnp0 : lp_hi - dc->lnp0;
+    const double lu = log(dc->u);
+    const double mg = fabs(lnpdiff - lu) / (1.0 + fabs(lu));
+    for (int d = 0; d < 2; d++)
+        if (mg < D[d].margin) D[d].margin = mg;
+    if (decide_accepts(dc, lp_hi)) return 0;
+    for (int d = 0; d < 2; d++) {
+        D[d].cut = D[d].open;
+        D[d].open = 0;
+        D[d].chi2 = D[d].lb;
+    }
+    return 1;
+}
+
+static int any_enc(const rvo_dir* D) { return D[0].st == RVO_ENCOUNTER || D[1].st == RVO_ENCOUNTER; }
+static int any_open(const rvo_dir* D) { return D[0].open || D[1].open; }
 
 /* logp with adaptive resolution: rf_used[2] / est[2] (fwd, bwd) report the stage reached (0 the
  * plan's step, 1 the extension, 2.. halvings; without the extension 1.. halvings) and
  * the final estimates.  Status: PRIOR, else the forward direction's non-OK status, else the
  * backward one's (the kernel's direction meeting).  est[4]: the final estimates (fwd, bwd) and the
- * closest any pass came to the bound, min |est / tol_dir - 1| (fwd, bwd): a refinement decision
- * a second implementation may take the other way when that is at roundoff level. */
+ * closest any decision came to its bound, min |x / bound - 1| (fwd, bwd): a decision a second
+ * implementation may take the other way when that is at roundoff level.  cut[2]: the directions
+ * a certain reject stopped. */
 int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double hill_factor, const double* t,
                        const double* rvobs, const double* err, int n, double npoints, double dt, int nl,
                        const int* mult, int ext_mult, double tol_dir, int rf_max, const rvo_decide* dc,
@@ -1204,12 +1242,33 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
         *logl = -INFINITY;
         return RVO_PRIOR;
     }
+    rvo_plan_ctx X;
+    memset(&X, 0, sizeof X);
+    X.np = np;
+    X.pl = pl;
+    X.hill_factor = hill_factor;
+    X.dt = dt;
+    X.tol_dir = tol_dir;
+    X.npoints = npoints;
+    X.ecc_guard = ecc_guard;
+    X.nl = nl;
+    X.mult = mult;
+    X.rf_max = rf_max;
+    X.adaptive = nl >= 2 && tol_dir < INFINITY;
+    X.ext = ext_mult > 0 && rf_max > 0 && nl >= 2 && nl < 8;
+    X.ext_mult = X.ext ? ext_mult : 0;
+    rvo_richardson_weights_seq(nl, mult, X.w);
+    if (nl >= 2) rvo_richardson_weights_seq(nl - 1, mult + 1, X.w3 + 1);
+    if (X.ext) {
+        int m5[9];
+        for (int k = 0; k < nl; k++) m5[k] = mult[k];
+        m5[nl] = ext_mult;
+        rvo_richardson_weights_seq(nl + 1, m5, X.w5);
+    }
     int* idx = (int*)malloc(sizeof(int) * (size_t)(n + 1));
-    double* at = (double*)malloc(sizeof(double) * (size_t)(3 * n + 3));
-    double* ob = at + n + 1;
-    double* s2 = ob + n + 1;
-    int sd[2] = {RVO_OK, RVO_OK};
-    double chi2[2] = {0.0, 0.0};
+    rvo_dir D[2];
+    memset(D, 0, sizeof D);
+    double* buf[2];
     for (int dir = 0; dir < 2; dir++) {
         int cnt = 0;
         for (int i = 0; i < n; i++)
@@ -1223,26 +1282,60 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
             }
             idx[b + 1] = key;
         }
+        /* |t|, observed RV, sigma^2; the main pass's levels (+ the extension), a halving pass's
+         * levels, the last pass's RV */
+        buf[dir] = (double*)malloc(sizeof(double) * (size_t)((4 + 2 * nl + 1) * cnt + 1));
+        double* A = buf[dir];
+        double* ob = A + cnt;
+        double* s2 = ob + cnt;
         for (int a = 0; a < cnt; a++) {
-            at[a] = fabs(t[idx[a]]);
+            A[a] = fabs(t[idx[a]]);
             ob[a] = rvobs[idx[a]];
             s2[a] = err[idx[a]] * err[idx[a]];
         }
-        int rf = 0, ct = 0;
-        double e = 0.0, mg = INFINITY;
-        if (cnt)
-            sd[dir] = whx_direction_adapt(np, pl, hill_factor, at, ob, s2, cnt, dir == 0 ? 1.0 : -1.0, dt, nl, mult,
-                                          ext_mult, tol_dir, rf_max, npoints, dc, ecc_guard, &chi2[dir], &rf, &e, &mg,
-                                          &ct);
-        cut[dir] = ct;
-        rf_used[dir] = rf;
-        est[dir] = e;
-        est[2 + dir] = mg;
+        rvo_dir* d = &D[dir];
+        d->at = A;
+        d->ob = ob;
+        d->s2 = s2;
+        d->cnt = cnt;
+        d->sign = dir == 0 ? 1.0 : -1.0;
+        d->lv0 = s2 + cnt;
+        d->lv = d->lv0 + (size_t)(nl + 1) * cnt;
+        d->prev = d->lv + (size_t)nl * cnt;
+        d->st = RVO_OK;
+        d->margin = INFINITY;
+    }
+    for (int dir = 0; dir < 2; dir++)
+        if (D[dir].cnt) dir_main(&X, &D[dir]);
+    if (!any_enc(D) && X.ext) {
+        for (int dir = 0; dir < 2 && !any_enc(D); dir++)
+            if (D[dir].open) dir_extend(&X, &D[dir]);
+    }
+    if (!any_enc(D) && X.adaptive) {
+        int rf = 0;
+        while (any_open(D) && !walker_cut(&X, D, dc)) {
+            if (rf == rf_max) {
+                for (int dir = 0; dir < 2; dir++)
+                    if (D[dir].open) D[dir].st = RVO_UNRESOLVED;
+                break;
+            }
+            rf++;
+            for (int dir = 0; dir < 2 && !any_enc(D); dir++)
+                if (D[dir].open) dir_halve(&X, &D[dir], rf);
+            if (any_enc(D)) break;
+        }
+    }
+    for (int dir = 0; dir < 2; dir++) {
+        cut[dir] = D[dir].cut;
+        rf_used[dir] = D[dir].stage;
+        est[dir] = D[dir].est;
+        est[2 + dir] = D[dir].margin;
     }
     free(idx);
-    free(at);
-    int st = sd[0] != RVO_OK ? sd[0] : sd[1];
-    const double lp = -((chi2[1] + chi2[0]) / npoints);
+    free(buf[0]);
+    free(buf[1]);
+    int st = D[0].st != RVO_OK ? D[0].st : D[1].st;
+    const double lp = -((D[1].chi2 + D[0].chi2) / npoints);
     if (st == RVO_OK && !isfinite(lp)) st = RVO_NONFINITE;
     *logl = st == RVO_OK ? lp : -INFINITY;
     return st;

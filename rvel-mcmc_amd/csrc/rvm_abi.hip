@@ -18,6 +18,8 @@
 namespace rvm {
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
                        double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
+hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
+                         int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
 hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
                                   uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
                                   double* z, hipStream_t st);
@@ -62,10 +64,29 @@ struct rvm_plan {
     void* lvmem = nullptr;       // level-split layout workspace (DevPlan::lv_*), when usable
     size_t lv_bytes = 0;
     void* xmem = nullptr;        // the extension's stored levels (DevPlan::lvx), when the plan has one
+    void* rqmem = nullptr;       // the refinement kernel's work lists (DevPlan::rq_*), adaptive plans
     unsigned long long* slots = nullptr;  // [max_walkers] direction meeting slots (rvm_logl.hip)
     int32_t max_walkers = 0;
     int32_t steps[2] = {0, 0};
+    // rvm_plan_time_kernels: event triples around the likelihood and refinement kernels of the next
+    // `cap` launches (the kernels' own durations on their stream, for the bench's roofline)
+    mutable std::vector<hipEvent_t> tev;
+    mutable int32_t tcap = 0, tn = 0;
 };
+
+// One likelihood evaluation as every entry point runs it: the likelihood kernel, then (adaptive
+// plans) the refinement kernel for the walkers it handed on, stream-ordered.
+static hipError_t run_logl(const rvm_plan* plan, int W, const double* params, double hill_factor, double* logl,
+                           int32_t* status, double* rv_out, const rvm::StretchArgs& sa, hipStream_t st) {
+    const bool tm = plan->tn < plan->tcap;
+    if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn], st);
+    hipError_t e = rvm::launch_logl(plan->dev, W, params, hill_factor, plan->slots, logl, status, rv_out, sa, st);
+    if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 1], st);
+    if (e == hipSuccess) e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, st);
+    if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 2], st);
+    if (tm) plan->tn++;
+    return e;
+}
 
 static thread_local std::string g_err;
 
@@ -104,8 +125,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     }
     if (!(cfg->period_hint >= 0.0) || !std::isfinite(cfg->period_hint))
         return fail(-1, "rvm_plan_create: period_hint must be >= 0");
-    if (std::isnan(cfg->resolve_tol) || cfg->resolve_max < 0 || cfg->resolve_max > 8)
-        return fail(-1, "rvm_plan_create: resolve_tol must be a number and resolve_max in 0..8");
+    if (std::isnan(cfg->resolve_tol) || cfg->resolve_max < 0 || cfg->resolve_max > RVM_RESOLVE_MAX_LIMIT)
+        return fail(-1, "rvm_plan_create: resolve_tol must be a number and resolve_max in 0..12");
     const int rmax = cfg->resolve_tol > 0.0 ? cfg->resolve_max : 0;
     for (int i = 0; i < n_obs; i++) {
         if (!std::isfinite(t[i]) || !std::isfinite(rv[i]) || !std::isfinite(sigma[i]))
@@ -390,12 +411,35 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             P.lvx_stride = max_walkers;
         }
     }
+    // the refinement kernel's work lists (rvm_refine.hip): sizes [4] (zero), walkers [3][max_walkers],
+    // settled directions' chi2 [2][max_walkers]
+    P.rq_n = nullptr;
+    P.rq_w = nullptr;
+    P.rq_c = nullptr;
+    P.rq_cap = 0;
+    if (P.rmax > 0) {
+        const size_t b_c = 2 * (size_t)max_walkers * sizeof(double);
+        const size_t b_w = 3 * (size_t)max_walkers * sizeof(int32_t);
+        if (hipMalloc(&plan->rqmem, b_c + b_w + 64) != hipSuccess ||
+            hipMemset(plan->rqmem, 0, b_c + b_w + 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipGetLastError();
+            rvm_plan_destroy(plan);
+            return fail(-3, "rvm_plan_create: hipMalloc of the refinement work lists failed");
+        }
+        unsigned char* base = reinterpret_cast<unsigned char*>(plan->rqmem);
+        P.rq_c = reinterpret_cast<double*>(base);
+        P.rq_w = reinterpret_cast<int32_t*>(base + b_c);
+        P.rq_n = reinterpret_cast<int32_t*>(base + b_c + b_w);
+        P.rq_cap = max_walkers;
+    }
     *out = plan;
     return 0;
 }
 
 void rvm_plan_destroy(rvm_plan* plan) {
     if (!plan) return;
+    for (hipEvent_t ev : plan->tev) (void)hipEventDestroy(ev);
+    if (plan->rqmem) (void)hipFree(plan->rqmem);
     if (plan->lvmem) (void)hipFree(plan->lvmem);
     if (plan->xmem) (void)hipFree(plan->xmem);
     if (plan->dmem) (void)hipFree(plan->dmem);
@@ -439,6 +483,38 @@ int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, in
     return 0;
 }
 
+int rvm_plan_time_kernels(rvm_plan* plan, int32_t max_launches) {
+    if (!plan) return fail(-1, "rvm_plan_time_kernels: null plan");
+    if (max_launches < 0 || max_launches > 4096) return fail(-1, "rvm_plan_time_kernels: max_launches out of range");
+    while ((int32_t)plan->tev.size() < 3 * max_launches) {
+        hipEvent_t ev;
+        const hipError_t e = hipEventCreate(&ev);
+        if (e != hipSuccess) return hip_fail(e, "rvm_plan_time_kernels: hipEventCreate");
+        plan->tev.push_back(ev);
+    }
+    plan->tcap = max_launches;
+    plan->tn = 0;
+    return 0;
+}
+
+int rvm_plan_kernel_times(rvm_plan* plan, float* logl_ms, float* refine_ms, int32_t max, int32_t* n_out) {
+    if (!plan || max < 0) return fail(-1, "rvm_plan_kernel_times: bad arguments");
+    const int n = std::min(plan->tn, max);
+    for (int i = 0; i < n; i++) {
+        hipError_t e = hipEventSynchronize(plan->tev[3 * i + 2]);
+        float a = 0.0f, b = 0.0f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&a, plan->tev[3 * i], plan->tev[3 * i + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&b, plan->tev[3 * i + 1], plan->tev[3 * i + 2]);
+        if (e != hipSuccess) return hip_fail(e, "rvm_plan_kernel_times");
+        if (logl_ms) logl_ms[i] = a;
+        if (refine_ms) refine_ms[i] = b;
+    }
+    if (n_out) *n_out = n;
+    plan->tn = 0;
+    plan->tcap = 0;
+    return 0;
+}
+
 int rvm_plan_set_handoff_timeout(rvm_plan* plan, double seconds) {
     if (!plan) return fail(-1, "rvm_plan_set_handoff_timeout: null plan");
     if (!(seconds > 0.0) || !(seconds < 1e9)) return fail(-1, "rvm_plan_set_handoff_timeout: seconds out of range");
@@ -465,8 +541,7 @@ int rvm_logl_batch(const rvm_plan* plan, int32_t n_walkers, const double* params
     if (!params || !logl_out || !status_out) return fail(-1, "rvm_logl_batch: null buffer");
     if (!(hill_factor >= 0.0)) return fail(-1, "rvm_logl_batch: hill_factor must be >= 0");
     rvm::StretchArgs none{};
-    hipError_t e = rvm::launch_logl(plan->dev, n_walkers, params, hill_factor, plan->slots, logl_out, status_out,
-                                    rv_out, none, (hipStream_t)stream);
+    hipError_t e = run_logl(plan, n_walkers, params, hill_factor, logl_out, status_out, rv_out, none, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "rvm_logl_batch");
     return 0;
 }
@@ -504,8 +579,7 @@ int rvm_stretch_half_step(const rvm_plan* plan, const rvm_param_map* map, int32_
         sa.src[r] = k < 0 ? -1 : k;
         sa.base[r] = r < rows ? map->base[r] : 0.0;
     }
-    hipError_t e = rvm::launch_logl(plan->dev, n_s0, nullptr, hill_factor, plan->slots, lnp_new_out, status_out,
-                                    nullptr, sa, (hipStream_t)stream);
+    hipError_t e = run_logl(plan, n_s0, nullptr, hill_factor, lnp_new_out, status_out, nullptr, sa, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_half_step");
 }
 
@@ -552,8 +626,7 @@ int rvm_stretch_iteration_begin(const rvm_plan* plan, const rvm_param_map* map, 
         sa.src[r] = k < 0 ? -1 : k;
         sa.base[r] = r < rows ? map->base[r] : 0.0;
     }
-    hipError_t e = rvm::launch_logl(plan->dev, 3 * n_loc, nullptr, hill_factor, plan->slots, lnp_spec, status_spec,
-                                    nullptr, sa, (hipStream_t)stream);
+    hipError_t e = run_logl(plan, 3 * n_loc, nullptr, hill_factor, lnp_spec, status_spec, nullptr, sa, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_stretch_iteration_begin");
 }
 
@@ -669,8 +742,7 @@ int rvm_mh_step(const rvm_plan* plan, const rvm_param_map* map, int32_t n_params
         sa.src[r] = k < 0 ? -1 : k;
         sa.base[r] = r < rows ? map->base[r] : 0.0;
     }
-    hipError_t e = rvm::launch_logl(plan->dev, n_chains, nullptr, hill_factor, plan->slots, lnp_new_out, status_out,
-                                    nullptr, sa, (hipStream_t)stream);
+    hipError_t e = run_logl(plan, n_chains, nullptr, hill_factor, lnp_new_out, status_out, nullptr, sa, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_mh_step");
 }
 
@@ -698,8 +770,7 @@ int rvm_smala_stencil_logl(const rvm_plan* plan, const rvm_param_map* map, int32
         sa.src[r] = k < 0 ? -1 : k;
         sa.base[r] = r < rows ? map->base[r] : 0.0;
     }
-    hipError_t e = rvm::launch_logl(plan->dev, (int)W, nullptr, hill_factor, plan->slots, logl_out, status_out, rv_out,
-                                    sa, (hipStream_t)stream);
+    hipError_t e = run_logl(plan, (int)W, nullptr, hill_factor, logl_out, status_out, rv_out, sa, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_stencil_logl");
 }
 

@@ -69,6 +69,15 @@ struct DevPlan {
     // e^2 above it counts as above the bound after the main pass (it gets the extension)
     double e2_guard;
     int32_t lvx_emax, lvx_stride;
+    // walkers handed from the likelihood kernel to the refinement kernel (rvm_refine.hip): a walker
+    // with a direction still open after the main pass and the extension (and no certain reject) is
+    // appended to list 0 (both directions open), 1 (forward only) or 2 (backward only):
+    // rq_n[0..2] the list sizes (the refinement kernel resets them; rq_n[3] counts its blocks),
+    // rq_w [3][rq_cap] walker slots, rq_c [2][rq_cap] the settled direction's chi2 (fwd, bwd)
+    int32_t* rq_n;
+    int32_t* rq_w;
+    double* rq_c;
+    int32_t rq_cap;
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
     // [3] walker-direction refinement passes (extension + halvings), [4] refinements cut short as

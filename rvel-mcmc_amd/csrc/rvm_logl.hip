@@ -30,9 +30,7 @@
 // (The default -ffp-contract=fast fuses across statements depending on the surrounding code.)
 #pragma clang fp contract(on)
 
-#include "rvm_device.h"
-#include "rvm_internal.h"
-#include "rvm_stretch.h"
+#include "rvm_walker.h"
 
 namespace rvm {
 
@@ -50,117 +48,6 @@ __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 #define PROF_COUNT(var)
 #endif
 
-// One epoch-to-epoch segment of ns Wisdom-Holman kick-drift-kick steps of size h (ns >= 1,
-// wave-uniform): K(h/2) [D(h) K(h)]^(ns-1) D(h) K(h/2).  kp holds the interaction at the current
-// positions (rvm_device.h kick_prep): evaluated at the end of the previous segment, it serves this
-// segment's opening half kick, and leaves holding the one at the next epoch.  (The step loop is
-// unrolled by hand: the compiler will not unroll a runtime trip count around the convergent DPP /
-// ballot operations.)
-template <int NT, bool GATED, bool D3, int NP, int L>
-__device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, bool& bad) {
-    lane_set_step(s, h);
-    const VConsts vk = vconsts_for<NT>();  // loop-invariant VGPR constants
-    kick_apply<NP, true, D3>(s, kp);
-    int j = 0;
-    for (; j + 2 <= ns - 1; j += 2) {
-        drift<NT, GATED, D3>(s, h, bad, vk);
-        kp = kick_prep<NP, L, D3>(s, vk.c1875);
-        kick_apply<NP, false, D3>(s, kp);
-        drift<NT, GATED, D3>(s, h, bad, vk);
-        kp = kick_prep<NP, L, D3>(s, vk.c1875);
-        kick_apply<NP, false, D3>(s, kp);
-    }
-    if (j < ns - 1) {
-        drift<NT, GATED, D3>(s, h, bad, vk);
-        kp = kick_prep<NP, L, D3>(s, vk.c1875);
-        kick_apply<NP, false, D3>(s, kp);
-    }
-    drift<NT, GATED, D3>(s, h, bad, vk);
-    kp = kick_prep<NP, L, D3>(s, vk.c1875);
-    kick_apply<NP, true, D3>(s, kp);
-}
-
-// SPEC: run the segment with ungated drifts (rvm_device.h) and vote once at its end; if any lane
-// of the wave had a step that needs the general solver, restore the segment's initial state and
-// redo it gated.  Used on the fine levels, where such steps are rare.  Returns whether the
-// segment was redone (wave-uniform).  Either way every lane ends bit-identical to a gated run.
-template <int NT, bool SPEC, bool D3, int NP, int L>
-__device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int& redo) {
-    bool bad = false;
-    if constexpr (SPEC) {
-        const double rx = s.rx, ry = s.ry, vx = s.vx, vy = s.vy, r = s.r, ir = s.ir;
-        const double rz = s.rz, vz = s.vz;
-        const uint64_t encm = s.encm;
-        const KickPrep<NP> kp0 = kp;
-        segment_steps<NT, false, D3, NP, L>(s, kp, h, ns, bad);
-        if (__builtin_expect(ballot(bad) != 0, 0)) {
-            PROF_COUNT(redo);
-            s.rx = rx;
-            s.ry = ry;
-            s.vx = vx;
-            s.vy = vy;
-            s.rz = rz;
-            s.vz = vz;
-            s.r = r;
-            s.ir = ir;
-            s.encm = encm;
-            kp = kp0;
-            segment_steps<NT, true, D3, NP, L>(s, kp, h, ns, bad);
-            return true;
-        }
-    } else {
-        segment_steps<NT, true, D3, NP, L>(s, kp, h, ns, bad);
-    }
-    return false;
-}
-
-// kernel parameter row r of walker w: from the SoA input, or (fused sampler step) the row's fixed
-// value or the walker's proposal of the free parameter feeding it: MH (sa.mh_scale), or stretch
-// (kind 1 / 2: half 1's walker of a speculative iteration against its partner's rejected /
-// accepted position, StretchArgs)
-__device__ __forceinline__ double walker_param(bool mapped, const double* __restrict__ params, int W, int w,
-                                               const StretchArgs& sa, int r, double z, int j, int kind, double zp,
-                                               int jp) {
-    if (!mapped) return params[(size_t)r * W + w];
-    const int k = sa.src[r];
-    if (k < 0) return sa.base[r];
-    if (sa.fd_x) return fd_point(sa.fd_x, sa.fd_floor, sa.fd_rel, sa.fd_n, k, w);
-    if (sa.mh_scale)
-        return mh_q(sa.x[(size_t)k * sa.xstride + w], sa.mh_step, sa.mh_scale[k],
-                    mh_normal(sa.seed, (uint64_t)(sa.s0_begin + w), sa.iteration, k));
-    if (kind == 0) return stretch_q(sa.c[(size_t)j * sa.dim + k], z, sa.x[(size_t)k * sa.xstride + w]);
-    double c = sa.c0[(size_t)j * sa.dim + k];
-    if (kind == 2) c = stretch_q(sa.c[(size_t)jp * sa.dim + k], zp, c);  // q0(j): bit-identical to slot j's
-    return stretch_q(c, z, sa.x1[(size_t)k * sa.n_spec + w]);
-}
-
-// a fused launch's walker slot: its kind (0 = half-step / half 0, 1 / 2 = half 1 against its
-// partner's rejected / accepted position), walker index within its half, its stretch draws and
-// (kind 2) the partner's
-__device__ __forceinline__ void stretch_slot(const StretchArgs& sa, int wl, int& kind, int& wk, double& z, int& j,
-                                             double& zp, int& jp) {
-    const int nsp = sa.n_spec;
-    kind = nsp > 0 ? (wl < nsp ? 0 : (wl < 2 * nsp ? 1 : 2)) : 0;
-    wk = wl - kind * nsp;
-    zp = 0.0;
-    jp = 0;
-    if (kind == 0) {
-        stretch_draw(sa.seed, (uint64_t)(sa.s0_begin + wk), sa.iteration, sa.half, sa.a, sa.n1, z, j);
-    } else {
-        stretch_draw(sa.seed, (uint64_t)(sa.s1_begin + wk), sa.iteration, 1u, sa.a, sa.n1, z, j);
-        // the partner's own draws (half 0's keys are its global indices 0 .. n1-1)
-        if (kind == 2) stretch_draw(sa.seed, (uint64_t)j, sa.iteration, 0u, sa.a, sa.n1, zp, jp);
-    }
-}
-
-__device__ __forceinline__ double stage_row(bool stager, double* l_q, int GW, int gi, int r, double v) {
-    if (stager) l_q[r * GW + gi] = v;
-    return v;
-}
-
-// Direction results meet in one 64-bit slot per walker (plan workspace, RVM_SLOT_EMPTY between
-// launches): chi2 >= 0 for an OK direction, -status otherwise.
-#define RVM_SLOT_EMPTY 0x7FF4DEADBEEF0001ULL  // a NaN pattern no direction result can take
 
 // Level-split hand-off of level 1 (type-B block -> the unit's combiner): the star vx of walker w at
 // epoch e of direction d sits in P.lv_rv[(d lv_emax + e) lv_stride + w]; all-ones (a NaN no
@@ -183,10 +70,6 @@ struct SpinClock {
         return __builtin_amdgcn_s_memrealtime() - last > ticks;
     }
 };
-// per-direction flag bits of a walker (encflag / enc): 1 encounter, 2 prior, 4 unresolved after
-// the last refinement, 8 a hand-off of this launch gave up (the values are not trustworthy)
-#define RVM_ENC_UNRESOLVED 4
-#define RVM_ENC_FAULT 8
 
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
 template <int NP, bool D3, bool DEC>
@@ -321,12 +204,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // the estimate bound; the level-split combiners' verdicts (0 pending, 1 finished, 2 refine) and
     // their results for the refinement team
     __shared__ unsigned long long s_need[2];
-    __shared__ int s_vd[2];
     __shared__ double s_fchi[2][64];
     __shared__ int s_fenc[2][64];
     // (the early certain-reject test of the refinement team: the main pass's estimate and the
     // concurrent extension's chi2 and change, per unit and walker slot)
-    __shared__ double s_fx[3][2][64];
+    __shared__ double s_fx[1][2][64];
     double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
     // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
@@ -397,8 +279,21 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         constexpr int NI = (R + L - 1) / L;
 #pragma unroll
         for (int i = 0; i < NI; i++) {
-            const int r = L * i + pl_idx < R ? L * i + pl_idx : R - 1;
-            const double v = walker_param(true, params, W, wk, sa, r, zst, jst, kind, zp, jp);
+            // (the row's map entries selected with compile-time indices: a lane-dependent index into
+            // the kernel argument would make the compiler copy StretchArgs to scratch)
+            int k = -1;
+            double bs = 0.0;
+#pragma unroll
+            for (int q = 0; q < L; q++) {
+                const int rr = L * i + q < R ? L * i + q : R - 1;
+                if (pl_idx == q) {
+                    k = sa.src[rr];
+                    bs = sa.base[rr];
+                }
+            }
+            const double v = k < 0 ? bs
+                                   : mh_q(sa.x[(size_t)k * sa.xstride + wk], sa.mh_step, sa.mh_scale[k],
+                                          mh_normal(sa.seed, (uint64_t)(sa.s0_begin + wk), sa.iteration, k));
 #pragma unroll
             for (int q = 0; q < L; q++)
                 if (L * i + q < R) rowv[L * i + q] = grp_get<L>(v, q);
@@ -407,119 +302,17 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #pragma unroll
         for (int r = 0; r < R; r++) rowv[r] = walker_param(mapped, params, W, wk, sa, r, zst, jst, kind, zp, jp);
     }
-#define prm(r) stage_row(stager, l_q, GW, gi, (r), rowv[(r)])
+    if (stager) {
+#pragma unroll
+        for (int r = 0; r < R; r++) l_q[r * GW + gi] = rowv[r];
+    }
+    // ---- setup_sim: prior, Pal -> heliocentric (own planet) -> Jacobi; Hill exit (rvm_walker.h) ----
     Lane<NP> s;
-    double pa[NP], ph[NP], pk[NP], pl[NP], pix[NP], piy[NP];
     int status = RVM_STATUS_OK;
-#pragma unroll
-    for (int p = 0; p < NP; p++) {
-        s.m[p] = prm(PR * p + 0);
-        pa[p] = prm(PR * p + 1);
-        ph[p] = prm(PR * p + 2);
-        pk[p] = prm(PR * p + 3);
-        pl[p] = prm(PR * p + 4);
-        pix[p] = D3 ? prm(PR * p + 5) : 0.0;
-        piy[p] = D3 ? prm(PR * p + 6) : 0.0;
-        bool bad = !(pa[p] > 0.02) || !(s.m[p] > 5e-6) || !(ph[p] * ph[p] + pk[p] * pk[p] < 1.0) ||
-                   !isfinite(pl[p]);
-        if constexpr (D3) bad = bad || !(pix[p] * pix[p] + piy[p] * piy[p] < 4.0);  // state.py:311-313
-        if (bad) status = RVM_STATUS_PRIOR;
-    }
-    // the adaptive resolution's eccentricity guard (P.e2_guard): the walker's largest e^2
-    double e2w = 0.0;
-#pragma unroll
-    for (int p = 0; p < NP; p++) e2w = fmax(e2w, ph[p] * ph[p] + pk[p] * pk[p]);
-    PROF_T(t_p1);  // parameters read, prior checked
-    if (status != RVM_STATUS_OK) {  // keep the lane numerically benign; its result is discarded
-#pragma unroll
-        for (int p = 0; p < NP; p++) {
-            s.m[p] = 1e-3;
-            pa[p] = 1.0 + p;
-            ph[p] = 0.0;
-            pk[p] = 0.0;
-            pl[p] = 0.0;
-            pix[p] = 0.0;
-            piy[p] = 0.0;
-        }
-    }
-
-    // ---- setup_sim: Pal -> heliocentric (own planet) -> Jacobi; Hill-radius exit distance -------
-    s.p = pl_idx < NP ? pl_idx : NP - 1;
-    s.q = pl_idx;
-    double Mi[NP + 1];
-    Mi[0] = 1.0;
-    double hill = 0.0;
-#pragma unroll
-    for (int p = 0; p < NP; p++) {
-        Mi[p + 1] = Mi[p] + s.m[p];
-        const double rh = pa[p] * cbrt(s.m[p] / 3.0);
-        hill = rh > hill ? rh : hill;
-    }
-#pragma unroll
-    for (int p = 0; p <= NP; p++) s.iMi[p] = 1.0 / Mi[p];
-#pragma unroll
-    for (int p = 0; p < NP; p++) s.mu[p] = s.m[p] / Mi[p + 1];
-    s.dmin2 = (hill_factor * hill) * (hill_factor * hill);
-    double own_m = s.m[0], own_a = pa[0], own_h = ph[0], own_k = pk[0], own_l = pl[0], own_M = Mi[1];
-    double own_ix = pix[0], own_iy = piy[0];
-#pragma unroll
-    for (int p = 1; p < NP; p++) {
-        if (s.p == p) {
-            own_m = s.m[p];
-            own_a = pa[p];
-            own_h = ph[p];
-            own_k = pk[p];
-            own_l = pl[p];
-            own_M = Mi[p + 1];
-            own_ix = pix[p];
-            own_iy = piy[p];
-        }
-    }
-    s.GM = own_M;
-    double X, Y, VX, VY, Z = 0.0, VZ = 0.0;
-    pal_to_cart(1.0 + own_m, own_a, own_l, own_k, own_h, X, Y, VX, VY);
-    if constexpr (D3) {
-        if (own_ix != 0.0 || own_iy != 0.0) pal_incline(own_ix, own_iy, X, Y, Z, VX, VY, VZ);
-    }
-    {
-        // r'_p = x_p - (sum_{q<p} m_q x_q) / M_{p-1}   (heliocentric -> Jacobi)
-        double sx = 0.0, sy = 0.0, sz = 0.0, svx = 0.0, svy = 0.0, svz = 0.0;
-        double jx = X, jy = Y, jz = Z, jvx = VX, jvy = VY, jvz = VZ;
-#pragma unroll
-        for (int q = 0; q < NP - 1; q++) {
-            const double xq = grp_get<L>(X, q), yq = grp_get<L>(Y, q);
-            const double vxq = grp_get<L>(VX, q), vyq = grp_get<L>(VY, q);
-            sx += s.m[q] * xq;
-            sy += s.m[q] * yq;
-            svx += s.m[q] * vxq;
-            svy += s.m[q] * vyq;
-            if constexpr (D3) {
-                sz += s.m[q] * grp_get<L>(Z, q);
-                svz += s.m[q] * grp_get<L>(VZ, q);
-            }
-            if (s.p == q + 1) {
-                jx = X - sx * s.iMi[q + 1];
-                jy = Y - sy * s.iMi[q + 1];
-                jvx = VX - svx * s.iMi[q + 1];
-                jvy = VY - svy * s.iMi[q + 1];
-                if constexpr (D3) {
-                    jz = Z - sz * s.iMi[q + 1];
-                    jvz = VZ - svz * s.iMi[q + 1];
-                }
-            }
-        }
-        s.rx = jx;
-        s.ry = jy;
-        s.vx = jvx;
-        s.vy = jvy;
-        s.rz = D3 ? jz : 0.0;
-        s.vz = D3 ? jvz : 0.0;
-    }
-    PROF_T(t_p2);  // Pal -> Jacobi done
-    s.r = D3 ? sqrt(s.rx * s.rx + s.ry * s.ry + s.rz * s.rz) : sqrt(s.rx * s.rx + s.ry * s.ry);
-    s.ir = 1.0 / s.r;
-    s.encm = 0;
-    lane_finish(s);
+    double e2w;  // the adaptive resolution's eccentricity guard (P.e2_guard): the walker's largest e^2
+    walker_setup<NP, D3, L>(rowv, pl_idx, hill_factor, s, status, e2w);
+    PROF_T(t_p1);
+    PROF_T(t_p2);  // parameters read, prior checked, Pal -> Jacobi done
     // adaptive resolution: the lanes' state at t = 0 for refinement passes, in LDS after the
     // schedule and the stretch staging (LDS-coupled: [group][8][64]) or after the level-split ring
     // ([unit][8][64]; the unit's level-3 wave keeps it)
@@ -563,7 +356,6 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         if (threadIdx.x < 8) (&s_lvp[0][0])[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_cprog[threadIdx.x] = 0;
         if (threadIdx.x < 2) s_hof[threadIdx.x] = 0;
-        if (threadIdx.x < 2) s_vd[threadIdx.x] = 0;
         for (int dd = 0; dd < 2; dd++) {
             const DirSched& SD = dd ? P.bwd : P.fwd;
             double* b = s_sched + (size_t)dd * 4 * emax2;
@@ -791,60 +583,67 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         t_epo += tc - tb;
 #endif
     }
-#undef prm
     const int encflag = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) |
                         (status == RVM_STATUS_PRIOR ? 2 : 0) | (wfault ? RVM_ENC_FAULT : 0);
     // ---- the two directions of a walker meet: the second to arrive finishes it ----------------
-    // (one agent-scope exchange carries the other direction's result: no fence, no barrier).
-    // row(r), z, u3, lnp0: the walker's proposal and accept inputs (fused stretch half-step)
-    auto finish = [&](const int wo, const double chi2w, const int enc, auto&& row, const double z, const double u3,
-                      const double lnp0) {
-        int st = (enc & 2) ? RVM_STATUS_PRIOR : RVM_STATUS_OK;
-        if (st == RVM_STATUS_OK && (enc & 1)) st = RVM_STATUS_ENCOUNTER;
-        if (st == RVM_STATUS_OK && (enc & RVM_ENC_FAULT)) st = RVM_STATUS_NONFINITE;
-        if (st == RVM_STATUS_OK && (enc & RVM_ENC_UNRESOLVED)) st = RVM_STATUS_UNRESOLVED;
-        if (st == RVM_STATUS_OK && !isfinite(chi2w)) st = RVM_STATUS_NONFINITE;
-        const double mine = st == RVM_STATUS_OK ? chi2w : -(double)st;
-        const unsigned long long old = __hip_atomic_exchange(
-            slots + wo, (unsigned long long)__double_as_longlong(mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (one agent-scope exchange carries the other direction's result: no fence, no barrier; the
+    // slot encoding is rvm_walker.h's).  A direction arrives settled (chi2), open (the adaptive
+    // resolution's lower bound lbw on its chi2: it needs halving passes) or with a status.  The
+    // second arriver finishes the walker when neither direction is open; otherwise it applies the
+    // walker's certain-reject test on both lower bounds (a settled direction's is its chi2; fused
+    // sampler launches) and, unless that rejects, hands the walker to the refinement kernel
+    // (rvm_refine.hip) through the plan's work lists.  row(r), z, u3, lnp0: the walker's proposal
+    // and accept inputs (fused sampler step).
+    auto finish = [&](const int wo, const double chi2w, const int enc, const bool open, const double lbw, auto&& row,
+                      const double z, const double u3, const double lnp0) __attribute__((always_inline)) {
+        const int st = dir_status(enc, open, chi2w);
+        const unsigned long long mine =
+            st != RVM_STATUS_OK ? slot_status(st)
+                                : (unsigned long long)__double_as_longlong(open ? -lbw : chi2w);
+        const unsigned long long old =
+            __hip_atomic_exchange(slots + wo, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == RVM_SLOT_EMPTY) return;
         __hip_atomic_store(slots + wo, RVM_SLOT_EMPTY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double other = __longlong_as_double((long long)old);
-        const int st_o = other < 0.0 ? (int)(-other) : RVM_STATUS_OK;
-        const int sf = d == 0 ? st : st_o, sb = d == 0 ? st_o : st;
-        const double cf = d == 0 ? chi2w : other, cb = d == 0 ? other : chi2w;
-        int stw = sf != RVM_STATUS_OK ? sf : sb;  // both directions see the same PRIOR verdict
-        const double lp0 = -((cb + cf) / P.npoints);  // state.py:98, 109
-        if (stw == RVM_STATUS_OK && !isfinite(lp0)) stw = RVM_STATUS_NONFINITE;
-        const double lp = stw == RVM_STATUS_OK ? lp0 : -INFINITY;
-        if (logl_out) logl_out[wo] = lp;
-        if (status_out) status_out[wo] = stw;
-        // (rare: counted for rvm_plan_faults -- never a silent rejection)
-        if (stw == RVM_STATUS_NONFINITE || stw == RVM_STATUS_UNRESOLVED)
-            __hip_atomic_fetch_add(P.counters + (stw == RVM_STATUS_NONFINITE ? 1 : 2), 1ull, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        if (fused && (sa.n_spec == 0 || wo < sa.n_spec)) {
-            // emcee / MH accept (half 1's slots of a speculative iteration only deliver their
-            // logl: rvm_stretch_iteration_end)
-            const bool acc = mh ? mh_accepts(lp, lnp0, u3) : stretch_accepts(sa.dim, z, lp, lnp0, u3);
-            if (acc) {
-#pragma unroll
-                for (int r = 0; r < R; r++) {
-                    if (sa.src[r] >= 0) {
-                        const double v = row(r);
-                        sa.x[(size_t)sa.src[r] * sa.xstride + wo] = v;
-                        if (sa.x_aos) sa.x_aos[(size_t)wo * sa.dim + sa.src[r]] = v;
-                    }
-                }
-                sa.lnp[wo] = lp;
-                if (sa.accepted) sa.accepted[wo] += 1;
-            }
-            if (sa.dec) sa.dec[wo] = acc ? 1 : 0;
+        int st_o = RVM_STATUS_OK;
+        bool open_o = false;
+        double v_o = 0.0;
+        if (slot_is_status(old)) {
+            st_o = (int)(old & 0xFF);
+        } else {
+            v_o = __longlong_as_double((long long)old);
+            open_o = signbit(v_o);
+            v_o = fabs(v_o);
         }
+        const double v_m = open ? lbw : chi2w;
+        const int sf = d == 0 ? st : st_o, sb = d == 0 ? st_o : st;
+        const bool of = d == 0 ? open : open_o, ob = d == 0 ? open_o : open;
+        const double cf = d == 0 ? v_m : v_o, cb = d == 0 ? v_o : v_m;
+        int stw = sf != RVM_STATUS_OK ? sf : sb;  // both directions see the same PRIOR verdict
+        const double lp0 = -((cb + cf) / P.npoints);  // state.py:98, 109 (open: the upper bound lp_hi)
+        if (stw == RVM_STATUS_OK && (of || ob)) {
+            int dmode = 0;
+            double dz, du, dl;
+            if (P.ext_mult > 0) accept_inputs(sa, wo, dmode, dz, du, dl);
+            if (dmode != 0 && isfinite(lp0) && !accepts_at(sa, dmode, dz, du, dl, lp0)) {
+                // a certain reject: rejected whatever the refinement would give; reports lp_hi
+                __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)((of ? 1 : 0) + (ob ? 1 : 0)),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                // to the refinement kernel: list 0 both directions open, 1 forward only, 2 backward only
+                const int li = of && ob ? 0 : (of ? 1 : 2);
+                const int ix = __hip_atomic_fetch_add(P.rq_n + li, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                P.rq_w[(size_t)li * P.rq_cap + ix] = wo;
+                P.rq_c[wo] = of ? 0.0 : cf;
+                P.rq_c[(size_t)P.rq_cap + wo] = ob ? 0.0 : cb;
+                return;
+            }
+        }
+        if (stw == RVM_STATUS_OK && !isfinite(lp0)) stw = RVM_STATUS_NONFINITE;
+        walker_out<R>(P, sa, wo, stw, stw == RVM_STATUS_OK ? lp0 : -INFINITY, logl_out, status_out, row, z, u3, lnp0);
     };
     // finishing a walker without the LDS-staged proposal (level-split layout): the slot's draws again
     // (recomputed from an opaque index rather than kept live through the integration)
-    auto finish_recompute = [&](const int w_in, const double chi2w, const int enc) {
+    auto finish_recompute = [&](const int w_in, const double chi2w, const int enc, const bool open, const double lbw) __attribute__((always_inline)) {
         if (stretch) {
             int wo = w_in, k2, wk2, j2, jp2;
             double z2, zp2;
@@ -852,100 +651,19 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             stretch_slot(sa, wo, k2, wk2, z2, j2, zp2, jp2);
             auto row = [&](int r) { return walker_param(true, params, W, wk2, sa, r, z2, j2, k2, zp2, jp2); };
             // (lnp0 exists for the accepting kind-0 slots only: sa.lnp is n_spec long)
-            finish(wo, chi2w, enc, row, z2, stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half),
-                   k2 == 0 ? sa.lnp[wo] : 0.0);
+            finish(wo, chi2w, enc, open, lbw, row, z2,
+                   stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half), k2 == 0 ? sa.lnp[wo] : 0.0);
         } else if (mh) {
             auto row = [&](int r) { return walker_param(true, params, W, w_in, sa, r, 0.0, 0, 0, 0.0, 0); };
-            finish(w_in, chi2w, enc, row, 0.0, mh_u(sa.seed, (uint64_t)(sa.s0_begin + w_in), sa.iteration),
+            finish(w_in, chi2w, enc, open, lbw, row, 0.0, mh_u(sa.seed, (uint64_t)(sa.s0_begin + w_in), sa.iteration),
                    sa.lnp[w_in]);
         } else {
             auto row = [&](int) { return 0.0; };
-            finish(w_in, chi2w, enc, row, 0.0, 0.0, 0.0);
+            finish(w_in, chi2w, enc, open, lbw, row, 0.0, 0.0, 0.0);
         }
     };
 
-    // ---- adaptive resolution: one refinement pass with every step halved rf times -------------
-    // Run by the whole block in the LDS-coupled style: this wave integrates level lr of walker group
-    // (LDS-coupled) or unit (level-split) gr -- direction dr, whose schedule sits at
-    // s_sched + dr * 4 * emax2 (level-split) or l_dir -- from the lanes' state at t = 0 (l_init),
-    // gated drifts, one barrier per epoch over eb epochs (the longer direction's count in the
-    // level-split layout, whose units are the two directions); lr < 0: an idle wave (barriers
-    // only).  The combiner lanes (level 0's wave, lane = walker slot) accumulate chi2 (c2), the
-    // estimate (e2) and the change of chi2 from the previous pass (d2: sum |(rv - o)^2 - (rv_prev -
-    // o)^2| / s2, the previous pass's RV kept in P.rvp; +inf without it) of the walkers marked in
-    // `need` and overwrite their rv_out rows.  The wave's encounter flags land in
-    // s_enc_all[gr][lr][slot] (final barrier).
     int dummy_redo = 0;
-    auto refine_pass = [&](const int rf, const int lr, const int gr, const int dr, const int eb, const uint64_t need,
-                           double& c2, double& e2, double& d2) {
-        const DirSched& SR = dr ? P.bwd : P.fwd;
-        const int Er = SR.n_epochs;
-        const double* r_dir = dec ? s_sched + (size_t)dr * 4 * emax2 : l_dir;
-        const double* r_len = r_dir;
-        const double* r_rv = r_dir + Er;
-        const double* r_s2 = r_dir + 2 * Er;
-        const int* r_n = reinterpret_cast<const int*>(r_dir + 3 * Er);
-        const int* r_idx = r_n + Er;
-        const bool work = lr >= 0 && need != 0;
-        const int lr_u = __builtin_amdgcn_readfirstlane(lr < 0 ? 0 : lr);
-        KickPrep<NP> kq{};
-        if (work) {
-            const double* in = l_init + (size_t)gr * RVM_INIT_DOUBLES + lane;
-            s.rx = in[0];
-            s.ry = in[64];
-            s.vx = in[128];
-            s.vy = in[192];
-            s.rz = in[256];
-            s.vz = in[320];
-            s.r = in[384];
-            s.ir = in[448];
-            s.encm = 0;
-            if (Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
-        }
-        const int m_r = P.mult[lr_u] << rf;
-        const int nt_r = P.nt[lr_u];
-        const double sc = ldexp(P.inv_mult[lr_u], -rf);  // (exact: a power-of-two scaling)
-        c2 = 0.0;
-        e2 = 0.0;
-        d2 = P.ext_mult > 0 ? 0.0 : INFINITY;
-        const bool mine = work && lr == 0 && lane < WPB && ((need >> lane) & 1) && P.ext_mult > 0;
-        double* pp = P.rvp + (size_t)dr * P.lvx_emax * P.lvx_stride + (mine ? w0 + lane : 0);
-        for (int e = 0; e < eb; e++) {
-            const bool here = e < Er;
-            const double pv = mine && here ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued before the segment)
-            const int ns = work && here ? r_n[e] * m_r : 0;
-            if (ns > 0) {
-                const double h = r_len[e] * sc;
-                if (nt_r <= 6)
-                    segment<6, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
-                else if (nt_r == 7)
-                    segment<7, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
-                else
-                    segment<8, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
-            }
-            if (work) {  // (star_vx gathers over the walker's lanes by DPP: outside the lane branch)
-                const double v0 = star_vx<NP, L>(s);
-                if (pl_idx == 0) s_rv_all[gr][e & 1][lr_u][slot] = v0;
-            }
-            __syncthreads();
-            if (work && here && lr == 0 && lane < WPB && ((need >> lane) & 1)) {
-                double rvx = 0.0, rv3 = 0.0;
-                for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv_all[gr][e & 1][k][lane];
-                for (int k = 1; k < nl; k++) rv3 += P.lw3[k] * s_rv_all[gr][e & 1][k][lane];
-                const double r = rvx - r_rv[e];
-                c2 += (r * r) / r_s2[e];
-                e2 += fabs((rvx - rv3) * (r + (rv3 - r_rv[e]))) / r_s2[e];
-                if (mine) {
-                    d2 += fabs((rvx - pv) * (r + (pv - r_rv[e]))) / r_s2[e];
-                    pp[(size_t)e * P.lvx_stride] = rvx;
-                }
-                const int wo = w0 + lane;
-                if (rv_out != nullptr && wo < W) rv_out[(size_t)r_idx[e] * W + wo] = rvx;
-            }
-        }
-        if (work && pl_idx == 0) s_enc_all[gr][lr_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
-        __syncthreads();
-    };
     // ---- adaptive resolution, stage 1: the extension level ----------------------------------
     // One wave per group / unit -- its combiner wave -- integrates one more level (P.ext_mult steps
     // per base step) of direction dr from t = 0 and joins it, epoch by epoch, to the main pass's
@@ -959,7 +677,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // moves from the walker's first lane to its combiner lane by a shuffle, and the stored levels
     // of the next epoch load while this one integrates.
     auto extend_pass = [&](const int gr, const int dr, const uint64_t need_m, bool& need, double& chi2w, int& enc,
-                           double& c5o, double& ddo) {
+                           double& c5o, double& ddo) __attribute__((always_inline)) {
         const DirSched& SR = dr ? P.bwd : P.fwd;
         const int Er = SR.n_epochs;
         const double* r_dir = dec ? s_sched + (size_t)dr * 4 * emax2 : l_dir;
@@ -1049,130 +767,34 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             }
         }
     };
-    // Refinement loop over the walker slots still marked in s_need[g] of the active groups (gmask;
-    // set by the caller, one barrier since): first the extension (the combiner waves, lr == 0),
-    // then halving passes; the combiner lanes (cmb: level 0's wave, lane < WPB) update chi2w / enc /
-    // need per pass; a walker leaves when its estimate drops to the bound or a finer pass meets an
-    // encounter, and is UNRESOLVED if still above after rmax passes.
-    // Certain rejects (fused sampler launches only): after a halving pass, a proposal whose accept
-    // test fails even at logL_hi = -(c2 - min(d2, RVM_CUT_EST_FACTOR e2)) / npoints -- this
-    // direction's chi2 less a bound on the pass's own error (the change the halving brought,
-    // asymptotically 255x that error; or a large multiple of the pass's estimate), the other
-    // direction's chi2 >= 0 left out -- is rejected whatever further passes would give: it stops
-    // refining and keeps this pass's value (never stored: rejected).  Counted in counters[4].
-    // xest: the combiner lane's main-pass estimate (raw sum); xc5, xdd: the concurrent extension's chi2
-    // and change (ext_done), else set by extend_pass here.
-    auto refine_loop = [&](const int lr, const int gr, const int dr, const int gmask, const int eb, const bool cmb,
-                           bool& need, double& chi2w, int& enc, const bool ext_done, const double xest, double xc5,
-                           double xdd) {
-        // the combiner lane's accept inputs: 0 none, 1 stretch (emcee), 2 MH
-        int dmode = 0;
-        double dz = 0.0, du = 0.0, dl = 0.0;
-        if (cmb && need && P.ext_mult > 0) {
-            const int wo = w0 + lane;
-            if (stretch) {
-                int k2, wk2, j2, jp2;
-                double z2, zp2;
-                stretch_slot(sa, wo, k2, wk2, z2, j2, zp2, jp2);
-                if (k2 == 0) {
-                    dmode = 1;
-                    du = stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration, sa.half);
-                    dl = sa.lnp[wo];
-                } else if (sa.lnp1 != nullptr) {  // half 1 of a speculative iteration (accepts later)
-                    dmode = 1;
-                    du = stretch_u3(sa.seed, (uint64_t)(sa.s1_begin + wk2), sa.iteration, 1u);
-                    dl = sa.lnp1[wk2];
-                }
-                dz = z2;
-            } else if (mh) {
-                dmode = 2;
-                du = mh_u(sa.seed, (uint64_t)(sa.s0_begin + wo), sa.iteration);
-                dl = sa.lnp[wo];
-            }
-        }
-        if (P.ext_mult > 0 && !ext_done) {
+    // The extension stage over the walker slots marked in s_need[g] of the active groups (gmask;
+    // set by the caller, one barrier since) when the launch has no concurrent extension wave: the
+    // combiner waves (lr == 0) run extend_pass, every wave meets at the barrier.  The combiner lanes
+    // (cmb: level 0's wave, lane < WPB) update need / chi2w / enc and take the extension's chi2
+    // and change (xc5, xdd) for the walker's lower bound.  Halving passes are the refinement
+    // kernel's (rvm_refine.hip).
+    auto extend_stage = [&](const int lr, const int gr, const int dr, bool& need, double& chi2w, int& enc,
+                            double& xc5, double& xdd) __attribute__((always_inline)) {
+        if (P.ext_mult > 0) {
             const uint64_t gneed = s_need[gr];
             if (lr == 0 && gneed) {
                 if (lane == 0)
                     __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(gneed),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 extend_pass(gr, dr, gneed, need, chi2w, enc, xc5, xdd);
-                const uint64_t nb = ballot(need);
-                if (lane == 0) s_need[gr] = nb;
             }
             __syncthreads();
-            if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) return;
         }
-        // a certain reject already after the extension (rvoracle.c whx_direction_adapt): a proposal
-        // whose accept test fails even at lp_hi = -(c5 - min(d, RVM_CUT_EST_FACTOR est)) / npoints
-        // -- the extension's chi2 less the change it brought (or a large multiple of the main
-        // pass's estimate) -- starts no halving pass and keeps the extension's chi2 (counters[4])
-        if (P.ext_mult > 0) {
-            bool cut = false;
-            if (cmb && need && dmode != 0) {
-                const double lp_hi = -(xc5 - fmin(xdd, RVM_CUT_EST_FACTOR * xest)) / P.npoints;
-                if (isfinite(lp_hi) && (dmode == 1 ? !stretch_accepts(sa.dim, dz, lp_hi, dl, du)
-                                                   : !mh_accepts(lp_hi, dl, du))) {
-                    cut = true;
-                    need = false;
-                    chi2w = xc5;
-                }
-            }
-            if (lr == 0) {
-                const uint64_t nb = ballot(need);
-                const uint64_t nc = ballot(cut);
-                if (lane == 0) {
-                    s_need[gr] = nb;
-                    if (nc)
-                        __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)__builtin_popcountll(nc),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            __syncthreads();
-            if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) return;
-        }
-        for (int rf = 1; rf <= P.rmax; rf++) {
-            const uint64_t gneed = s_need[gr];
-            if (lr == 0 && lane == 0 && gneed)
-                __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(gneed),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            double c2, e2, d2;
-            refine_pass(rf, lr, gr, dr, eb, gneed, c2, e2, d2);
-            bool cut = false;
-            if (cmb && need) {
-                int er = 0;
-                for (int k = 0; k < nl; k++) er |= s_enc_all[gr][k][lane];
-                chi2w = c2;
-                const double lp_hi = -(c2 - fmin(d2, RVM_CUT_EST_FACTOR * e2)) / P.npoints;
-                const bool fin = isfinite(c2) && isfinite(e2);  // (a non-finite pass refines on)
-                if (er) {
-                    enc |= er;
-                    need = false;
-                } else if (fin && !(e2 / P.npoints > P.rtol_dir)) {
-                    need = false;
-                } else if (fin && isfinite(lp_hi) &&
-                           (dmode == 1 ? !stretch_accepts(sa.dim, dz, lp_hi, dl, du)
-                                       : (dmode == 2 && !mh_accepts(lp_hi, dl, du)))) {
-                    cut = true;  // a certain reject
-                    need = false;
-                } else if (rf == P.rmax) {
-                    enc |= RVM_ENC_UNRESOLVED;
-                    need = false;
-                }
-            }
-            if (lr == 0) {
-                const uint64_t nb = ballot(need);
-                const uint64_t nc = ballot(cut);
-                if (lane == 0) {
-                    s_need[gr] = nb;
-                    if (nc)
-                        __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)__builtin_popcountll(nc),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            __syncthreads();
-            if (((gmask & 1 ? s_need[0] : 0ull) | (gmask & 2 ? s_need[1] : 0ull)) == 0) break;
-        }
+    };
+    // a combiner lane's direction after the main pass and the extension: open (need) with the lower
+    // bound on its chi2 (oracle/rvoracle.c dir_extend: the extension's when it is finite, else the
+    // main pass's with its estimate alone), or settled; without halving passes (rmax = 0) an open
+    // direction is UNRESOLVED
+    auto direction_lb = [&](const bool need, const double chi2_main, const double est_raw, const bool xran,
+                            const double xc5, const double xdd) __attribute__((always_inline)) {
+        if (!need) return 0.0;
+        if (xran && isfinite(xc5) && isfinite(xdd)) return open_lb(xc5, xdd, est_raw);
+        return open_lb(chi2_main, INFINITY, est_raw);
     };
 
     if (!dec) {
@@ -1184,50 +806,58 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         if (cmb)
             for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
         double chi2w = chi2;
+        bool need = false;
+        double lbw = 0.0;
         if (P.rtol_dir < INFINITY) {  // (kernel argument: uniform)
             // (a non-finite chi2 -- the fixed step blowing up on an extreme orbit -- refines too, and
             // so does a walker past the eccentricity guard: its e^2 from the walker's first lane)
             const double e2c = __shfl(e2w, (lane & (WPB - 1)) * L);
-            bool need = cmb && wo < W && enc == 0 &&
-                        (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est) ||
-                         (P.ext_mult > 0 && e2c > P.e2_guard));
+            need = cmb && wo < W && enc == 0 &&
+                   (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est) ||
+                    (P.ext_mult > 0 && e2c > P.e2_guard));
             if (P.rmax == 0) {
                 if (need) enc |= RVM_ENC_UNRESOLVED;
+                need = false;
             } else {
-                if (cx && lvl == 0) {
-                    // the concurrent extension's verdict (extend_pass's rule on the same sums)
-                    const uint64_t nx = ballot(need);
-                    if (lane == 0 && nx)
-                        __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(nx),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (need) {
-                        if (s_enc[nl][lane] & 1) {
-                            enc |= 1;
-                            chi2w = c5x;
-                            need = false;
-                        } else if (ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
-                            chi2w = c5x;
-                            need = false;
+                const bool need0 = need;
+                if (cx) {  // (block-uniform)
+                    if (lvl == 0) {
+                        // the concurrent extension's verdict (extend_pass's rule on the same sums)
+                        const uint64_t nx = ballot(need);
+                        if (lane == 0 && nx)
+                            __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(nx),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (need) {
+                            if (s_enc[nl][lane] & 1) {
+                                enc |= 1;
+                                chi2w = c5x;
+                                need = false;
+                            } else if (ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
+                                chi2w = c5x;
+                                need = false;
+                            }
                         }
                     }
+                } else if (P.ext_mult > 0) {
+                    if (lvl == 0) {
+                        const uint64_t nb = ballot(need);
+                        if (lane == 0) s_need[grp] = nb;
+                    }
+                    __syncthreads();
+                    if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
+                        extend_stage(lvl, grp, d, need, chi2w, enc, c5x, ddx);
                 }
-                if (lvl == 0) {
-                    const uint64_t nb = ballot(need);
-                    if (lane == 0) s_need[grp] = nb;
-                }
-                __syncthreads();
-                if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
-                    refine_loop(cx ? (lvl < nl ? lvl : -1) : lvl, grp, d, G > 1 ? 3 : 1, E, cmb, need, chi2w, enc, cx,
-                                est, c5x, ddx);
+                lbw = direction_lb(need, chi2, est, need0 && P.ext_mult > 0, c5x, ddx);
             }
         }
         if (cmb && wo < W) {
             const int gl = grp * WPB + lane;
             auto row = [&](int r) { return l_q[r * GW + gl]; };
             if (fused)
-                finish(wo, chi2w, enc, row, l_q[R * GW + gl], l_q[(R + 1) * GW + gl], l_q[(R + 2) * GW + gl]);
+                finish(wo, chi2w, enc, need, lbw, row, l_q[R * GW + gl], l_q[(R + 1) * GW + gl],
+                       l_q[(R + 2) * GW + gl]);
             else
-                finish(wo, chi2w, enc, row, 0.0, 0.0, 0.0);
+                finish(wo, chi2w, enc, need, lbw, row, 0.0, 0.0, 0.0);
         }
     } else {
         // level-split: level waves publish their flags; the combiner finishes the unit, or hands it
@@ -1456,7 +1086,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 #ifdef RVM_PROFILE
             const unsigned long long rt_arr = __builtin_amdgcn_s_memrealtime();
 #endif
-            // adaptive resolution: finish now, or leave the unit to the refinement team
+            // adaptive resolution: settled, or open (with its lower bound) for the refinement kernel
             bool need = P.rtol_dir < INFINITY && valid && pl_idx == 0 && enc == 0 &&
                         (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est) ||
                          (P.ext_mult > 0 && e2w > P.e2_guard));
@@ -1464,6 +1094,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 enc |= RVM_ENC_UNRESOLVED;
                 need = false;
             }
+            const bool need0 = need;
+            const double chi2m = chi2w;
             if (lsx) {  // the concurrent extension's verdict (extend_pass's rule on the same sums)
                 const uint64_t nx = ballot(need);
                 if (lane == 0 && nx)
@@ -1480,61 +1112,38 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                     }
                 }
             }
-            const bool refine = ballot(need) != 0;
-            if (!refine) {
-                if (valid && pl_idx == 0) finish_recompute(w, chi2w, enc);
+            if (!lsx && P.ext_mult > 0 && ballot(need) != 0) {
+                // the extension after the main pass, on this wave: its lanes take the walker slots
+                // (lane = slot, extend_pass's convention) through LDS
+                if (valid && pl_idx == 0) {
+                    s_fchi[ul][slot] = chi2w;
+                    s_fenc[ul][slot] = enc | (need ? 16 : 0);
+                    s_fx[0][ul][slot] = est;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                const bool cl = lane < WPB && w0 + lane < W;
+                double c2 = cl ? s_fchi[ul][lane] : 0.0;
+                const int f = cl ? s_fenc[ul][lane] : 0;
+                const double es = cl ? s_fx[0][ul][lane] : 0.0;
+                const double cm = c2;
+                int en = f & 15;
+                bool nd = (f & 16) != 0;
+                const uint64_t nm = ballot(nd);
+                if (lane == 0)
+                    __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(nm),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                double xc5 = 0.0, xdd = 0.0;
+                extend_pass(ul, d, nm, nd, c2, en, xc5, xdd);
+                const double lb = direction_lb(nd, cm, es, (f & 16) != 0, xc5, xdd);
+                if (cl) finish_recompute(w0 + lane, c2, en, nd, lb);
             } else if (valid && pl_idx == 0) {
-                s_fchi[ul][slot] = chi2w;
-                s_fenc[ul][slot] = enc | (need ? 16 : 0);
-                s_fx[0][ul][slot] = est;
-                s_fx[1][ul][slot] = c5x;
-                s_fx[2][ul][slot] = ddx;
+                finish_recompute(w, chi2w, enc, need, direction_lb(need, chi2m, est, lsx && need0, c5x, ddx));
             }
-            if (lane == 0) __hip_atomic_store(s_vd + ul, refine ? 2 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef RVM_PROFILE
             prof_dec(rt_arr, nl - 1);
 #endif
         }
-        // every wave of a type-A block: wait for both units' verdicts, then leave, or refine as one
-        // LDS-coupled team.  (Unbounded on purpose: every wait of a combiner is bounded, so both
-        // verdicts always come; a wave that left early would break the team's barriers.)
-        __builtin_amdgcn_s_setprio(0);
-        int v0 = 0, v1 = 0;
-        for (;;) {
-            v0 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(s_vd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-            v1 = __builtin_amdgcn_readfirstlane(__hip_atomic_load(s_vd + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
-            if (v0 != 0 && v1 != 0) break;
-            __builtin_amdgcn_s_sleep(8);
-        }
-        if (v0 != 2 && v1 != 2) return;
-        // the refinement team.  Both units refine: wave wv takes level lr of its own unit gr = wv & 1
-        // (SIMD i carries levels (0, 3) or (1, 2) of the two units).  One unit refines: waves 0..3
-        // take its levels 0..3, one per SIMD (each at the lone-wave rate), waves 4..7 idle.
-        __builtin_amdgcn_s_setprio(1);
-        const bool both = v0 == 2 && v1 == 2;
-        const int gr = both ? ul : (v0 == 2 ? 0 : 1);
-        const int lr = both ? (wv < 4 ? (wv >> 1) : 5 - (wv >> 1)) : (wv < 4 ? wv : -1);
-        d = gr;  // (the finishing lanes meet the other direction as unit gr: finish() reads d)
-        const bool cmb = lr == 0 && lane < WPB;
-        const bool mine = (gr == 0 ? v0 : v1) == 2;
-        double chi2w = 0.0;
-        int enc = 0;
-        bool need = false;
-        if (cmb && mine) {
-            chi2w = s_fchi[gr][lane];
-            const int f = s_fenc[gr][lane];
-            enc = f & 15;
-            need = (f & 16) != 0 && w0 + lane < W;
-        }
-        if (lr == 0) {
-            const uint64_t nb = ballot(need);
-            if (lane == 0) s_need[gr] = nb;
-        }
-        __syncthreads();
-        refine_loop(lr, gr, gr, both ? 3 : 1 << gr, emax2, cmb, need, chi2w, enc, lsx,
-                    cmb && mine ? s_fx[0][gr][lane] : 0.0, cmb && mine ? s_fx[1][gr][lane] : 0.0,
-                    cmb && mine ? s_fx[2][gr][lane] : 0.0);
-        if (cmb && mine && w0 + lane < W) finish_recompute(w0 + lane, chi2w, enc);
         return;
     }
 #ifdef RVM_PROFILE
@@ -1671,25 +1280,34 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     return hipGetLastError();
 }
 
+// the likelihood kernel (main pass + extension); an adaptive plan's walkers it hands on are
+// finished by the refinement kernel (rvm_refine.hip launch_refine), which the caller enqueues next
+// on the same stream (rvm_abi.hip run_logl): every output is final when both have run
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
                        double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
     const bool inc = P.inclined != 0;
+    hipError_t e = hipErrorInvalidValue;
 #define RVM_LAUNCH(NPV) \
     (inc ? launch_logl_t<NPV, true>(P, W, params, hill_factor, slots, logl, status, rv_out, sa, stream) \
          : launch_logl_t<NPV, false>(P, W, params, hill_factor, slots, logl, status, rv_out, sa, stream))
     switch (P.n_planets) {
         case 1:
-            return RVM_LAUNCH(1);
+            e = RVM_LAUNCH(1);
+            break;
         case 2:
-            return RVM_LAUNCH(2);
+            e = RVM_LAUNCH(2);
+            break;
         case 3:
-            return RVM_LAUNCH(3);
+            e = RVM_LAUNCH(3);
+            break;
         case 4:
-            return RVM_LAUNCH(4);
+            e = RVM_LAUNCH(4);
+            break;
         default:
-            return hipErrorInvalidValue;
+            break;
     }
 #undef RVM_LAUNCH
+    return e;
 }
 
 }  // namespace rvm

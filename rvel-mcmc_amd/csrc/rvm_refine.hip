@@ -1,0 +1,383 @@
+// rvm_refine.hip -- the adaptive resolution's halving passes, for the walkers the
+// likelihood kernel (rvm_logl.hip) left with a direction above the error bound after its main pass
+// and extension.
+//
+// Replaces, for those walkers, the reference's per-proposal step adaptivity: REBOUND's IAS15 picks
+// its steps per orbit (state.py:61-73), a plan's step is fixed, and a walker far from the plan's
+// reference orbit is integrated again with every step halved until its extrapolation-error
+// estimate is within the bound.
+//
+// The rule is the WALKER's (oracle/rvoracle.c rvo_logl_whx_adapt): its two directions go through
+// the passes together (rf = 1, 2, ... rmax, every open direction each time) and after every pass
+//   * an encounter in either direction ends the walker (ENCOUNTER);
+//   * a direction whose estimate is within the bound settles (chi2 of that pass);
+//   * the certain-reject test (fused sampler launches): with each direction's lower bound on its
+//     chi2 (a settled one's chi2; an open one's chi2 less min(the step-doubling change of the pass,
+//     RVM_CUT_EST_FACTOR x its estimate)) the walker stops when its accept test fails even at
+//     lp_hi = -(lb_f + lb_b) / npoints, and reports lp_hi;
+//   * still open after rmax: UNRESOLVED (counted; the samplers raise on it).
+//
+// Layout.  Work lists (DevPlan rq_*): walkers with both directions open, forward only, backward
+// only, in the order they met.  A workgroup of 8 waves takes WPB = 64 / L walkers of one list (a
+// group; persistent blocks stride over the groups, both-direction groups first) and integrates
+// their open directions LDS-coupled, one wave per (direction, level), one barrier per epoch:
+// both directions open -> waves 0..3 direction 0's levels 0..3, waves 4..7 direction 1's in
+// mirrored order (wave i runs on SIMD i % 4: each SIMD carries levels i and nl-1-i, 11 steps per
+// base step at 4..7); one direction -> waves 0..nl-1, each alone on its SIMD (the lone-wave rate).
+// More than four levels with both open: one direction after the other.  Level 0's wave of a
+// direction combines (lane = walker slot): Richardson RV, chi2, estimate and the step-doubling
+// change against the previous pass's RV (P.rvp, written back), then wave 0's lanes decide per walker.
+// Each wave re-derives its lanes' state at t = 0 from the walker's parameters (rvm_walker.h, the
+// same bits as the likelihood kernel's prologue) and finishes the walker as it would have
+// (rvm_walker.h walker_out: logl, status, counters, the fused accept).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+// FMA contraction only within one source expression, as in rvm_logl.hip (the same step code must
+// round identically here)
+#pragma clang fp contract(on)
+
+#include "rvm_walker.h"
+
+namespace rvm {
+
+template <int NP, bool D3>
+__global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int W, const double* __restrict__ params,
+                                                     const double hill_factor, double* __restrict__ rv_out,
+                                                     double* __restrict__ logl_out, int32_t* __restrict__ status_out,
+                                                     const StretchArgs sa) {
+    constexpr int L = LanesPerWalker<NP>::value;
+    constexpr int WPB = 64 / L;
+    constexpr int PR = D3 ? 7 : 5;
+    constexpr int R = PR * NP;
+    const int wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int slot = lane / L;
+    const int pl_idx = lane % L;
+    const int nl = P.n_levels;
+
+    // the list sizes are final (the likelihood kernel has ended); the last block to read them
+    // resets them for the plan's next launch
+    __shared__ int s_n[3];
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 3; i++) s_n[i] = __hip_atomic_load(P.rq_n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int done = __hip_atomic_fetch_add(P.rq_n + 3, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == (int)gridDim.x - 1)
+            for (int i = 0; i < 4; i++) __hip_atomic_store(P.rq_n + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int nq[3] = {s_n[0], s_n[1], s_n[2]};
+    const int gq0 = (nq[0] + WPB - 1) / WPB, gq1 = (nq[1] + WPB - 1) / WPB, gq2 = (nq[2] + WPB - 1) / WPB;
+    const int ng = gq0 + gq1 + gq2;
+    if ((int)blockIdx.x >= ng) return;
+
+    // LDS: both directions' schedules ([d][seg_h1 | obs_rv | obs_s2 | (seg_n, obs_idx)], E_d each),
+    // the levels' star vx per epoch (double-buffered), encounter flags, the lanes' state at t = 0,
+    // and per walker slot its directions' state
+    extern __shared__ double s_sched[];
+    __shared__ double s_rv[2][2][RVM_MAX_LEVELS][64];
+    __shared__ int s_enc[2][RVM_MAX_LEVELS][64];
+    __shared__ double s_init[8][64];
+    __shared__ double s_chi[2][64], s_lb[2][64];
+    __shared__ int s_open[2][64];  // 1 open, 0 settled, 2 encounter
+    __shared__ int s_live[64];     // the walker is still refining
+    __shared__ int s_stw[64];      // its final status and logl (finished after the passes)
+    __shared__ double s_lpw[64];
+    __shared__ double s_acc[3][64];  // its accept inputs z, u, lnp0 (s_dmode: 0 none, 1 stretch, 2 MH)
+    __shared__ int s_dmode[64];
+    __shared__ unsigned long long s_mask[2];
+    const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
+    for (int dd = 0; dd < 2; dd++) {
+        const DirSched& SD = dd ? P.bwd : P.fwd;
+        double* b = s_sched + (size_t)dd * 4 * emax;
+        const int ED = SD.n_epochs;
+        int* bn = reinterpret_cast<int*>(b + 3 * ED);
+        for (int i = threadIdx.x; i < ED; i += blockDim.x) {
+            b[i] = SD.seg_h1[i];
+            b[ED + i] = SD.obs_rv[i];
+            b[2 * ED + i] = SD.obs_s2[i];
+            bn[i] = SD.seg_n[i];
+            bn[ED + i] = SD.obs_idx[i];
+        }
+    }
+    const bool stretch = sa.c != nullptr;
+    const bool mh = sa.mh_scale != nullptr;
+    const bool mapped = stretch || mh || sa.fd_x != nullptr;
+
+    for (int g = blockIdx.x; g < ng; g += gridDim.x) {
+        const int li = g < gq0 ? 0 : (g < gq0 + gq1 ? 1 : 2);
+        const int base = (li == 0 ? g : (li == 1 ? g - gq0 : g - gq0 - gq1)) * WPB;
+        const int cnt = nq[li] - base < WPB ? nq[li] - base : WPB;
+        const int* items = P.rq_w + (size_t)li * P.rq_cap + base;
+        // this lane's walker (lanes past the group's last repeat its first walker: benign values)
+        const int wo = items[slot < cnt ? slot : 0];
+        int kind = 0, wk = wo, jst = 0, jp = 0;
+        double zst = 0.0, zp = 0.0;
+        if (stretch) stretch_slot(sa, wo, kind, wk, zst, jst, zp, jp);
+        double rowv[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) rowv[r] = walker_param(mapped, params, W, wk, sa, r, zst, jst, kind, zp, jp);
+        Lane<NP> s;
+        int status = RVM_STATUS_OK;
+        double e2w;
+        walker_setup<NP, D3, L>(rowv, pl_idx, hill_factor, s, status, e2w);
+        __syncthreads();  // (the previous group's LDS state is no longer read)
+        if (wv == 0) {
+            s_init[0][lane] = s.rx;
+            s_init[1][lane] = s.ry;
+            s_init[2][lane] = s.vx;
+            s_init[3][lane] = s.vy;
+            s_init[4][lane] = s.rz;
+            s_init[5][lane] = s.vz;
+            s_init[6][lane] = s.r;
+            s_init[7][lane] = s.ir;
+            if (lane < WPB) {
+                const bool v = lane < cnt;
+                const int wl = items[v ? lane : 0];
+                const bool of = v && li != 2, ob = v && li != 1;
+                s_open[0][lane] = of ? 1 : 0;
+                s_open[1][lane] = ob ? 1 : 0;
+                s_chi[0][lane] = of ? 0.0 : P.rq_c[wl];
+                s_chi[1][lane] = ob ? 0.0 : P.rq_c[(size_t)P.rq_cap + wl];
+                s_lb[0][lane] = s_chi[0][lane];
+                s_lb[1][lane] = s_chi[1][lane];
+                s_live[lane] = v ? 1 : 0;
+                s_stw[lane] = RVM_STATUS_NONFINITE;  // (every pass loop ends with a decision)
+                s_lpw[lane] = -INFINITY;
+            }
+            const uint64_t m0 = ballot(lane < WPB && lane < cnt && li != 2);
+            const uint64_t m1 = ballot(lane < WPB && lane < cnt && li != 1);
+            if (lane == 0) {
+                s_mask[0] = m0;
+                s_mask[1] = m1;
+            }
+        }
+        // the decision lanes' accept inputs (wave 0, lane = walker slot), kept in LDS through the passes
+        const int wme = items[lane < WPB && lane < cnt ? lane : 0];
+        if (wv == 0 && lane < WPB) {
+            int dmode = 0;
+            double dz = 0.0, du = 0.0, dl = 0.0;
+            if (lane < cnt && P.ext_mult > 0) accept_inputs(sa, wme, dmode, dz, du, dl);
+            s_dmode[lane] = dmode;
+            s_acc[0][lane] = dz;
+            s_acc[1][lane] = du;
+            s_acc[2][lane] = dl;
+        }
+        __syncthreads();
+
+        for (int rf = 1; rf <= P.rmax; rf++) {
+            const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
+            const int am = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);
+            if (am == 0) break;
+            // sub-passes: both directions at once (up to four levels), else one after the other
+            const int nsub = (am == 3 && nl > 4) ? 2 : 1;
+            for (int sp = 0; sp < nsub; sp++) {
+                // this wave's (direction, level) task, or none
+                const bool both = am == 3 && nl <= 4;
+                const int sd = am == 3 ? sp : (am == 1 ? 0 : 1);  // the sub-pass's direction (one-direction mode)
+                int dd = -1, k = -1;
+                if (both) {
+                    const int j = wv & 3;
+                    dd = wv >> 2;
+                    k = j < nl ? (dd == 0 ? j : nl - 1 - j) : -1;
+                } else {
+                    dd = sd;
+                    k = wv < nl ? wv : -1;
+                }
+                if (k < 0) dd = -1;
+                // (wave-uniform in the compiler's eyes, SGPRs: a role derived from threadIdx would make
+                // the step loops divergent loops, with their state in extra registers)
+                dd = __builtin_amdgcn_readfirstlane(dd);
+                k = __builtin_amdgcn_readfirstlane(k);
+                const int dd_u = dd < 0 ? 0 : dd;
+                const int k_u = k < 0 ? 0 : k;
+                const bool work = dd >= 0;
+                const DirSched& SR = dd_u ? P.bwd : P.fwd;
+                const int Er = SR.n_epochs;
+                // the barrier count (the same on every wave): the longer direction, or the sub-pass's
+                const int eb = both ? emax : (sd ? P.bwd : P.fwd).n_epochs;
+                const double* r_dir = s_sched + (size_t)dd_u * 4 * emax;
+                const double* r_len = r_dir;
+                const double* r_rv = r_dir + Er;
+                const double* r_s2 = r_dir + 2 * Er;
+                const int* r_n = reinterpret_cast<const int*>(r_dir + 3 * Er);
+                const int* r_idx = r_n + Er;
+                const uint64_t need = dd_u ? mk1 : mk0;
+                KickPrep<NP> kq{};
+                if (work) {
+                    s.rx = s_init[0][lane];
+                    s.ry = s_init[1][lane];
+                    s.vx = s_init[2][lane];
+                    s.vy = s_init[3][lane];
+                    s.rz = s_init[4][lane];
+                    s.vz = s_init[5][lane];
+                    s.r = s_init[6][lane];
+                    s.ir = s_init[7][lane];
+                    s.encm = 0;
+                    if (Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
+                }
+                const int m_r = P.mult[k_u] << rf;
+                const int nt_r = P.nt[k_u];
+                const double sc = ldexp(P.inv_mult[k_u], -rf);  // (exact: a power-of-two scaling)
+                const bool cmb = work && k == 0 && lane < WPB && ((need >> lane) & 1);
+                const bool hasp = P.rvp != nullptr;
+                double c2 = 0.0, e2 = 0.0, d2 = hasp ? 0.0 : INFINITY;  // (the combiner lanes)
+                double* pp = hasp ? P.rvp + (size_t)dd_u * P.lvx_emax * P.lvx_stride + (cmb ? wme : 0) : nullptr;
+                for (int e = 0; e < eb; e++) {
+                    const bool here = e < Er;
+                    const double pv = cmb && here && hasp ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued early)
+                    const int ns = __builtin_amdgcn_readfirstlane(work && here ? r_n[e] * m_r : 0);
+                    if (ns > 0) segment_gated<D3, NP, L>(s, kq, r_len[e] * sc, ns, nt_r);
+                    if (work && here) {  // (star_vx gathers over the walker's lanes by DPP: outside the lane branch)
+                        const double v0 = star_vx<NP, L>(s);
+                        if (pl_idx == 0) s_rv[dd_u][e & 1][k_u][slot] = v0;
+                    }
+                    __syncthreads();
+                    if (cmb && here) {
+                        double rvx = 0.0, rv3 = 0.0;
+                        for (int q = 0; q < nl; q++) rvx += P.lw[q] * s_rv[dd_u][e & 1][q][lane];
+                        for (int q = 1; q < nl; q++) rv3 += P.lw3[q] * s_rv[dd_u][e & 1][q][lane];
+                        const double r = rvx - r_rv[e];
+                        c2 += (r * r) / r_s2[e];
+                        e2 += fabs((rvx - rv3) * (r + (rv3 - r_rv[e]))) / r_s2[e];
+                        if (hasp) {
+                            d2 += fabs((rvx - pv) * (r + (pv - r_rv[e]))) / r_s2[e];
+                            pp[(size_t)e * P.lvx_stride] = rvx;
+                        }
+                        if (rv_out != nullptr) rv_out[(size_t)r_idx[e] * W + wme] = rvx;
+                    }
+                }
+                if (work && pl_idx == 0) s_enc[dd_u][k_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
+                __syncthreads();
+                // the direction's combiner lanes: settle, open (with the pass's lower bound) or encounter
+                if (work && k == 0 && lane < WPB) {
+                    if ((need >> lane) & 1) {
+                        int er = 0;
+                        for (int q = 0; q < nl; q++) er |= s_enc[dd_u][q][lane];
+                        const bool fin = isfinite(c2) && isfinite(e2);
+                        if (er) {
+                            s_open[dd_u][lane] = 2;
+                        } else if (fin && !(e2 / P.npoints > P.rtol_dir)) {
+                            s_open[dd_u][lane] = 0;
+                            s_chi[dd_u][lane] = c2;
+                            s_lb[dd_u][lane] = c2;
+                        } else {
+                            s_chi[dd_u][lane] = fin ? c2 : __builtin_nan("");
+                            s_lb[dd_u][lane] = fin ? open_lb(c2, d2, e2) : 0.0;
+                        }
+                    }
+                    if (lane == 0 && need)
+                        __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(need),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            __syncthreads();
+            // the walker's decision (wave 0, lane = walker slot)
+            if (wv == 0) {
+                bool live = lane < WPB && s_live[lane] != 0;
+                if (live) {
+                    const int of = s_open[0][lane], ob = s_open[1][lane];
+                    int stw = RVM_STATUS_OK;
+                    double lp = 0.0;
+                    bool done = true;
+                    if (of == 2 || ob == 2) {
+                        stw = RVM_STATUS_ENCOUNTER;
+                    } else if (of == 0 && ob == 0) {
+                        lp = -((s_chi[1][lane] + s_chi[0][lane]) / P.npoints);  // state.py:98, 109
+                        if (!isfinite(lp)) stw = RVM_STATUS_NONFINITE;
+                    } else {
+                        const double lp_hi = -((s_lb[1][lane] + s_lb[0][lane]) / P.npoints);
+                        const int dmode = s_dmode[lane];
+                        if (dmode != 0 && isfinite(lp_hi) &&
+                            !accepts_at(sa, dmode, s_acc[0][lane], s_acc[1][lane], s_acc[2][lane], lp_hi)) {
+                            lp = lp_hi;  // a certain reject
+                            __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)((of ? 1 : 0) + (ob ? 1 : 0)),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        } else if (rf == P.rmax) {
+                            stw = RVM_STATUS_UNRESOLVED;
+                        } else {
+                            done = false;
+                        }
+                    }
+                    if (done) {
+                        live = false;
+                        s_live[lane] = 0;
+                        s_stw[lane] = stw;
+                        s_lpw[lane] = stw == RVM_STATUS_OK ? lp : -INFINITY;
+                    }
+                }
+                const uint64_t m0 = ballot(live && s_open[0][lane] == 1);
+                const uint64_t m1 = ballot(live && s_open[1][lane] == 1);
+                if (lane == 0) {
+                    s_mask[0] = m0;
+                    s_mask[1] = m1;
+                }
+            }
+            __syncthreads();
+        }
+        // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h)
+        if (wv == 0 && lane < WPB && lane < cnt) {
+            int k2 = 0, wk2 = wme, j2 = 0, jp2 = 0;
+            double z2 = 0.0, zp2 = 0.0;
+            if (stretch) stretch_slot(sa, wme, k2, wk2, z2, j2, zp2, jp2);
+            auto row = [&](int r) { return walker_param(mapped, params, W, wk2, sa, r, z2, j2, k2, zp2, jp2); };
+            const double u3 = stretch ? stretch_u3(sa.seed, (uint64_t)(sa.s0_begin + wme), sa.iteration, sa.half)
+                                      : (mh ? mh_u(sa.seed, (uint64_t)(sa.s0_begin + wme), sa.iteration) : 0.0);
+            const double lnp0 = (stretch && k2 == 0) || mh ? sa.lnp[wme] : 0.0;
+            walker_out<R>(P, sa, wme, s_stw[lane], s_lpw[lane], logl_out, status_out, row, z2, u3, lnp0);
+        }
+    }
+}
+
+template <int NPV, bool D3V>
+static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
+                                  int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
+    constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
+    const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
+    const size_t smem = (size_t)emax * 8 * sizeof(double);
+    static size_t budget[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (budget[dev] == 0) {
+        const void* f = reinterpret_cast<const void*>(&refine_kernel<NPV, D3V>);
+        hipFuncAttributes fa{};
+        size_t b = 32 * 1024;
+        if (hipFuncGetAttributes(&fa, f) == hipSuccess && fa.sharedSizeBytes < (size_t)RVM_LDS_PER_CU) {
+            const size_t lim = (size_t)RVM_LDS_PER_CU - fa.sharedSizeBytes;
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim) == hipSuccess) b = lim;
+        }
+        (void)hipGetLastError();
+        budget[dev] = b;
+    }
+    if (smem > budget[dev]) return hipErrorInvalidConfiguration;
+    // every block reads the list sizes (the last one resets them): a grid of at most one block
+    // per CU, and no more than the lists could fill
+    const int groups = (W + wpb - 1) / wpb + 2;
+    const int nb = std::max(1, std::min(P.n_cu > 0 ? P.n_cu : 256, groups));
+    refine_kernel<NPV, D3V><<<dim3(nb), dim3(512), smem, stream>>>(P, W, params, hill_factor, rv_out, logl, status, sa);
+    return hipGetLastError();
+}
+
+hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
+                         int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
+    if (P.rmax <= 0 || P.rq_n == nullptr) return hipSuccess;
+    const bool inc = P.inclined != 0;
+#define RVM_LAUNCH_R(NPV)                                                                        \
+    (inc ? launch_refine_t<NPV, true>(P, W, params, hill_factor, logl, status, rv_out, sa, stream) \
+         : launch_refine_t<NPV, false>(P, W, params, hill_factor, logl, status, rv_out, sa, stream))
+    switch (P.n_planets) {
+        case 1:
+            return RVM_LAUNCH_R(1);
+        case 2:
+            return RVM_LAUNCH_R(2);
+        case 3:
+            return RVM_LAUNCH_R(3);
+        case 4:
+            return RVM_LAUNCH_R(4);
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef RVM_LAUNCH_R
+}
+
+}  // namespace rvm

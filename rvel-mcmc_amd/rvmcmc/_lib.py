@@ -18,7 +18,7 @@ RVM_STATUS_NONFINITE = 3
 RVM_STATUS_UNRESOLVED = 4
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
-ABI_VERSION = 10  # include/rvmcmc.h RVM_ABI_VERSION
+ABI_VERSION = 11  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):
@@ -82,6 +82,9 @@ SIGNATURES = {
     "rvm_plan_faults": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                   C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64), _dp]),
     "rvm_plan_set_handoff_timeout": (C.c_int, [C.c_void_p, C.c_double]),
+    "rvm_plan_time_kernels": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rvm_plan_kernel_times": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int32,
+                                        C.POINTER(C.c_int32)]),
     "rvm_plan_extension": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rvm_plan_set_verify_eccentricity": (C.c_int, [C.c_void_p, C.c_double]),
     "rvm_plan_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),

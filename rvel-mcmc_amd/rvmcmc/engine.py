@@ -36,6 +36,7 @@ def level_multipliers(levels) -> tuple:
 
 
 DT_GRID = 16  # base-step grid points per factor of two (IntegratorConfig.step_for)
+ECC_GRID = 64  # the eccentricity guard's reference eccentricity is rounded to multiples of 1/ECC_GRID
 
 
 @dataclass(frozen=True)
@@ -66,7 +67,7 @@ class IntegratorConfig:
     # fixed step; at the chain's steady state 6.2 ms against 0.69.  resolve_tol = 0
     # turns it off (the round-2 fixed-step algorithm).
     resolve_tol: float = 5e-7
-    resolve_max: int = 4
+    resolve_max: int = 8
     # eccentricity guard (rvm_plan_set_verify_eccentricity): walkers whose pericentre passage is more
     # than this factor quicker than the plan's reference orbit's always get the extension -- the
     # estimate under-read on such orbits (all three T2 misses it left at the bench chain's steady
@@ -99,9 +100,13 @@ class IntegratorConfig:
         return float(self.resolve_tol), int(self.resolve_max), self.ecc_guard(planets)
 
     def ecc_guard(self, planets) -> float:
+        """The guard from the reference planets' largest eccentricity, rounded to the grid
+        ECC_GRID (as step_for grids the step): the scalar State API plans from each state's own
+        planets, and a guard that varied continuously would give every state a plan of its own."""
         if not planets or not (self.verify_speedup > 0.0) or not (self.resolve_tol > 0.0):
             return 0.0
         e_ref = max(float(np.hypot(p.get("h", 0.0), p.get("k", 0.0))) for p in planets)
+        e_ref = round(e_ref * ECC_GRID) / ECC_GRID
         if not e_ref < 1.0:
             return 0.0
         return float(1.0 - (self.verify_speedup * (1.0 - e_ref) ** -1.5) ** (-2.0 / 3.0))
@@ -200,15 +205,43 @@ class LoglPlan:
         return dict(handoff_timeouts=vals[0].value, nonfinite=vals[1].value, unresolved=vals[2].value,
                     refined=vals[3].value, truncated=vals[4].value)
 
-    def check_faults(self, what="plan", stream=None) -> dict:
-        """Raise RvmError on hand-off timeouts or NONFINITE results since the last check (emcee
-        raises on a NaN log-probability, mcmc.py:28-35 / emcee 2.2.1; a stalled hand-off must never
-        pass as an ordinary rejection); returns the counters (then reset)."""
+    def check_faults(self, what="plan", stream=None, group=None) -> dict:
+        """Raise RvmError on hand-off timeouts, NONFINITE results, or (a plan that refines, resolve_max
+        > 0) UNRESOLVED results since the last check: emcee raises on a NaN log-probability
+        (mcmc.py:28-35 / emcee 2.2.1), and neither a stalled hand-off nor a walker the adaptive
+        resolution could not bring within its bound may pass as an ordinary rejection.  Returns the
+        counters (then reset).  group: a torch.distributed group whose ranks check together (the
+        counts are summed over it, so every rank raises, or none -- a rank raising alone would leave
+        the others blocked in the sampler's next collective)."""
         f = self.faults(reset=True, stream=stream)
-        if f["handoff_timeouts"] or f["nonfinite"]:
-            raise _lib.RvmError(f"{what}: {f['handoff_timeouts']} level-split hand-off timeout(s), {f['nonfinite']} "
-                                f"non-finite log-likelihood(s) on the GPU (rvm_plan_faults)")
+        bad = [f["handoff_timeouts"], f["nonfinite"], f["unresolved"] if self.resolve_max > 0 else 0]
+        if group is not None:
+            torch = _torch()
+            dist = torch.distributed
+            dev = self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+            t = torch.tensor(bad, dtype=torch.int64, device=dev)
+            dist.all_reduce(t, group=group)
+            bad = [int(v) for v in t.cpu()]
+        if any(bad):
+            raise _lib.RvmError(f"{what}: {bad[0]} level-split hand-off timeout(s), {bad[1]} non-finite "
+                                f"log-likelihood(s), {bad[2]} walker(s) not resolved to the plan's tolerance after "
+                                f"{self.resolve_max} halvings on the GPU (rvm_plan_faults"
+                                f"{', summed over the ranks' if group is not None else ''})")
         return f
+
+    def time_kernels(self, max_launches):
+        """rvm_plan_time_kernels: the next max_launches evaluations on this plan record HIP events
+        around their likelihood and refinement kernels (read with kernel_times)."""
+        _lib.check(self.lib.rvm_plan_time_kernels(self._h, int(max_launches)), "rvm_plan_time_kernels")
+
+    def kernel_times(self, max_launches=4096):
+        """(likelihood kernel ms [n], refinement kernel ms [n]) of the evaluations timed since
+        time_kernels (waits for them); timing stops."""
+        a = (C.c_float * max_launches)()
+        b = (C.c_float * max_launches)()
+        n = C.c_int32()
+        _lib.check(self.lib.rvm_plan_kernel_times(self._h, a, b, int(max_launches), C.byref(n)), "rvm_plan_kernel_times")
+        return np.array(a[:n.value], dtype=np.float64), np.array(b[:n.value], dtype=np.float64)
 
     def set_handoff_timeout(self, seconds):
         _lib.check(self.lib.rvm_plan_set_handoff_timeout(self._h, float(seconds)), "rvm_plan_set_handoff_timeout")
@@ -394,7 +427,12 @@ def periodic_fault_check(sampler, plan):
     step; `sampler.check_faults()` runs it on demand."""
     every = getattr(sampler, "fault_check_every", FAULT_CHECK_EVERY)
     if plan is not None and every and sampler.iteration % every == 0:
-        sampler.last_faults = plan.check_faults(type(sampler).__name__)
+        sampler.last_faults = plan.check_faults(type(sampler).__name__, group=fault_group(sampler))
+
+
+def fault_group(sampler):
+    """The process group whose ranks must check a sampler's faults together (None on one rank)."""
+    return getattr(sampler, "group", None) if getattr(sampler, "world", 1) > 1 else None
 
 
 PLAN_CACHE_SIZE = 32  # plans kept per observation set

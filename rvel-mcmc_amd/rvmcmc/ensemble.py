@@ -342,7 +342,7 @@ class EnsembleSampler:
         """Raise on level-split hand-off timeouts or NONFINITE log-likelihoods since the last check
         (rvm_plan_faults; also run every FAULT_CHECK_EVERY iterations by step()); returns the
         counters, including walker-directions refined by the adaptive resolution."""
-        self.last_faults = self.plan.check_faults(type(self).__name__)
+        self.last_faults = self.plan.check_faults(type(self).__name__, group=engine.fault_group(self))
         return self.last_faults
 
     def gather_mirrors(self):

@@ -172,10 +172,12 @@ class Mh(Mcmc):
             entries.append([prop, False, after_normal, u, np.random.get_state(), 0])
             live.append(entries[-1])
         # one launch per plan: a proposal's own scalar get_logp would use the plan of its own
-        # (gridded) base step, so proposals are grouped by it to give bit-identical values
+        # (gridded) base step and resolution settings (its eccentricity guard included), so
+        # proposals are grouped by the whole plan key to give bit-identical values
         groups = {}
         for e in live:
-            groups.setdefault(e[0].integrator.plan_args(e[0].planets), []).append(e)
+            it = e[0].integrator
+            groups.setdefault((it.plan_args(e[0].planets), it.resolve(e[0].planets)), []).append(e)
         for grp in groups.values():
             X = torch.as_tensor(np.array([e[0].get_params() for e in grp]).T.copy(), device=engine.default_device())
             lp, st, _ = grp[0][0].get_logp_batch(self.obs, X)

@@ -155,14 +155,51 @@ class SmalaChains:
         return engine.plan_for(self.obs, len(self.state.planets), dt, mult, max_walkers, self.device, hint,
                                engine.is_inclined(self.state.planets), (0.0, 0))
 
-    def _center_logl(self, X, lp, st):
-        """Overwrite the stencil centres' logp / status (walkers 0 .. C-1) with the adaptive plan's
-        (T2: the value the accept test uses)."""
+    def _center_plan(self):
+        """The adaptive plan of the chains' own logp (on the side stream: _center_start), created at
+        the size the centre launch needs and kept, so its fault counters are the ones read."""
+        torch = _torch()
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        with torch.cuda.stream(self._side):
+            self._cplan = self.state._plan(self.obs, max_walkers=self.n, device=self.device)
+        return self._cplan
+
+    def _center_start(self, X):
+        """Start the centres' logp on the adaptive plan (T2: the value the accept test uses) on a
+        side stream, concurrently with the stencil launch on the fixed-step plan: both launches are
+        latency-bound and together fill a fraction of the CUs, so the centres' main pass, extension
+        and halving passes hide behind the stencil.  Returns what _center_join needs (None when the
+        resolution is off: the stencil's own centre values are the fixed-step logp)."""
+        torch = _torch()
         if self.state.integrator.resolve()[0] <= 0.0:
+            return None
+        plan = self._center_plan()
+        main = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(self._side):
+            self._side.wait_event(ready)
+            lpc, stc, _ = plan.logl(self.pmap.to_kernel(X), hill_factor=1.0)
+            done = torch.cuda.Event()
+            done.record(self._side)
+        return lpc, stc, done
+
+    def _center_join(self, pending, lp, st):
+        """Overwrite the stencil centres' logp / status (walkers 0 .. C-1) with the side stream's."""
+        if pending is None:
             return
-        lpc, stc, _ = self.state.get_logp_batch(self.obs, X, hill_factor=1.0, pmap=self.pmap)
+        torch = _torch()
+        lpc, stc, done = pending
+        main = torch.cuda.current_stream(self.device)
+        main.wait_event(done)
         lp[:self.n].copy_(lpc)
         st[:self.n].copy_(stc)
+        lpc.record_stream(main)  # (allocated on the side stream, last read on this one)
+        stc.record_stream(main)
+
+    def _center_logl(self, X, lp, st):
+        self._center_join(self._center_start(X), lp, st)
 
     def _stencil_logl(self, X, fused=True):
         """logp, status [(2P+1) C] and model RVs [n_obs][(2P+1) C] over the central-difference
@@ -172,12 +209,13 @@ class SmalaChains:
         torch = _torch()
         S = 2 * self.P + 1
         plan = self._fixed_plan(S * self.n)
+        pending = self._center_start(X)
         if not fused:
             _lib.check(self.lib.rvm_fd_params(self.P, self.n, X.data_ptr(), self.rel_step, self.floor.data_ptr(),
                                               self.stencil.data_ptr(), _lib.stream_handle()), "rvm_fd_params")
             lp, st, rv = plan.logl(self.pmap.to_kernel(self.stencil), hill_factor=1.0, want_rv=True)
             self._plan_keep = plan
-            self._center_logl(X, lp, st)
+            self._center_join(pending, lp, st)
             return lp, st, rv
         if getattr(self, "_st_bufs", None) is None:
             self._st_bufs = (torch.empty(S * self.n, dtype=torch.float64, device=self.device),
@@ -190,14 +228,15 @@ class SmalaChains:
                                                        lp.data_ptr(), st.data_ptr(), rv.data_ptr(),
                                                        _lib.stream_handle()), "rvm_smala_stencil_logl")
         self._plan_keep = plan  # the launch's plan stays alive with the sampler
-        self._center_logl(X, lp, st)
+        self._center_join(pending, lp, st)
         return lp, st, rv
 
     def _derive_into(self, X, cache, fused=True):
         st_h = _lib.stream_handle()
         if self.hessian == "exact":
+            pending = self._center_start(X)  # (the adaptive logp beside the derivative launch)
             lp, g, H, st = self.state.get_logp_d_dd_batch(self.obs, X, hill_factor=1.0, pmap=self.pmap)
-            self._center_logl(X, lp, st)
+            self._center_join(pending, lp, st)
             _lib.check(self.lib.rvm_smala_metric(self.P, self.n, X.data_ptr(), lp.data_ptr(), st.data_ptr(),
                                                  g.data_ptr(), H.data_ptr(), self.alpha, self.eps,
                                                  C.byref(cache["_c"]), st_h), "rvm_smala_metric")
@@ -255,8 +294,9 @@ class SmalaChains:
                    "rvm_smala_propose")
         cur, prop = C.byref(self.cache["_c"]), C.byref(self.prop["_c"])
         if fused and self.hessian == "exact":
+            pending = self._center_start(self.Xs)  # (the logp the accept uses: adaptive resolution)
             lp, g, H, st = self.state.get_logp_d_dd_batch(self.obs, self.Xs, hill_factor=1.0, pmap=self.pmap)
-            self._center_logl(self.Xs, lp, st)  # (the logp the accept uses: adaptive resolution)
+            self._center_join(pending, lp, st)
             _lib.check(self.lib.rvm_smala_metric_accept(self.P, self.n, 0, self.X.data_ptr(), self.Xs.data_ptr(),
                                                         lp.data_ptr(), st.data_ptr(), g.data_ptr(), H.data_ptr(),
                                                         self.alpha, self.eps, cur, prop, self.seed, self.iteration,
@@ -284,8 +324,6 @@ class SmalaChains:
         self.iteration += 1
         self._periodic_faults()
 
-    def _fault_plan(self):
-        return self.state._plan(self.obs, max_walkers=(2 * self.P + 1) * self.n, device=self.device)
 
     def _periodic_faults(self):  # (engine.periodic_fault_check over both plans)
         every = getattr(self, "fault_check_every", engine.FAULT_CHECK_EVERY)
@@ -293,10 +331,19 @@ class SmalaChains:
             self.check_faults()
 
     def check_faults(self):
-        """rvm_plan_faults of the chains' plans (adaptive, and the stencil's fixed-step one): raises on
-        hand-off timeouts / NONFINITE results; returns the adaptive plan's counters."""
-        self._fixed_plan((2 * self.P + 1) * self.n).check_faults(type(self).__name__)
-        self.last_faults = self._fault_plan().check_faults(type(self).__name__)
+        """rvm_plan_faults of the chains' plans (the centres' adaptive one, on its side stream, and the
+        stencil's fixed-step one): raises on hand-off timeouts / NONFINITE / UNRESOLVED results;
+        returns the adaptive plan's counters."""
+        torch = _torch()
+        name = type(self).__name__
+        if self.hessian == "gauss-newton":
+            self._fixed_plan((2 * self.P + 1) * self.n).check_faults(name)
+        if self.state.integrator.resolve()[0] <= 0.0:
+            self.last_faults = {}
+            return self.last_faults
+        plan = getattr(self, "_cplan", None) or self._center_plan()
+        with torch.cuda.stream(self._side):
+            self.last_faults = plan.check_faults(name)
         return self.last_faults
 
 

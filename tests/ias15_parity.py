@@ -30,7 +30,7 @@ import oracle as O
 MARGIN = 1e-6  # walkers with |lnpdiff - ln U| < 1e-6 are exempt (counted)
 ROUNDOFF_REL = 1e-9  # IAS15 logL response to a 1e-15 relative input nudge, relative to max(1, |logL|)
 NUDGES = [(0, 4, 1), (-1, 4, -1), (0, 1, 1), (-1, 1, -1)]
-ST_OK, ST_PRIOR, ST_ENC = 0, 1, 2
+ST_OK, ST_PRIOR, ST_ENC, ST_UNRESOLVED = 0, 1, 2, 4
 
 
 def n_threads():
@@ -125,6 +125,7 @@ class Tally:
         self.disagree_roundoff = 0
         self.n_beyond_margin_dlogl = 0
         self.beyond_margin_not_roundoff = 0
+        self.n_unresolved = 0
 
     def add(self, acc_dev, acc_ref, margin, st_dev, st_ref, lnq_dev=None, lnq_ref=None, idx_offset=0,
             roundoff=None, current_differs=None):
@@ -139,7 +140,12 @@ class Tally:
         st_dev = np.asarray(st_dev)
         st_ref = np.asarray(st_ref)
         near = margin < MARGIN
-        sdiff = st_dev != st_ref
+        # a status pair is exempt only where the two integrators legitimately differ (an encounter
+        # caught by one and not the other); a walker the device left UNRESOLVED (4) has no
+        # counterpart in the reference (IAS15 always integrates, mcmc.py:28-35 maps only exceptions
+        # to -inf): its decision must match like any other
+        sdiff = (st_dev != st_ref) & (st_dev != ST_UNRESOLVED)
+        self.n_unresolved += int((st_dev == ST_UNRESOLVED).sum())
         exempt = near | sdiff
         if current_differs is not None:
             cd = np.asarray(current_differs, bool) & ~exempt
@@ -161,7 +167,7 @@ class Tally:
         self.accepted_ref += int(acc_ref.sum())
         self.n_enc_ref += int((st_ref == ST_ENC).sum())
         self.n_prior += int((st_ref == ST_PRIOR).sum())
-        for a, b in zip(st_dev[sdiff], st_ref[sdiff]):
+        for a, b in zip(st_dev[st_dev != st_ref], st_ref[st_dev != st_ref]):
             k = f"{int(a)}/{int(b)}"
             self.status_pairs[k] = self.status_pairs.get(k, 0) + 1
         self.mismatch += [int(i) + idx_offset for i in np.nonzero(~same & ~exempt)[0]]
@@ -189,7 +195,7 @@ class Tally:
              "differing_ias15_roundoff_sensitive": self.disagree_roundoff,
              "ok_proposals_dlogl_above_margin_not_roundoff": self.beyond_margin_not_roundoff,
              "max_abs_dlogl_ok_proposals_not_roundoff": getattr(self, "max_dlogl_ok_not_roundoff", 0.0),
-             "margin": MARGIN, "roundoff_rel": ROUNDOFF_REL}
+             "unresolved_device": self.n_unresolved, "margin": MARGIN, "roundoff_rel": ROUNDOFF_REL}
         d.update(extra)
         line = json.dumps(d)
         print(line)

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 10
+    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 11
 
 
 def test_python_binding_matches_header():
@@ -68,7 +68,7 @@ def test_argument_errors_do_not_touch_the_device():
     assert rc < 0 and b"too many epochs" in lib.rvm_last_error()
     # adaptive resolution bounds, and the fault-counter / timeout entry points on a null plan
     cfg3 = _lib.RvmConfig(2, 0.5, 4, 100.0)
-    cfg3.resolve_tol, cfg3.resolve_max = 5e-7, 9
+    cfg3.resolve_tol, cfg3.resolve_max = 5e-7, 13
     rc = lib.rvm_plan_create(C.byref(cfg3), z, z, z, 1, 64, C.byref(h))
     assert rc < 0 and b"resolve_max" in lib.rvm_last_error()
     assert lib.rvm_plan_faults(None, 0, None, None, None, None, None, 0) < 0

@@ -62,9 +62,11 @@ def _device_logl(ens_or_plan, pm, Q, hill):
     return lp.cpu().numpy(), st.cpu().numpy()
 
 
-def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, roundoff=False, seed=2017, ball_seed=0):
+def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, roundoff=False, seed=2017, ball_seed=0,
+                   X0=None):
     """Run the device EnsembleSampler (default path) and compare its decisions, iteration by
-    iteration, with emcee 2.2.1 restated in numpy on IAS15 logL and the same Philox draws."""
+    iteration, with emcee 2.2.1 restated in numpy on IAS15 logL and the same Philox draws.
+    X0: start from these positions [W][dim] (e.g. a chain's steady state) instead of a ball."""
     torch = _torch()
     from rvmcmc.ensemble import EnsembleSampler
     from rvmcmc.state import State
@@ -73,8 +75,9 @@ def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, roundoff=F
     pm = s.param_map()
     dim = s.Nvars
     scales = np.array([S2_SCALES[k] for k in s.get_rawkeys()])
-    rng = np.random.default_rng(ball_seed)
-    X0 = s.get_params()[None] + ball * scales * rng.standard_normal((W, dim))
+    if X0 is None:
+        rng = np.random.default_rng(ball_seed)
+        X0 = s.get_params()[None] + ball * scales * rng.standard_normal((W, dim))
     ens = EnsembleSampler(W, s, obs, seed=seed)
     ens.set_positions(X0)
     ens.compute_lnprob()
@@ -149,12 +152,80 @@ def test_stretch_vs_ias15_wide_ball_encounters():
                                  warm=0, roundoff=True, ball_seed=3)
     rep = tally.report(**info)
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    # no proposal is left UNRESOLVED (a forced reject the reference never makes): device status 4 is
+    # never exempt, and none occurs
+    assert rep["unresolved_device"] == 0 and not any(k.startswith("4/") for k in rep["status_pairs_device/ias15"])
     assert rep["encounters_ias15"] > 20 and rep["prior_rejections"] > 20
     assert rep["exempt_status_disagreement"] <= max(4, rep["decisions"] // 100)
     assert rep["exempt_current_status_disagreement"] <= max(4, rep["decisions"] // 100)
     assert rep["ok_proposals_dlogl_above_margin_not_roundoff"] == 0
     assert rep["max_abs_dlogl_ok_proposals_not_roundoff"] <= T2_ABS
     assert rep["exempt_ias15_roundoff_sensitive"] <= rep["decisions"] // 100
+
+
+def test_stretch_vs_ias15_steady_state():
+    """The bench chain at its steady state: 4096 walkers from the ensemble after 2000 iterations
+    (scripts/probe/ens_it2000.npy, scripts/dump_bench_ensemble.py), where the posterior is wide in h, k
+    (eccentricities to 0.45) and the plan's fixed step alone missed T2 on 668 of 5823 proposals.  Two
+    speculative iterations of the real sampler; every decision and every OK proposal's logL against
+    IAS15 (the adaptive resolution's regime: extensions, halving passes, certain rejects)."""
+    import os
+
+    from conftest import ROOT
+
+    X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_it2000.npy"))
+    tally, info = stretch_parity("stretch/steady-state S2 4096 walkers (iteration 2000)", S2_PLANETS, s2_obs_oracle(),
+                                 len(X0), 0.0, warm=0, roundoff=True, X0=X0)
+    rep = tally.report(**info)
+    assert info["speculative"]
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["unresolved_device"] == 0
+    assert rep["ok_proposals_dlogl_above_margin_not_roundoff"] == 0
+    assert rep["max_abs_dlogl_ok_proposals_not_roundoff"] <= T2_ABS
+    assert rep["exempt_status_disagreement"] <= max(4, rep["decisions"] // 500)
+
+
+def _burned_in(planets, obs, W, iters, seed=2017):
+    """An ensemble after `iters` iterations of the device sampler from the tight ball (the chain's
+    steady state, the regime of the adaptive resolution)."""
+    torch = _torch()
+    from rvmcmc.ensemble import EnsembleSampler
+    from rvmcmc.state import State
+
+    s = State(planets=[dict(p) for p in planets])
+    scales = np.array([S2_SCALES[k] for k in s.get_rawkeys()])
+    X0 = s.get_params()[None] + 1e-3 * scales * np.random.default_rng(1).standard_normal((W, s.Nvars))
+    ens = EnsembleSampler(W, s, obs, seed=seed + 1)
+    ens.set_positions(X0)
+    ens.compute_lnprob()
+    for _ in range(iters):
+        ens.step()
+    torch.cuda.synchronize()
+    ens.check_faults()
+    return ens.gather_positions()
+
+
+@pytest.mark.parametrize("case", ["HD155358", "3-planet"])
+def test_stretch_vs_ias15_steady_state_other_systems(case):
+    """HD155358 and the 3-planet system at the steady state of their own chains (1000 iterations
+    of the device sampler from the tight ball): the adaptive resolution, and its eccentricity guard,
+    calibrated on S2, must hold T2 on these posteriors too."""
+    if case == "HD155358":
+        planets, obs = _hd()
+        W = 512
+    else:
+        np.random.seed(2017)
+        planets = [dict(p) for p in S2_PLANETS] + [dict(THIRD)]
+        obs = O.fake_obs(planets, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+        W = 512
+    X0 = _burned_in(planets, obs, W, 1000)
+    tally, info = stretch_parity(f"stretch/steady-state {case} {W} walkers (iteration 1000)", planets, obs, W, 0.0,
+                                 warm=0, roundoff=True, X0=X0)
+    rep = tally.report(**info)
+    assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
+    assert rep["unresolved_device"] == 0
+    assert rep["ok_proposals_dlogl_above_margin_not_roundoff"] == 0
+    assert rep["max_abs_dlogl_ok_proposals_not_roundoff"] <= T2_ABS
 
 
 def test_stretch_vs_ias15_config2():

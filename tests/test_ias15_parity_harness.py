@@ -93,3 +93,50 @@ def test_adaptive_resolution_keeps_t2_on_a_wide_ball():
     assert (rf == 1).sum() > 5 and (rf >= 2).sum() > 5 and ok.sum() > 40  # (both stages: extension, halving)
     assert d_adapt.max() <= IP.MARGIN, d_adapt.max()
     assert np.abs(l0[ok0] - li[ok0]).max() > 1e-3  # (the fixed-step algorithm alone misses T2 here)
+
+
+def test_joint_certain_reject_at_the_steady_state():
+    """The walker-level rule (rvoracle.c rvo_logl_whx_adapt) on stretch proposals
+    formed from the bench chain's ensemble after 2000 iterations (scripts/probe/ens_it2000.npy), the
+    regime where the per-direction rule of round 3 climbed to 3-4 halvings: with both directions'
+    lower bounds in the certain-reject test no proposal needs more than one halving pass, no cut
+    proposal is one IAS15 would accept, nothing is left UNRESOLVED, and every uncut OK proposal is
+    within T2 of IAS15."""
+    import os
+
+    from conftest import ROOT
+    from rvmcmc import engine
+
+    E = np.load(os.path.join(ROOT, "scripts", "probe", "ens_it2000.npy"))
+    obs = s2_obs_oracle()
+    n = 192
+    X, C = E[:n], E[2048:2048 + n]
+    rng = np.random.default_rng(7)
+    z = ((2.0 - 1.0) * rng.random(n) + 1.0) ** 2 / 2.0
+    j = rng.integers(0, n, n)
+    u = rng.random(n)
+    Q = C[j] - z[:, None] * (C[j] - X)
+
+    def rows(A):
+        P = np.zeros((len(A), 2, 7))
+        P[:, :, :5] = A.reshape(-1, 2, 5)
+        return P
+
+    cfg = engine.IntegratorConfig()
+    dt, mult, _ = cfg.plan_args(S2_PLANETS)
+    tol, rmax, guard = cfg.resolve(S2_PLANETS)
+    l0 = IP.ias15_logl(rows(X), 2, obs)[0]
+    li, si = IP.ias15_logl(rows(Q), 2, obs)
+    ctx = dict(mode=np.ones(n, dtype=np.int32), dim=10, z=z, u=u, lnp0=l0)
+    la, sa, rf, _, margin, cut = O.logl_whx_adapt_batch(rows(Q), 2, obs, dt, mult, tol, rmax, ecc_guard=guard, ctx=ctx)
+    acc_ias = 9.0 * np.log(z) + li - l0 > np.log(u)
+    cutw = cut.any(axis=1)
+    assert (rf == 1).sum() > 20 and cutw.sum() > 5  # (the regime: extensions and certain rejects)
+    assert rf.max() <= 2, np.bincount(rf.ravel())  # (stage 2 = one halving pass)
+    assert not np.any(cutw & acc_ias)
+    assert not np.any(sa == O.ORACLE_UNRESOLVED)
+    ok = (sa == 0) & (si == 0) & ~cutw
+    assert np.abs(la[ok] - li[ok]).max() <= IP.MARGIN
+    # a cut proposal reports the upper bound its rejection was decided on: still a reject
+    with np.errstate(invalid="ignore"):
+        assert not np.any(cutw & (9.0 * np.log(z) + la - l0 > np.log(u)))
