@@ -619,6 +619,10 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const bool of = d == 0 ? open : open_o, ob = d == 0 ? open_o : open;
         const double cf = d == 0 ? v_m : v_o, cb = d == 0 ? v_o : v_m;
         int stw = sf != RVM_STATUS_OK ? sf : sb;  // both directions see the same PRIOR verdict
+        // (an encounter in one direction ends the walker whatever the other's resolution: a direction
+        // left UNRESOLVED by a flag-only plan does not hide it -- oracle/rvoracle.c any_enc)
+        if (stw == RVM_STATUS_UNRESOLVED && (sf == RVM_STATUS_ENCOUNTER || sb == RVM_STATUS_ENCOUNTER))
+            stw = RVM_STATUS_ENCOUNTER;
         const double lp0 = -((cb + cf) / P.npoints);  // state.py:98, 109 (open: the upper bound lp_hi)
         if (stw == RVM_STATUS_OK && (of || ob)) {
             int dmode = 0;
@@ -960,7 +964,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             // one epoch: the levels in order 0..3 (same arithmetic as the LDS-coupled path), b1 the
             // HBM-handed level's bits
             auto consume = [&](const int e, const unsigned long long b1) {
-                const double* rg = ring + (size_t)rr * WPB + slot;
+                double* rg = ring + (size_t)rr * WPB + slot;
                 const size_t rs = (size_t)RING * WPB;
                 const double vh = __longlong_as_double((long long)b1);
                 double v[4];
@@ -994,10 +998,14 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                         const double q = r5 - l_rv[e];
                         c5x += (q * q) / l_s2[e];
                         ddx += fabs((r5 - rvx) * (q + (rvx - l_rv[e]))) / l_s2[e];
+                        // the RV for a refinement's first step-doubling change, kept in level 0's ring
+                        // slot (read; the ring holds the whole direction) and written to HBM only for
+                        // the walkers the refinement kernel gets (below)
+                        rg[(ul * 4 + 2) * rs] = rvx;
                     } else {
                         P.lvx[xi] = s5;
+                        P.rvp[xi] = rvx;
                     }
-                    P.rvp[xi] = rvx;
                 }
                 // (the levels wait on it only when the ring wraps; a release store also waits for
                 // every load in flight, the prefetched HBM values included)
@@ -1138,6 +1146,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 const double lb = direction_lb(nd, cm, es, (f & 16) != 0, xc5, xdd);
                 if (cl) finish_recompute(w0 + lane, c2, en, nd, lb);
             } else if (valid && pl_idx == 0) {
+                if (lsx && need) {  // the main pass's RV of an open direction (the ring, consume above)
+                    const double* rg = ring + (size_t)(ul * 4 + 2) * RING * WPB + slot;
+                    for (int e = 0; e < E; e++)
+                        P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = rg[(size_t)e * WPB];
+                }
                 finish_recompute(w, chi2w, enc, need, direction_lb(need, chi2m, est, lsx && need0, c5x, ddx));
             }
 #ifdef RVM_PROFILE

@@ -170,6 +170,7 @@ class EnsembleSampler:
             raise ValueError("The number of walkers needs to be more than twice the dimension of your parameter space.")
         self.k = int(nwalkers)
         self.dim = dim
+        self.comm_timing = None  # set to [] to collect HIP events around the collectives (N > 1)
         self.a = float(a)
         self.seed = int(seed) & ((1 << 64) - 1)
         self.state = state
@@ -365,11 +366,24 @@ class EnsembleSampler:
         launch (one all-gather of the pair buffer, re-laid out by one copy), half 0's decisions
         between the two launches."""
         torch = _torch()
+        ct = self.comm_timing is not None and self.world > 1
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if ct else None
+        if ct:
+            ev[0].record()
         c0, c1 = self.gather_mirrors()
+        if ct:
+            ev[1].record()
         dec_all = self._dec if self.world == 1 else self._dec_all
         self.ops.iteration_begin(c0, c1)
         if self.world > 1:
+            if ct:
+                ev[2].record()
+            # (every rank's half-0 decisions: this is where a rank waits for the slowest rank's
+            # likelihood and refinement kernels)
             torch.distributed.all_gather_into_tensor(self._dec_all, self._dec, group=self.group)
+            if ct:
+                ev[3].record()
+                self.comm_timing.append(ev)
         self.ops.iteration_end(c0, c1, dec_all)
         self.nevals += 2 * self.nloc
         self.nevals_speculative += self.nloc
