@@ -19,7 +19,8 @@ namespace rvm {
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
                        double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
 hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                         int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
+                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen,
+                         hipStream_t stream);
 hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
                                   uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
                                   double* z, hipStream_t st);
@@ -72,6 +73,7 @@ struct rvm_plan {
     // `cap` launches (the kernels' own durations on their stream, for the bench's roofline)
     mutable std::vector<hipEvent_t> tev;
     mutable int32_t tcap = 0, tn = 0;
+    mutable unsigned long long gen = 0;  // refinement launches so far (the split exchange's flag tag)
 };
 
 // One likelihood evaluation as every entry point runs it: the likelihood kernel, then (adaptive
@@ -82,7 +84,8 @@ static hipError_t run_logl(const rvm_plan* plan, int W, const double* params, do
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn], st);
     hipError_t e = rvm::launch_logl(plan->dev, W, params, hill_factor, plan->slots, logl, status, rv_out, sa, st);
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 1], st);
-    if (e == hipSuccess) e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, st);
+    if (e == hipSuccess)
+        e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, ++plan->gen, st);
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 2], st);
     if (tm) plan->tn++;
     return e;
@@ -417,20 +420,34 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.rq_w = nullptr;
     P.rq_c = nullptr;
     P.rq_cap = 0;
+    P.rq_x = nullptr;
+    P.rq_xf = nullptr;
+    P.rq_xgroups = 0;
     if (P.rmax > 0) {
+        // (+ the split exchange: flags and double-buffered values per both-direction group of up to 64
+        // walkers; groups of 16 walkers at 3-4 planets)
+        const int64_t xg = ((int64_t)max_walkers + 15) / 16 + 1;
+        const size_t b_x = (size_t)xg * 2 * 2 * 64 * sizeof(unsigned long long);
+        const size_t b_xf = (size_t)xg * 2 * sizeof(unsigned long long);
         const size_t b_c = 2 * (size_t)max_walkers * sizeof(double);
         const size_t b_w = 3 * (size_t)max_walkers * sizeof(int32_t);
-        if (hipMalloc(&plan->rqmem, b_c + b_w + 64) != hipSuccess ||
-            hipMemset(plan->rqmem, 0, b_c + b_w + 64) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        const size_t b_all = b_x + b_xf + b_c + b_w + 64;
+        if (hipMalloc(&plan->rqmem, b_all) != hipSuccess || hipMemset(plan->rqmem, 0, b_all) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
             rvm_plan_destroy(plan);
             return fail(-3, "rvm_plan_create: hipMalloc of the refinement work lists failed");
         }
         unsigned char* base = reinterpret_cast<unsigned char*>(plan->rqmem);
-        P.rq_c = reinterpret_cast<double*>(base);
-        P.rq_w = reinterpret_cast<int32_t*>(base + b_c);
-        P.rq_n = reinterpret_cast<int32_t*>(base + b_c + b_w);
+        P.rq_x = reinterpret_cast<unsigned long long*>(base);
+        P.rq_xf = reinterpret_cast<unsigned long long*>(base + b_x);
+        P.rq_c = reinterpret_cast<double*>(base + b_x + b_xf);
+        P.rq_w = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_c);
+        P.rq_n = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_c + b_w);
         P.rq_cap = max_walkers;
+        P.rq_xgroups = (int32_t)xg;
+        if (const char* sp = getenv("RVM_REFINE_SPLIT"))  // (A/B knob: 0 keeps both directions in one block)
+            if (sp[0] == '0') P.rq_x = nullptr;
     }
     *out = plan;
     return 0;

@@ -78,6 +78,12 @@ struct DevPlan {
     int32_t* rq_w;
     double* rq_c;
     int32_t rq_cap;
+    // a both-direction group split over two workgroups exchanges its walkers' per-direction state
+    // after every halving pass (rvm_refine.hip): rq_x [groups][2 directions][2 pass parities][64]
+    // values in the meeting slot's encoding, rq_xf [groups][2] the flag (launch generation << 8 | pass)
+    unsigned long long* rq_x;
+    unsigned long long* rq_xf;
+    int32_t rq_xgroups;
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
     // [3] walker-direction refinement passes (extension + halvings), [4] refinements cut short as

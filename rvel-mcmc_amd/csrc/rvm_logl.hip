@@ -56,20 +56,11 @@ __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 // bypassed) and puts the sentinel back: the value is the flag (cdna_hip_programming.md §6
 // Guideline 16, R2), no fence on either side.  Encounter / prior flags likewise in P.lv_enc (-1).
 #define RVM_LV_EMPTY 0xFFFFFFFFFFFFFFFFULL
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) int gi32;
 // Bounded waits: a hand-off wait gives up after P.spin_ticks of the 100 MHz real-time counter
 // WITHOUT PROGRESS (the clock restarts at every epoch that arrives, so a long launch never times
 // out while it advances), counts the give-up in the plan's fault counter (rvm_plan_faults) and
 // reports its walkers NONFINITE instead of hanging the GPU.  Blocks are all resident by
 // construction: launch_logl uses the layout only when its grid fits the CUs.
-struct SpinClock {
-    unsigned long long last;
-    __device__ __forceinline__ void restart() { last = __builtin_amdgcn_s_memrealtime(); }
-    __device__ __forceinline__ bool expired(unsigned long long ticks) const {
-        return __builtin_amdgcn_s_memrealtime() - last > ticks;
-    }
-};
 
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
 template <int NP, bool D3, bool DEC>

@@ -45,7 +45,7 @@ template <int NP, bool D3>
 __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int W, const double* __restrict__ params,
                                                      const double hill_factor, double* __restrict__ rv_out,
                                                      double* __restrict__ logl_out, int32_t* __restrict__ status_out,
-                                                     const StretchArgs sa) {
+                                                     const StretchArgs sa, const unsigned long long gen) {
     constexpr int L = LanesPerWalker<NP>::value;
     constexpr int WPB = 64 / L;
     constexpr int PR = D3 ? 7 : 5;
@@ -69,7 +69,16 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     const int nq[3] = {s_n[0], s_n[1], s_n[2]};
     const int gq0 = (nq[0] + WPB - 1) / WPB, gq1 = (nq[1] + WPB - 1) / WPB, gq2 = (nq[2] + WPB - 1) / WPB;
     const int ng = gq0 + gq1 + gq2;
-    if ((int)blockIdx.x >= ng) return;
+    // split: each both-direction group's two directions on two workgroups (2j, 2j + 1) -- every
+    // direction's levels then alone on their SIMDs (7 x 2^rf steps per base step on the busiest
+    // instead of 11 x 2^rf with both in one block) -- exchanging the walkers' per-direction state
+    // after every pass; only when every task has a workgroup of its own in the grid (all co-resident
+    // once dispatched; in-order dispatch leaves at most one workgroup waiting for its partner)
+    const int ntask_split = 2 * gq0 + gq1 + gq2;
+    const bool split = P.rq_x != nullptr && gq0 <= P.rq_xgroups && ((int)gridDim.x & 1) == 0 &&
+                       ntask_split <= (int)gridDim.x;
+    const int ntask = split ? ntask_split : ng;
+    if ((int)blockIdx.x >= ntask) return;
 
     // LDS: both directions' schedules ([d][seg_h1 | obs_rv | obs_s2 | (seg_n, obs_idx)], E_d each),
     // the levels' star vx per epoch (double-buffered), encounter flags, the lanes' state at t = 0,
@@ -86,6 +95,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     __shared__ double s_acc[3][64];  // its accept inputs z, u, lnp0 (s_dmode: 0 none, 1 stretch, 2 MH)
     __shared__ int s_dmode[64];
     __shared__ unsigned long long s_mask[2];
+    __shared__ int s_xfault;  // a split task's exchange gave up (its walkers end NONFINITE)
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     for (int dd = 0; dd < 2; dd++) {
         const DirSched& SD = dd ? P.bwd : P.fwd;
@@ -104,7 +114,17 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     const bool mh = sa.mh_scale != nullptr;
     const bool mapped = stretch || mh || sa.fd_x != nullptr;
 
-    for (int g = blockIdx.x; g < ng; g += gridDim.x) {
+    for (int t = blockIdx.x; t < ntask; t += gridDim.x) {
+        // the task's group, and (split both-direction group) the direction this workgroup integrates
+        int g = t, own = -1;
+        if (split) {
+            if (t < 2 * gq0) {
+                g = t >> 1;
+                own = t & 1;
+            } else {
+                g = t - gq0;
+            }
+        }
         const int li = g < gq0 ? 0 : (g < gq0 + gq1 ? 1 : 2);
         const int base = (li == 0 ? g : (li == 1 ? g - gq0 : g - gq0 - gq1)) * WPB;
         const int cnt = nq[li] - base < WPB ? nq[li] - base : WPB;
@@ -150,6 +170,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             if (lane == 0) {
                 s_mask[0] = m0;
                 s_mask[1] = m1;
+                s_xfault = 0;
             }
         }
         // the decision lanes' accept inputs (wave 0, lane = walker slot), kept in LDS through the passes
@@ -167,10 +188,12 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
 
         for (int rf = 1; rf <= P.rmax; rf++) {
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
-            const int am = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);
-            if (am == 0) break;
-            // sub-passes: both directions at once (up to four levels), else one after the other
-            const int nsub = (am == 3 && nl > 4) ? 2 : 1;
+            const int amw = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);  // directions a live walker still needs
+            if (amw == 0) break;
+            const int am = own < 0 ? amw : (amw & (1 << own));  // the ones this workgroup integrates
+            // sub-passes: both directions at once (up to four levels), else one after the other;
+            // none when a split task's own direction is done (the partner's pass only)
+            const int nsub = am == 0 ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
             for (int sp = 0; sp < nsub; sp++) {
                 // this wave's (direction, level) task, or none
                 const bool both = am == 3 && nl <= 4;
@@ -272,7 +295,61 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 }
             }
             __syncthreads();
-            // the walker's decision (wave 0, lane = walker slot)
+            if (own >= 0 && wv == 0) {
+                // split: publish this direction's state of every walker (the meeting slot's encoding,
+                // rvm_walker.h: chi2, -lb, or the ENCOUNTER status) as write-through granules, drain,
+                // one lane stores the flag (launch generation, pass); then the partner's, after its
+                // flag and one agent-scope acquire (cdna_hip_programming.md §6 Guideline 16, R1).
+                // Double-buffered by the pass's parity: a partner reads pass rf's values before it
+                // publishes rf + 1, which this workgroup awaits before it writes rf + 2.
+                const size_t xb = ((size_t)g * 2) * 2 * 64;
+                gu64* mine = (gu64*)(P.rq_x + xb + ((size_t)own * 2 + (rf & 1)) * 64);
+                gu64* theirs = (gu64*)(P.rq_x + xb + ((size_t)(own ^ 1) * 2 + (rf & 1)) * 64);
+                if (lane < WPB) {
+                    const int o = s_open[own][lane];
+                    const unsigned long long b =
+                        o == 2 ? slot_status(RVM_STATUS_ENCOUNTER)
+                               : (unsigned long long)__double_as_longlong(o == 1 ? -s_lb[own][lane] : s_chi[own][lane]);
+                    __hip_atomic_store(mine + lane, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned long long tag = (gen << 8) | (unsigned long long)rf;
+                if (lane == 0)
+                    __hip_atomic_store((gu64*)(P.rq_xf + (size_t)g * 2 + own), tag, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                gu64* tf = (gu64*)(P.rq_xf + (size_t)g * 2 + (own ^ 1));
+                SpinClock clk;
+                clk.restart();
+                bool ok = true;
+                while (__hip_atomic_load(tf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) {
+                    if (clk.expired(P.spin_ticks)) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (!ok) {
+                    if (lane == 0) {
+                        s_xfault = 1;
+                        __hip_atomic_fetch_add(P.counters, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                } else if (lane < WPB) {
+                    const unsigned long long b = __hip_atomic_load(theirs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const int od = own ^ 1;
+                    if (slot_is_status(b)) {
+                        s_open[od][lane] = 2;
+                    } else {
+                        const double v = __longlong_as_double((long long)b);
+                        s_open[od][lane] = signbit(v) ? 1 : 0;
+                        s_chi[od][lane] = fabs(v);  // (an open direction's chi2 is not needed: only its lb)
+                        s_lb[od][lane] = fabs(v);
+                    }
+                }
+            }
+            // the walker's decision (wave 0, lane = walker slot; a split task's two workgroups take the
+            // same decisions from the same states)
             if (wv == 0) {
                 bool live = lane < WPB && s_live[lane] != 0;
                 if (live) {
@@ -280,7 +357,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     int stw = RVM_STATUS_OK;
                     double lp = 0.0;
                     bool done = true;
-                    if (of == 2 || ob == 2) {
+                    if (s_xfault) {
+                        stw = RVM_STATUS_NONFINITE;
+                    } else if (of == 2 || ob == 2) {
                         stw = RVM_STATUS_ENCOUNTER;
                     } else if (of == 0 && ob == 0) {
                         lp = -((s_chi[1][lane] + s_chi[0][lane]) / P.npoints);  // state.py:98, 109
@@ -291,8 +370,10 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                         if (dmode != 0 && isfinite(lp_hi) &&
                             !accepts_at(sa, dmode, s_acc[0][lane], s_acc[1][lane], s_acc[2][lane], lp_hi)) {
                             lp = lp_hi;  // a certain reject
-                            __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)((of ? 1 : 0) + (ob ? 1 : 0)),
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            if (own <= 0)
+                                __hip_atomic_fetch_add(P.counters + 4,
+                                                       (unsigned long long)((of ? 1 : 0) + (ob ? 1 : 0)),
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         } else if (rf == P.rmax) {
                             stw = RVM_STATUS_UNRESOLVED;
                         } else {
@@ -315,8 +396,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             }
             __syncthreads();
         }
-        // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h)
-        if (wv == 0 && lane < WPB && lane < cnt) {
+        // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h;
+        // a split group's by its forward-direction workgroup)
+        if (own <= 0 && wv == 0 && lane < WPB && lane < cnt) {
             int k2 = 0, wk2 = wme, j2 = 0, jp2 = 0;
             double z2 = 0.0, zp2 = 0.0;
             if (stretch) stretch_slot(sa, wme, k2, wk2, z2, j2, zp2, jp2);
@@ -331,7 +413,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
 
 template <int NPV, bool D3V>
 static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                                  int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
+                                  int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen,
+                                  hipStream_t stream) {
     constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t smem = (size_t)emax * 8 * sizeof(double);
@@ -352,19 +435,23 @@ static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params,
     if (smem > budget[dev]) return hipErrorInvalidConfiguration;
     // every block reads the list sizes (the last one resets them): a grid of at most one block
     // per CU, and no more than the lists could fill
+    // (an even count: a split group's two workgroups are 2j, 2j + 1)
     const int groups = (W + wpb - 1) / wpb + 2;
-    const int nb = std::max(1, std::min(P.n_cu > 0 ? P.n_cu : 256, groups));
-    refine_kernel<NPV, D3V><<<dim3(nb), dim3(512), smem, stream>>>(P, W, params, hill_factor, rv_out, logl, status, sa);
+    int nb = std::max(2, std::min(P.n_cu > 0 ? P.n_cu : 256, 2 * groups));
+    nb &= ~1;
+    refine_kernel<NPV, D3V><<<dim3(nb), dim3(512), smem, stream>>>(P, W, params, hill_factor, rv_out, logl, status, sa,
+                                                                   gen);
     return hipGetLastError();
 }
 
 hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                         int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream) {
+                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen,
+                         hipStream_t stream) {
     if (P.rmax <= 0 || P.rq_n == nullptr) return hipSuccess;
     const bool inc = P.inclined != 0;
-#define RVM_LAUNCH_R(NPV)                                                                        \
-    (inc ? launch_refine_t<NPV, true>(P, W, params, hill_factor, logl, status, rv_out, sa, stream) \
-         : launch_refine_t<NPV, false>(P, W, params, hill_factor, logl, status, rv_out, sa, stream))
+#define RVM_LAUNCH_R(NPV)                                                                             \
+    (inc ? launch_refine_t<NPV, true>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, stream) \
+         : launch_refine_t<NPV, false>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, stream))
     switch (P.n_planets) {
         case 1:
             return RVM_LAUNCH_R(1);

@@ -243,6 +243,20 @@ __device__ __forceinline__ void walker_setup(const double* rowv, const int pl_id
     lane_finish(s);
 }
 
+// global-address-space views for agent-scope atomics (cdna_hip_programming.md §6 Guideline 16)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+// Bounded waits: a cross-workgroup wait gives up after P.spin_ticks of the 100 MHz real-time counter
+// WITHOUT PROGRESS (restarted whenever the awaited side advances), counts the give-up in the plan's
+// fault counter (rvm_plan_faults) and reports its walkers NONFINITE instead of hanging the GPU.
+struct SpinClock {
+    unsigned long long last;
+    __device__ __forceinline__ void restart() { last = __builtin_amdgcn_s_memrealtime(); }
+    __device__ __forceinline__ bool expired(unsigned long long ticks) const {
+        return __builtin_amdgcn_s_memrealtime() - last > ticks;
+    }
+};
+
 // ---- the two directions of a walker meet (rvm_logl.hip finish) -------------------------------
 // One 64-bit slot per walker (plan workspace, RVM_SLOT_EMPTY between launches).  The direction that
 // arrives first leaves its result there, the second takes it with one agent-scope exchange:

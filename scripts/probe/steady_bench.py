@@ -20,7 +20,9 @@ from rvmcmc.observations import FakeObservation  # noqa: E402
 from rvmcmc.state import State  # noqa: E402
 
 
-def run(resolve_tol, levels=(4, 5, 6, 7), resolve_max=4, iters=10, warm=3):
+def run(resolve_tol, levels=(4, 5, 6, 7), resolve_max=None, iters=30, warm=3):
+    if resolve_max is None:
+        resolve_max = engine.IntegratorConfig().resolve_max
     state = State(planets=[dict(p) for p in S2_PLANETS])
     state.integrator = engine.IntegratorConfig(resolve_tol=resolve_tol, levels=tuple(levels), resolve_max=resolve_max)
     np.random.seed(2017)
@@ -49,5 +51,5 @@ if __name__ == "__main__":
     specs = sys.argv[1:] or ["4,5,6,7:0", "4,5,6,7:5e-7"]
     for sp in specs:
         f = sp.split(":")
-        print(json.dumps(run(float(f[1]), tuple(int(v) for v in f[0].split(",")), int(f[2]) if len(f) > 2 else 4)),
+        print(json.dumps(run(float(f[1]), tuple(int(v) for v in f[0].split(",")), int(f[2]) if len(f) > 2 else None)),
               flush=True)

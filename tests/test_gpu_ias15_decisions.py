@@ -372,10 +372,12 @@ def test_smala_step_vs_ias15():
     """Exact-metric SMALA (the reference's Hessian, state.py:253-294), 128 chains."""
     rep, tally = smala_parity("smala/S2 128 chains exact metric", "exact", 128)
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
-    # eps = 0.5 in the metric's units reaches several posterior widths: the exact-derivative launch
-    # (rvm_logl_derivs) has no adaptive resolution, so a few proposals may leave the T2 regime
-    # (measured round 2: 1 of 128 at 2.7e-6); they are counted, and their decisions still agree
-    assert rep["ok_proposals_dlogl_above_margin"] <= 128 // 20
+    # the logp the accept uses is the adaptive plan's (SmalaChains._center_start, beside the
+    # derivative launch), so T2 holds on every OK proposal as on the other paths (eps = 0.5 in the
+    # metric's units reaches several posterior widths; round 2, before the adaptive resolution: 1 of
+    # 128 at 2.7e-6)
+    assert rep["exempt_status_disagreement"] == 0
+    assert rep["max_abs_dlogl_ok_proposals"] <= T2_ABS
     assert 0 < rep["accepted_ias15"]
 
 
