@@ -1003,8 +1003,8 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /*   the stored levels: r5 = Richardson over all nl + 1 levels.  Settled (chi2 from r5) when     */
 /*     dd = sum |(r5 - o)^2 - (r - o)^2| / s2 <= EXT_ACCEPT * tol_dir * npoints                   */
 /*   -- the change of chi2 the extension brought, an estimate of the main pass's own error (and  */
-/*   a conservative one of r5's: measured, r5's error stays below 2.6 tol_dir wherever this      */
-/*   holds);                                                                        */
+/*   a conservative one of r5's: measured, r5's error stays below 0.43 tol_dir wherever this     */
+/*   holds at EXT_ACCEPT = 1 (2.6 tol_dir at 2, round 3));                          */
 /*  stages 2..: passes with every step halved (level k: mult 2^rf steps per base step, rf = 1..  */
 /*   rf_max) over every direction still open, until est <= tol_dir; still open after rf_max:     */
 /*   RVO_UNRESOLVED.                                                                             */
@@ -1025,7 +1025,7 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /* ------------------------------------------------------------------------------------------ */
 enum { RVO_UNRESOLVED = 4 };
 #ifndef EXT_ACCEPT /* (overridable for studies of the rule: -DEXT_ACCEPT=...) */
-#define EXT_ACCEPT 2.0
+#define EXT_ACCEPT 1.0
 #endif
 #ifndef CUT_EST_FACTOR
 #define CUT_EST_FACTOR 100.0

@@ -371,13 +371,12 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const size_t emax = std::max<size_t>(std::max(nf, nb), 1);
         const size_t bl = 2 * emax * (size_t)max_walkers * sizeof(double);  // partial sums
         const size_t bx = 2 * bl;                                           // + last RV
-        if (bx <= RVM_EXT_MAX_BYTES) {
-            if (hipMalloc(&plan->xmem, bx) != hipSuccess) {
-                plan->xmem = nullptr;
-                (void)hipGetLastError();
-                rvm_plan_destroy(plan);
-                return fail(-3, "rvm_plan_create: hipMalloc of the extension's stored levels failed");
-            }
+        // (a failed allocation is not an error: the plan refines by halving passes alone, ext_mult 0)
+        if (bx <= RVM_EXT_MAX_BYTES && hipMalloc(&plan->xmem, bx) != hipSuccess) {
+            plan->xmem = nullptr;
+            (void)hipGetLastError();  // (clear the runtime's sticky status)
+        }
+        if (plan->xmem != nullptr) {
             int m5[RVM_MAX_LEVELS + 1];
             int fin = 0;
             for (int k = 0; k < nl; k++) {

@@ -67,7 +67,7 @@ class IntegratorConfig:
     # fixed step; at the chain's steady state 6.2 ms against 0.69.  resolve_tol = 0
     # turns it off (the round-2 fixed-step algorithm).
     resolve_tol: float = 5e-7
-    resolve_max: int = 8
+    resolve_max: int = 12
     # eccentricity guard (rvm_plan_set_verify_eccentricity): walkers whose pericentre passage is more
     # than this factor quicker than the plan's reference orbit's always get the extension -- the
     # estimate under-read on such orbits (all three T2 misses it left at the bench chain's steady
