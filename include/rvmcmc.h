@@ -125,6 +125,15 @@ int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult);
  * passage is much quicker than the plan's reference orbit.  e <= 0: off (default). */
 int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e);
 
+/* The certain-reject test of the adaptive resolution (on: default).  On fused sampler launches a
+ * walker whose accept test fails even at the upper bound on its logL that both directions' lower
+ * bounds on chi2 give stops refining and reports that bound (a certain reject).  The bound of an
+ * open direction is empirical (chi2 less the change its last stage brought, capped at 100 x its
+ * estimate; the measured error / estimate stays <= 57), so on = 0 lets every
+ * open walker refine to the plan's tolerance instead.  Replaces nothing in the reference (IAS15
+ * integrates every proposal in full, state.py:61-73). */
+int rvm_plan_set_certain_reject(rvm_plan* plan, int32_t on);
+
 /* Counters of a plan since its creation or the last reset, read in order on `stream` (the call
  * synchronises that stream; any output pointer may be NULL):
  *   handoff_timeouts  level-split hand-off waits that gave up (rvm_plan_set_handoff_timeout): their

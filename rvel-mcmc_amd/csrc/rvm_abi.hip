@@ -290,6 +290,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     }
     P.rtol_dir = cfg->resolve_tol > 0.0 && cfg->n_levels >= 2 ? 0.5 * cfg->resolve_tol : INFINITY;
     P.rmax = P.rtol_dir < INFINITY ? rmax : 0;
+    P.cut = 1;
     P.spin_ticks = 200000000ull;  // 2 s of the 100 MHz real-time counter without progress
     for (int k = 0; k < cfg->n_levels; k++) {
         const double xk = 1.0 / ((double)mult[k] * mult[k]);
@@ -460,6 +461,12 @@ void rvm_plan_destroy(rvm_plan* plan) {
     if (plan->xmem) (void)hipFree(plan->xmem);
     if (plan->dmem) (void)hipFree(plan->dmem);
     delete plan;
+}
+
+int rvm_plan_set_certain_reject(rvm_plan* plan, int32_t on) {
+    if (!plan) return fail(-1, "rvm_plan_set_certain_reject: null plan");
+    plan->dev.cut = on ? 1 : 0;
+    return 0;
 }
 
 int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e) {

@@ -57,6 +57,9 @@ struct DevPlan {
     double lw3[RVM_MAX_LEVELS];
     double rtol_dir;   // +inf: no estimate check
     int32_t rmax;
+    // 1: the certain-reject test runs on fused sampler launches (rvm_plan_set_certain_reject; an
+    // empirical lower bound on chi2), 0: every open walker refines to the bound
+    int32_t cut;
     // the extension (stage 1, rvm_logl.hip extend_pass): one more level of ext_mult steps per base
     // step (0: none) joined to the main pass's levels; lw5 = the weights of all n_levels + 1 levels.
     // Every launch keeps, per direction, epoch and walker ([2][lvx_emax][lvx_stride]), lvx = the

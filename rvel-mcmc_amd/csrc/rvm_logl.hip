@@ -618,7 +618,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         if (stw == RVM_STATUS_OK && (of || ob)) {
             int dmode = 0;
             double dz, du, dl;
-            if (P.ext_mult > 0) accept_inputs(sa, wo, dmode, dz, du, dl);
+            if (P.ext_mult > 0 && P.cut) accept_inputs(sa, wo, dmode, dz, du, dl);
             if (dmode != 0 && isfinite(lp0) && !accepts_at(sa, dmode, dz, du, dl, lp0)) {
                 // a certain reject: rejected whatever the refinement would give; reports lp_hi
                 __hip_atomic_fetch_add(P.counters + 4, (unsigned long long)((of ? 1 : 0) + (ob ? 1 : 0)),

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         if (wv == 0 && lane < WPB) {
             int dmode = 0;
             double dz = 0.0, du = 0.0, dl = 0.0;
-            if (lane < cnt && P.ext_mult > 0) accept_inputs(sa, wme, dmode, dz, du, dl);
+            if (lane < cnt && P.ext_mult > 0 && P.cut) accept_inputs(sa, wme, dmode, dz, du, dl);
             s_dmode[lane] = dmode;
             s_acc[0][lane] = dz;
             s_acc[1][lane] = du;

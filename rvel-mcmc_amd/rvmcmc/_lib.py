@@ -87,6 +87,7 @@ SIGNATURES = {
                                         C.POINTER(C.c_int32)]),
     "rvm_plan_extension": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rvm_plan_set_verify_eccentricity": (C.c_int, [C.c_void_p, C.c_double]),
+    "rvm_plan_set_certain_reject": (C.c_int, [C.c_void_p, C.c_int32]),
     "rvm_plan_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                 C.POINTER(C.c_int32)]),
     "rvm_logl_batch": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_double, _dp, _dp, _dp, _dp]),

@@ -74,6 +74,14 @@ class IntegratorConfig:
     # state had e >= 0.295 against the reference's 0.218; the guard at 1.1 -> e > 0.266 removes them,
     # DESIGN.md §3).  0: off.
     verify_speedup: float = 1.1
+    # certain-reject test (rvm_plan_set_certain_reject; fused sampler launches only): a proposal whose
+    # accept test fails even at the upper bound on its logL that both directions' lower bounds on
+    # chi2 give stops refining and is rejected.  The bound of an open direction is EMPIRICAL (chi2
+    # less the change its last stage brought, capped at 100 x its estimate; measured error / estimate
+    # <= 57, and no cut proposal was an IAS15 accept in the studies of DESIGN.md §3 item 5;
+    # tests/test_ias15_parity_harness.py re-checks it on every CPU run).  False: every open walker
+    # refines to the tolerance (slower at the steady state, no heuristic in the decision).
+    certain_reject: bool = True
 
     @property
     def mult(self) -> tuple:
@@ -94,10 +102,10 @@ class IntegratorConfig:
         return 2.0 ** (round(math.log2(raw) * DT_GRID) / DT_GRID)
 
     def resolve(self, planets=None) -> tuple:
-        """(resolve_tol, resolve_max, eccentricity guard) for plan_for / LoglPlan; the guard (0: off)
-        from the plan's reference planets: the eccentricity whose pericentre passage is
+        """(resolve_tol, resolve_max, eccentricity guard, certain_reject) for plan_for / LoglPlan; the
+        guard (0: off) from the plan's reference planets: the eccentricity whose pericentre passage is
         verify_speedup times quicker, (1 - e)^-3/2 = verify_speedup (1 - e_ref)^-3/2."""
-        return float(self.resolve_tol), int(self.resolve_max), self.ecc_guard(planets)
+        return float(self.resolve_tol), int(self.resolve_max), self.ecc_guard(planets), bool(self.certain_reject)
 
     def ecc_guard(self, planets) -> float:
         """The guard from the reference planets' largest eccentricity, rounded to the grid
@@ -178,6 +186,7 @@ class LoglPlan:
         self.max_walkers = int(max_walkers)
         self.resolve_tol, self.resolve_max = float(resolve[0]), int(resolve[1])
         self.ecc_guard = float(resolve[2]) if len(resolve) > 2 else 0.0
+        self.certain_reject = bool(resolve[3]) if len(resolve) > 3 else True
         lm = (C.c_int32 * _lib.RVM_MAX_LEVELS)(*self.mult)
         cfg = _lib.RvmConfig(self.n_planets, self.dt, self.n_levels, self.npoints, lm, self.period_hint,
                              int(self.inclined), self.resolve_tol, self.resolve_max)
@@ -194,6 +203,8 @@ class LoglPlan:
         if self.ecc_guard > 0.0:
             _lib.check(self.lib.rvm_plan_set_verify_eccentricity(self._h, self.ecc_guard),
                        "rvm_plan_set_verify_eccentricity")
+        if not self.certain_reject:
+            _lib.check(self.lib.rvm_plan_set_certain_reject(self._h, 0), "rvm_plan_set_certain_reject")
 
     def faults(self, reset=False, stream=None) -> dict:
         """rvm_plan_faults: the plan's counters (synchronises the stream): hand-off timeouts, NONFINITE

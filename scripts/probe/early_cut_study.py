@@ -49,7 +49,7 @@ def main():
     li, si = par(lambda p, ix: O.logl_ias15_batch(p, 2, obs), rows(Q))
     cfg = engine.IntegratorConfig()
     dt, mult, _ = cfg.plan_args(S2_PLANETS)
-    tol, rmax, guard = cfg.resolve(S2_PLANETS)
+    tol, rmax, guard, _ = cfg.resolve(S2_PLANETS)
     ctx = dict(mode=np.ones(n, dtype=np.int32), dim=10, z=z, u=u, lnp0=l0)
     la, sa, rf, _, _, cut = par(lambda p, ix: O.logl_whx_adapt_batch(
         p, 2, obs, dt, mult, tol, rmax, ecc_guard=guard,

@@ -24,7 +24,7 @@ def tau(X):  # X [W][10] rows m,a,h,k,l per planet
     return np.min(t,axis=0)
 cfg=engine.IntegratorConfig()
 x0=np.array([[p[k] for k in 'm a h k l'.split()] for p in S2_PLANETS]).reshape(1,-1)
-dt0,mult,_=cfg.plan_args(S2_PLANETS); tol,rmax,g0=cfg.resolve(S2_PLANETS)
+dt0,mult,_=cfg.plan_args(S2_PLANETS); tol,rmax,g0,_=cfg.resolve(S2_PLANETS)
 t0=tau(x0)[0]; D=dt0/t0
 ens=np.load(os.path.join(ROOT,'profiles','r03_bench_ensemble.npz'))['it2000']
 d=np.load(os.path.join(ROOT,'scripts','probe','slots_it2000.npz'))

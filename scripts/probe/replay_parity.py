@@ -45,7 +45,7 @@ def main():
     hill = s.hillRadiusFactor
     cfg = engine.IntegratorConfig()
     dt, mult, _ = cfg.plan_args(S2_PLANETS)
-    tol, _, guard = cfg.resolve(S2_PLANETS)
+    tol, _, guard, _ = cfg.resolve(S2_PLANETS)
     seed = 2017
 
     def adapt(A):

@@ -35,7 +35,7 @@ def main():
     P[:, :, :5] = X.reshape(-1, 2, 5)
     cfg = engine.IntegratorConfig()
     dt, mult, _ = cfg.plan_args(S2_PLANETS)
-    tol, rmax, guard = cfg.resolve(S2_PLANETS)
+    tol, rmax, guard, _ = cfg.resolve(S2_PLANETS)
     la, sa, rf, _, _ = par(lambda p: O.logl_whx_adapt_batch(p, 2, obs, dt, mult, tol, rmax, ecc_guard=guard), P)
     h = (rf >= 2).any(axis=1) & (sa == 0)
     Ph = P[h]

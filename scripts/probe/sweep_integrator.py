@@ -43,7 +43,7 @@ def main():
         lv, spo = c.split(":")
         cfg = engine.IntegratorConfig(levels=tuple(int(x) for x in lv.split(",")), steps_per_orbit=float(spo))
         dt, mult, _ = cfg.plan_args(S2_PLANETS)
-        tol, rmax, guard = cfg.resolve(S2_PLANETS)
+        tol, rmax, guard, _ = cfg.resolve(S2_PLANETS)
         la, sa, rf, _, _ = par(lambda p: O.logl_whx_adapt_batch(p, 2, obs, dt, mult, tol, rmax, ecc_guard=guard), P)
         ok = (sa == 0) & (si == 0)
         e = np.abs(la - li)[ok]

@@ -45,7 +45,7 @@ def main():
 
     cfg = engine.IntegratorConfig()
     dt, mult, _ = cfg.plan_args(S2_PLANETS)
-    tol, _, guard = cfg.resolve(S2_PLANETS)
+    tol, _, guard, _ = cfg.resolve(S2_PLANETS)
     for A, name in ((X0, "0.6-wide ball, 2048 walkers"), (Q, "stretch proposals between its halves, 1024")):
         for rmax in (4, 6, 8):
             la, sa, rf, _, _ = par(lambda p: O.logl_whx_adapt_batch(p, 2, obs, dt, mult, tol, rmax, ecc_guard=guard),

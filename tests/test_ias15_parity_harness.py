@@ -124,7 +124,7 @@ def test_joint_certain_reject_at_the_steady_state():
 
     cfg = engine.IntegratorConfig()
     dt, mult, _ = cfg.plan_args(S2_PLANETS)
-    tol, rmax, guard = cfg.resolve(S2_PLANETS)
+    tol, rmax, guard, _ = cfg.resolve(S2_PLANETS)
     l0 = IP.ias15_logl(rows(X), 2, obs)[0]
     li, si = IP.ias15_logl(rows(Q), 2, obs)
     ctx = dict(mode=np.ones(n, dtype=np.int32), dim=10, z=z, u=u, lnp0=l0)
