@@ -151,6 +151,12 @@ int rvm_plan_set_certain_reject(rvm_plan* plan, int32_t on);
  * refuses NaN log-probabilities) rather than treating them as ordinary rejections. */
 int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
                     int64_t* unresolved, int64_t* refined, int64_t* truncated, void* stream);
+/* All of a plan's counters as an array (the same reset): out[0..4] as rvm_plan_faults, out[5]
+ * walker-directions the adaptive resolution settled at their roundoff floor (a halving pass whose
+ * estimate no longer fell: the direction keeps its best pass, whose estimate was within
+ * RVM_FLOOR_BOUND = 4 x the bound); entries past RVM_N_COUNTERS read 0. */
+#define RVM_N_COUNTERS 6
+int rvm_plan_counters(rvm_plan* plan, int32_t reset, int64_t* out, int32_t n, void* stream);
 /* Kernel timing (benchmarks): the plan's next max_launches likelihood evaluations (any entry point)
  * record HIP events on their stream around the likelihood kernel and around the refinement kernel
  * that follows it (0..4096; 0 stops).  rvm_plan_kernel_times waits for those events and returns

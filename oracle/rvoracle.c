@@ -1006,8 +1006,10 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /*   a conservative one of r5's: measured, r5's error stays below 0.43 tol_dir wherever this     */
 /*   holds at EXT_ACCEPT = 1 (2.6 tol_dir at 2, round 3));                          */
 /*  stages 2..: passes with every step halved (level k: mult 2^rf steps per base step, rf = 1..  */
-/*   rf_max) over every direction still open, until est <= tol_dir; still open after rf_max:     */
-/*   RVO_UNRESOLVED.                                                                             */
+/*   rf_max) over every direction still open, until est <= tol_dir, or until the estimate stops   */
+/*   falling (from rf = 2 on, est >= half the previous pass's: the roundoff floor of the finer     */
+/*   steps) with the best pass's est <= FLOOR_BOUND * tol_dir -- the direction then keeps its best */
+/*   pass (the smallest est); still open after rf_max: RVO_UNRESOLVED.                            */
 /* The walker's two directions advance through the stages together (round 4): an encounter in   */
 /* either ends the walker (ENCOUNTER), and the certain-reject test (a sampler's accept inputs    */
 /* given: dmode 1 emcee stretch, 2 MH) runs on the WALKER after the extension stage and after    */
@@ -1029,6 +1031,9 @@ enum { RVO_UNRESOLVED = 4 };
 #endif
 #ifndef CUT_EST_FACTOR
 #define CUT_EST_FACTOR 100.0
+#endif
+#ifndef FLOOR_BOUND
+#define FLOOR_BOUND 4.0
 #endif
 
 
@@ -1064,8 +1069,9 @@ typedef struct {
     int cnt;
     double sign;
     double *lv0, *lv, *prev; /* main pass's levels (+ the extension), a halving pass's, the last RV */
-    int st, open, bad, stage, cut;
+    int st, open, bad, stage, cut, floor;
     double chi2, lb, est, est_raw, margin;
+    double pest, best, bchi; /* the previous halving pass's est, the smallest est and its chi2 */
 } rvo_dir;
 
 static double lb_of(double chi2, double d, double est_raw) {
@@ -1193,9 +1199,24 @@ static void dir_halve(const rvo_plan_ctx* X, rvo_dir* D, int rf) {
     D->est_raw = e2;
     D->est = e2 / X->npoints;
     if (margin_of(D->est, X->tol_dir) < D->margin) D->margin = margin_of(D->est, X->tol_dir);
+    const int fin = isfinite(c2) && isfinite(e2);
+    const int stall = fin && rf >= 2 && !(D->est < 0.5 * D->pest);
+    if (fin && rf >= 2 && D->best <= FLOOR_BOUND * X->tol_dir && D->est > X->tol_dir &&
+        margin_of(D->est, 0.5 * D->pest) < D->margin)
+        D->margin = margin_of(D->est, 0.5 * D->pest); /* (the floor decision, when it could matter) */
+    if (fin && D->est < D->best) {
+        D->best = D->est;
+        D->bchi = c2;
+    }
+    D->pest = fin ? D->est : INFINITY;
     if (!(D->est > X->tol_dir)) {
         D->open = 0;
         D->lb = c2;
+    } else if (stall && D->best <= FLOOR_BOUND * X->tol_dir) { /* the roundoff floor: the best pass */
+        D->open = 0;
+        D->floor = 1;
+        D->chi2 = D->lb = D->bchi;
+        D->est = D->best;
     } else {
         D->lb = lb_of(c2, d2, e2); /* (d2 NaN after a non-finite pass: fmin takes the estimate) */
     }
@@ -1304,6 +1325,7 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
         d->prev = d->lv + (size_t)nl * cnt;
         d->st = RVO_OK;
         d->margin = INFINITY;
+        d->pest = d->best = INFINITY;
     }
     for (int dir = 0; dir < 2; dir++)
         if (D[dir].cnt) dir_main(&X, &D[dir]);

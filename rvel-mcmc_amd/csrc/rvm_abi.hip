@@ -169,7 +169,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
 
     // device layout: per direction [seg_n | obs_idx] int32 and [seg_len | obs_rv | obs_s2] f64, + workspace
     const size_t nf = dir[0].idx.size(), nb = dir[1].idx.size();
-    const size_t n_dbl = 3 * (nf + nb) + (size_t)max_walkers + 5;  // schedule f64 | slots | counters (u64)
+    const size_t n_dbl = 3 * (nf + nb) + (size_t)max_walkers + RVM_N_COUNTERS;  // schedule f64 | slots | counters (u64)
     const size_t n_int = 2 * (nf + nb);
     const size_t bytes = n_dbl * sizeof(double) + n_int * sizeof(int32_t) + 64;
     rvm_plan* plan = new rvm_plan();
@@ -482,27 +482,37 @@ int rvm_plan_extension(const rvm_plan* plan, int32_t* ext_mult) {
     return 0;
 }
 
-int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
-                    int64_t* unresolved, int64_t* refined, int64_t* truncated, void* stream) {
-    if (!plan) return fail(-1, "rvm_plan_faults: null plan");
+int rvm_plan_counters(rvm_plan* plan, int32_t reset, int64_t* out, int32_t n, void* stream) {
+    if (!plan) return fail(-1, "rvm_plan_counters: null plan");
+    if (n < 0 || (n > 0 && !out)) return fail(-1, "rvm_plan_counters: bad output array");
     hipStream_t st = (hipStream_t)stream;
-    unsigned long long h[5] = {0, 0, 0, 0, 0};
+    unsigned long long h[RVM_N_COUNTERS] = {};
     hipError_t e = hipMemcpyAsync(h, plan->dev.counters, sizeof(h), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return hip_fail(e, "rvm_plan_faults");
-    if (handoff_timeouts) *handoff_timeouts = (int64_t)h[0];
-    if (nonfinite) *nonfinite = (int64_t)h[1];
-    if (unresolved) *unresolved = (int64_t)h[2];
-    if (refined) *refined = (int64_t)h[3];
-    if (truncated) *truncated = (int64_t)h[4];
+    if (e != hipSuccess) return hip_fail(e, "rvm_plan_counters");
+    for (int i = 0; i < n; i++) out[i] = i < RVM_N_COUNTERS ? (int64_t)h[i] : 0;
     if (reset) {
         // the hand-off slots back to their sentinels (late level-1 stores of a launch that gave up
         // have landed: the stream's earlier work is complete), then the counters
         if (plan->lvmem) e = hipMemsetAsync(plan->lvmem, 0xFF, plan->lv_bytes, st);
         if (e == hipSuccess) e = hipMemsetAsync(plan->dev.counters, 0, sizeof(h), st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
-        if (e != hipSuccess) return hip_fail(e, "rvm_plan_faults: reset");
+        if (e != hipSuccess) return hip_fail(e, "rvm_plan_counters: reset");
     }
+    return 0;
+}
+
+int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, int64_t* nonfinite,
+                    int64_t* unresolved, int64_t* refined, int64_t* truncated, void* stream) {
+    if (!plan) return fail(-1, "rvm_plan_faults: null plan");
+    int64_t c[RVM_N_COUNTERS] = {};
+    const int rc = rvm_plan_counters(plan, reset, c, RVM_N_COUNTERS, stream);
+    if (rc != 0) return rc;
+    if (handoff_timeouts) *handoff_timeouts = c[0];
+    if (nonfinite) *nonfinite = c[1];
+    if (unresolved) *unresolved = c[2];
+    if (refined) *refined = c[3];
+    if (truncated) *truncated = c[4];
     return 0;
 }
 

@@ -23,6 +23,12 @@ constexpr double RVM_EXT_ACCEPT = 1.0;
 // (rvm_logl.hip refine_loop; oracle/rvoracle.c CUT_EST_FACTOR; measured error / estimate <= 57 on
 // the main pass at the plan's step, smaller after a halving)
 constexpr double RVM_CUT_EST_FACTOR = 100.0;
+// the roundoff floor of a halving pass (rvm_refine.hip; oracle/rvoracle.c FLOOR_BOUND): a direction
+// whose estimate stopped falling settles at its best pass when that pass's estimate is within this
+// x tol_dir (round 4: a crossing-orbit walker of the wide ball reached its floor at ~1e-7..2e-6 in
+// logL from the 5th halving on -- the finer steps' accumulated rounding -- and ended UNRESOLVED on
+// the GPU where the oracle's rounding happened to settle it)
+constexpr double RVM_FLOOR_BOUND = 4.0;
 // launches of fewer walkers than this run the extension after the main pass (only when a walker is
 // flagged) instead of as a concurrent fifth wave of the one-group-per-block layout (launch_logl_t)
 constexpr int RVM_CX_MIN_WALKERS = 32;
@@ -92,7 +98,7 @@ struct DevPlan {
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
     // [3] walker-direction refinement passes (extension + halvings), [4] refinements cut short as
-    // certain rejects
+    // certain rejects, [5] directions settled at their roundoff floor (RVM_FLOOR_BOUND)
     unsigned long long* counters;
     unsigned long long spin_ticks;  // hand-off waits give up after this long without progress (100 MHz)
     double npoints;

@@ -11,6 +11,10 @@
 // the passes together (rf = 1, 2, ... rmax, every open direction each time) and after every pass
 //   * an encounter in either direction ends the walker (ENCOUNTER);
 //   * a direction whose estimate is within the bound settles (chi2 of that pass);
+//   * a direction whose estimate stopped falling (a pass from rf = 2 on at least half the previous
+//     pass's: the roundoff floor of the finer steps, not the asymptotic h^8 fall) settles at its
+//     best pass so far (the smallest estimate) when that is within RVM_FLOOR_BOUND x the bound --
+//     counted (counters[5]); else it refines on;
 //   * the certain-reject test (fused sampler launches): with each direction's lower bound on its
 //     chi2 (a settled one's chi2; an open one's chi2 less min(the step-doubling change of the pass,
 //     RVM_CUT_EST_FACTOR x its estimate)) the walker stops when its accept test fails even at
@@ -88,6 +92,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     __shared__ int s_enc[2][RVM_MAX_LEVELS][64];
     __shared__ double s_init[8][64];
     __shared__ double s_chi[2][64], s_lb[2][64];
+    __shared__ double s_pest[2][64], s_best[2][64], s_bchi[2][64];  // previous / best estimate, best chi2
     __shared__ int s_open[2][64];  // 1 open, 0 settled, 2 encounter
     __shared__ int s_live[64];     // the walker is still refining
     __shared__ int s_stw[64];      // its final status and logl (finished after the passes)
@@ -161,6 +166,11 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 s_chi[1][lane] = ob ? 0.0 : P.rq_c[(size_t)P.rq_cap + wl];
                 s_lb[0][lane] = s_chi[0][lane];
                 s_lb[1][lane] = s_chi[1][lane];
+                for (int d2i = 0; d2i < 2; d2i++) {
+                    s_pest[d2i][lane] = INFINITY;
+                    s_best[d2i][lane] = INFINITY;
+                    s_bchi[d2i][lane] = 0.0;
+                }
                 s_live[lane] = v ? 1 : 0;
                 s_stw[lane] = RVM_STATUS_NONFINITE;  // (every pass loop ends with a decision)
                 s_lpw[lane] = -INFINITY;
@@ -278,12 +288,26 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                         int er = 0;
                         for (int q = 0; q < nl; q++) er |= s_enc[dd_u][q][lane];
                         const bool fin = isfinite(c2) && isfinite(e2);
+                        const double en = e2 / P.npoints;
+                        // (the roundoff floor: this pass's estimate no longer falls; the best pass's
+                        // estimate is e2 / npoints units too)
+                        const bool stall = fin && rf >= 2 && !(en < 0.5 * s_pest[dd_u][lane]);
+                        if (fin && en < s_best[dd_u][lane]) {
+                            s_best[dd_u][lane] = en;
+                            s_bchi[dd_u][lane] = c2;
+                        }
+                        s_pest[dd_u][lane] = fin ? en : INFINITY;
                         if (er) {
                             s_open[dd_u][lane] = 2;
-                        } else if (fin && !(e2 / P.npoints > P.rtol_dir)) {
+                        } else if (fin && !(en > P.rtol_dir)) {
                             s_open[dd_u][lane] = 0;
                             s_chi[dd_u][lane] = c2;
                             s_lb[dd_u][lane] = c2;
+                        } else if (stall && s_best[dd_u][lane] <= RVM_FLOOR_BOUND * P.rtol_dir) {
+                            s_open[dd_u][lane] = 0;
+                            s_chi[dd_u][lane] = s_bchi[dd_u][lane];
+                            s_lb[dd_u][lane] = s_bchi[dd_u][lane];
+                            __hip_atomic_fetch_add(P.counters + 5, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         } else {
                             s_chi[dd_u][lane] = fin ? c2 : __builtin_nan("");
                             s_lb[dd_u][lane] = fin ? open_lb(c2, d2, e2) : 0.0;

@@ -18,6 +18,7 @@ RVM_STATUS_NONFINITE = 3
 RVM_STATUS_UNRESOLVED = 4
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
+RVM_N_COUNTERS = 6  # rvm_plan_counters
 ABI_VERSION = 11  # include/rvmcmc.h RVM_ABI_VERSION
 
 
@@ -88,6 +89,7 @@ SIGNATURES = {
     "rvm_plan_extension": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "rvm_plan_set_verify_eccentricity": (C.c_int, [C.c_void_p, C.c_double]),
     "rvm_plan_set_certain_reject": (C.c_int, [C.c_void_p, C.c_int32]),
+    "rvm_plan_counters": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_int64), C.c_int32, C.c_void_p]),
     "rvm_plan_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                 C.POINTER(C.c_int32)]),
     "rvm_logl_batch": (C.c_int, [C.c_void_p, C.c_int32, _dp, C.c_double, _dp, _dp, _dp, _dp]),

@@ -207,14 +207,15 @@ class LoglPlan:
             _lib.check(self.lib.rvm_plan_set_certain_reject(self._h, 0), "rvm_plan_set_certain_reject")
 
     def faults(self, reset=False, stream=None) -> dict:
-        """rvm_plan_faults: the plan's counters (synchronises the stream): hand-off timeouts, NONFINITE
-        and UNRESOLVED results, refinement passes, refinements cut short on a certain reject;
-        reset=True zeroes them and restores the hand-off workspace."""
-        vals = [C.c_int64() for _ in range(5)]
-        _lib.check(self.lib.rvm_plan_faults(self._h, int(bool(reset)), *[C.byref(v) for v in vals],
-                                            _lib.stream_handle(stream)), "rvm_plan_faults")
-        return dict(handoff_timeouts=vals[0].value, nonfinite=vals[1].value, unresolved=vals[2].value,
-                    refined=vals[3].value, truncated=vals[4].value)
+        """rvm_plan_counters: the plan's counters (synchronises the stream): hand-off timeouts, NONFINITE
+        and UNRESOLVED results, refinement passes, refinements cut short on a certain reject,
+        directions settled at their roundoff floor; reset=True zeroes them and restores the hand-off
+        workspace."""
+        vals = (C.c_int64 * _lib.RVM_N_COUNTERS)()
+        _lib.check(self.lib.rvm_plan_counters(self._h, int(bool(reset)), vals, _lib.RVM_N_COUNTERS,
+                                              _lib.stream_handle(stream)), "rvm_plan_counters")
+        return dict(handoff_timeouts=vals[0], nonfinite=vals[1], unresolved=vals[2], refined=vals[3],
+                    truncated=vals[4], floor_settled=vals[5])
 
     def check_faults(self, what="plan", stream=None, group=None) -> dict:
         """Raise RvmError on hand-off timeouts, NONFINITE results, or (a plan that refines, resolve_max

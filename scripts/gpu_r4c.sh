@@ -8,9 +8,13 @@ R=$PWD
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 T=${T:-r04g}
-timeout -k 10 700 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_gpu_resolve.py \
-    tests/test_gpu_ias15_decisions.py > gpurun_out/${T}_pytest_dec.log 2>&1 || { grep -E "PASS|FAIL|ERROR" gpurun_out/${T}_pytest_dec.log | tail -40; tail -60 gpurun_out/${T}_pytest_dec.log; exit 1; }
+# (pytest exit 1 = test failures: reported, the chain goes on; anything else stops it)
+rc=0
+timeout -k 10 700 python -u -m pytest -v --timeout 300 --timeout-method thread ${TESTS:-tests/test_gpu_resolve.py \
+    tests/test_gpu_ias15_decisions.py} > gpurun_out/${T}_pytest_dec.log 2>&1 || rc=$?
+grep -E "FAIL|ERROR" gpurun_out/${T}_pytest_dec.log | tail -20 || true
 tail -3 gpurun_out/${T}_pytest_dec.log
+[ $rc -le 1 ] || exit $rc
 timeout -k 10 200 python -u scripts/probe/steady_bench.py > gpurun_out/${T}_steady.jsonl 2>&1 || { cat gpurun_out/${T}_steady.jsonl; exit 1; }
 cat gpurun_out/${T}_steady.jsonl
 mkdir -p gpurun_out/${T}_prof_steady

@@ -76,6 +76,7 @@ def test_argument_errors_do_not_touch_the_device():
     assert lib.rvm_plan_extension(None, None) < 0
     assert lib.rvm_plan_set_verify_eccentricity(None, 0.3) < 0
     assert lib.rvm_plan_set_certain_reject(None, 0) < 0
+    assert lib.rvm_plan_counters(None, 0, None, 0, None) < 0
     # workspace: per (chain, pair i >= j) and direction, 4 f64 partial sums and an int32 status
     assert lib.rvm_logl_derivs_workspace_bytes(256, 10) == 256 * 55 * 2 * (4 * 8 + 4)
 

@@ -15,6 +15,8 @@ rejections and encounters, HD155358 (real data, `sol` of (Ex)HD155358.ipynb:64-6
 (mcmc.py:167-187; likelihood terms from IAS15, proposal-density terms from the device metric,
 which test_gpu_derivs.py pins against IAS15 differences).
 """
+import json
+
 import numpy as np
 import pytest
 
@@ -125,6 +127,11 @@ def stretch_parity(name, planets, obs, W, ball, iterations=2, warm=4, roundoff=F
             cur = np.isneginf(lnp_dev[h]) != np.isneginf(lnp_ref[h])  # (e.g. UNRESOLVED vs OK)
             tally.add(acc_dev, acc_ref, margin, sq_dev, sq_ref, lq_dev, lq_ref, idx_offset=h * hk, roundoff=sens,
                       current_differs=cur)
+            # (the proposals left UNRESOLVED, for the failure message: oracle replay in
+            # scripts/probe/replay_parity.py)
+            tally.unresolved_rows = getattr(tally, "unresolved_rows", []) + q[sq_dev == IP.ST_UNRESOLVED].tolist()
+            if np.any(sq_dev == IP.ST_UNRESOLVED):
+                print("unresolved proposals:", json.dumps(q[sq_dev == IP.ST_UNRESOLVED].tolist()))
             lnp_ref[h] = np.where(acc_dev, lq_ref, lnp_ref[h])  # follow the device chain
     return tally, dict(walkers=W, ball=ball, iterations=iterations, warm_iterations=warm, speculative=bool(spec))
 
@@ -154,7 +161,8 @@ def test_stretch_vs_ias15_wide_ball_encounters():
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
     # no proposal is left UNRESOLVED (a forced reject the reference never makes): device status 4 is
     # never exempt, and none occurs
-    assert rep["unresolved_device"] == 0 and not any(k.startswith("4/") for k in rep["status_pairs_device/ias15"])
+    assert rep["unresolved_device"] == 0 and not any(k.startswith("4/") for k in rep["status_pairs_device/ias15"]), \
+        tally.unresolved_rows
     assert rep["encounters_ias15"] > 20 and rep["prior_rejections"] > 20
     assert rep["exempt_status_disagreement"] <= max(4, rep["decisions"] // 100)
     assert rep["exempt_current_status_disagreement"] <= max(4, rep["decisions"] // 100)
@@ -179,7 +187,7 @@ def test_stretch_vs_ias15_steady_state():
     rep = tally.report(**info)
     assert info["speculative"]
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
-    assert rep["unresolved_device"] == 0
+    assert rep["unresolved_device"] == 0, tally.unresolved_rows
     assert rep["ok_proposals_dlogl_above_margin_not_roundoff"] == 0
     assert rep["max_abs_dlogl_ok_proposals_not_roundoff"] <= T2_ABS
     assert rep["exempt_status_disagreement"] <= max(4, rep["decisions"] // 500)
@@ -223,7 +231,7 @@ def test_stretch_vs_ias15_steady_state_other_systems(case):
                                  warm=0, roundoff=True, X0=X0)
     rep = tally.report(**info)
     assert rep["mismatches_not_exempt"] == 0, tally.mismatch[:20]
-    assert rep["unresolved_device"] == 0
+    assert rep["unresolved_device"] == 0, tally.unresolved_rows
     assert rep["ok_proposals_dlogl_above_margin_not_roundoff"] == 0
     assert rep["max_abs_dlogl_ok_proposals_not_roundoff"] <= T2_ABS
 
