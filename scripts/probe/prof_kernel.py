@@ -20,7 +20,9 @@ SLOTS, MAXW = 18, 4096
 
 
 def main():
-    W = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+    slots = os.environ.get("SLOTS")  # (e.g. scripts/probe/slots_it2000.npz: a steady-state launch's slots)
+    KS = np.load(slots)["K"] if slots else None
+    W = int(sys.argv[1]) if len(sys.argv) > 1 else (len(KS) if KS is not None else 2048)
     assert W <= 8192
     _lib.LIB_PATH = os.path.join(ROOT, "scripts", "probe", "librvmcmc_prof.so")
     lib = _lib.load()
@@ -29,11 +31,14 @@ def main():
     cfg = engine.IntegratorConfig()
     dt, mult, hint = cfg.plan_args(S2_PLANETS)
     t, rv, er = engine.obs_arrays(obs)
-    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint)
+    res = cfg.resolve(S2_PLANETS) if os.environ.get("RESOLVE", "0") == "1" else (0.0, 0)
+    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 2, dt, mult, W, period_hint=hint, resolve=res)
     rng = np.random.default_rng(0)
     P = np.repeat(O.pal_params(S2_PLANETS)[None], W, 0)
     P[:, :, :5] *= 1 + float(os.environ.get("BALL", "1e-3")) * rng.standard_normal((W, 2, 5))
     K = torch.as_tensor(np.concatenate([P[:, p, :5].T for p in range(2)], 0).copy(), device="cuda")
+    if KS is not None:
+        K = torch.as_tensor(np.ascontiguousarray(KS[:W].T), device="cuda")
     for _ in range(3):
         plan.logl(K)
     torch.cuda.synchronize()
