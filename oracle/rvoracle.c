@@ -1072,6 +1072,7 @@ typedef struct {
     int st, open, bad, stage, cut, floor;
     double chi2, lb, est, est_raw, margin;
     double pest, best, bchi; /* the previous halving pass's est, the smallest est and its chi2 */
+    double dext;             /* the extension's change dd / npoints (0: none) */
 } rvo_dir;
 
 static double lb_of(double chi2, double d, double est_raw) {
@@ -1156,6 +1157,7 @@ static void dir_extend(const rvo_plan_ctx* X, rvo_dir* D) {
     const double bx = EXT_ACCEPT * X->tol_dir * X->npoints;
     if (margin_of(dd, bx) < D->margin) D->margin = margin_of(dd, bx);
     D->chi2 = c5;
+    D->dext = dd / X->npoints;
     if (dd <= bx) {
         D->est = dd / X->npoints;
         D->open = 0;
@@ -1287,6 +1289,9 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
         rvo_richardson_weights_seq(nl + 1, m5, X.w5);
     }
     int* idx = (int*)malloc(sizeof(int) * (size_t)(n + 1));
+#ifdef JUMP_T
+    int jumped = 0;
+#endif
     rvo_dir D[2];
     memset(D, 0, sizeof D);
     double* buf[2];
@@ -1335,6 +1340,12 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
     }
     if (!any_enc(D) && X.adaptive) {
         int rf = 0;
+#ifdef JUMP_T /* (study build: a walker whose extension changed an open direction by more than
+                 JUMP_T x tol_dir starts its halving passes at rf = 2) */
+        for (int dir = 0; dir < 2; dir++)
+            if (D[dir].open && D[dir].dext > JUMP_T * X.tol_dir) rf = 1;
+        jumped = rf;
+#endif
         while (any_open(D) && !walker_cut(&X, D, dc)) {
             if (rf == rf_max) {
                 for (int dir = 0; dir < 2; dir++)
@@ -1349,6 +1360,9 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
     }
     for (int dir = 0; dir < 2; dir++) {
         cut[dir] = D[dir].cut;
+#ifdef JUMP_T
+        if (jumped) cut[dir] |= 2; /* (study build: the walker started at rf = 2) */
+#endif
         rf_used[dir] = D[dir].stage;
         est[dir] = D[dir].est;
         est[2 + dir] = D[dir].margin;

@@ -585,6 +585,20 @@ __device__ __forceinline__ void drift_fail_count(int nt, bool zok, bool hok) {
 //   the others; the caller (segment<> in rvm_logl.hip) re-runs the whole segment gated when any
 //   lane was not good.  Good lanes compute bit-identical states either way.
 // No square root anywhere in the step.
+// Whether the lane's walker has already seen a pair inside the exit distance (Lane::encm; the
+// walker's bits relative to its first lane as kick_enc_bits): its result is ENCOUNTER whatever it
+// integrates next -- the reference stops there (exit_min_distance raises, state.py:36-47) -- so its
+// drifts no longer send the wave to the second Halley step or the general solver (an encountered
+// crossing orbit took them at every pericentre to the end of the span: the steady state's slowest
+// waves).  Only that lane's own, discarded values change.
+template <int NP>
+__device__ __forceinline__ bool lane_encountered(const Lane<NP>& s) {
+    constexpr int L = LanesPerWalker<NP>::value;
+    constexpr uint64_t bits = NP == 2 ? 3ull : (NP == 3 ? 0xFull : 1ull);  // kick_enc_bits
+    const int base = (int)(threadIdx.x & 63) & ~(L - 1);
+    return ((s.encm >> base) & bits) != 0;
+}
+
 template <int NT, bool GATED, bool D3 = false, int NP>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const VConsts& vk) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;
@@ -611,7 +625,7 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
     // converged all the same; only kepler_rare treats such steps separately (bracketed solver).
     if constexpr (GATED) {
         constexpr double B8 = stumpff_bound<8>();
-        const bool ok1 = fabs(z) <= B && halley_ok<NT>(Q, x);
+        const bool ok1 = (fabs(z) <= B && halley_ok<NT>(Q, x)) || lane_encountered(s);
         if (ballot(!ok1) != 0) {
 #ifdef RVM_PROFILE_FAILS
             rare_count(0, 0);
@@ -643,7 +657,7 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
             }
         }
     } else {
-        bad = bad || !(fabs(z) <= B) || !halley_ok<NT>(Q, x);
+        bad = bad || ((!(fabs(z) <= B) || !halley_ok<NT>(Q, x)) && !lane_encountered(s));
     }
     const DriftOut o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     s.rx = o.rx;
