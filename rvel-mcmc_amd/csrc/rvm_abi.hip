@@ -362,6 +362,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.inv_ext = 1.0;
     P.lvx = nullptr;
     P.rvp = nullptr;
+    P.rvp2 = nullptr;
     P.e2_guard = INFINITY;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
@@ -371,7 +372,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const int nl = cfg->n_levels;
         const size_t emax = std::max<size_t>(std::max(nf, nb), 1);
         const size_t bl = 2 * emax * (size_t)max_walkers * sizeof(double);  // partial sums
-        const size_t bx = 2 * bl;                                           // + last RV
+        const size_t bx = 3 * bl;                                           // + last RV (x2 teams)
         // (a failed allocation is not an error: the plan refines by halving passes alone, ext_mult 0)
         if (bx <= RVM_EXT_MAX_BYTES && hipMalloc(&plan->xmem, bx) != hipSuccess) {
             plan->xmem = nullptr;
@@ -410,6 +411,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             P.inv_mult[nl] = P.inv_ext;
             P.lvx = reinterpret_cast<double*>(plan->xmem);
             P.rvp = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(plan->xmem) + bl);
+            P.rvp2 = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(plan->xmem) + 2 * bl);
             P.lvx_emax = (int32_t)emax;
             P.lvx_stride = max_walkers;
         }
@@ -423,15 +425,19 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.rq_x = nullptr;
     P.rq_xf = nullptr;
     P.rq_xgroups = 0;
+    P.rq_t = nullptr;
+    P.rq_tf = nullptr;
     if (P.rmax > 0) {
         // (+ the split exchange: flags and double-buffered values per both-direction group of up to 64
-        // walkers; groups of 16 walkers at 3-4 planets)
+        // walkers and team; groups of 16 walkers at 3-4 planets; + team A's published state and flag)
         const int64_t xg = ((int64_t)max_walkers + 15) / 16 + 1;
-        const size_t b_x = (size_t)xg * 2 * 2 * 64 * sizeof(unsigned long long);
-        const size_t b_xf = (size_t)xg * 2 * sizeof(unsigned long long);
+        const size_t b_x = (size_t)xg * 2 * 2 * 2 * 64 * sizeof(unsigned long long);
+        const size_t b_xf = (size_t)xg * 2 * 2 * sizeof(unsigned long long);
+        const size_t b_t = (size_t)xg * 16 * 64 * sizeof(unsigned long long);
+        const size_t b_tf = (size_t)xg * sizeof(unsigned long long);
         const size_t b_c = 2 * (size_t)max_walkers * sizeof(double);
         const size_t b_w = 3 * (size_t)max_walkers * sizeof(int32_t);
-        const size_t b_all = b_x + b_xf + b_c + b_w + 64;
+        const size_t b_all = b_x + b_xf + b_t + b_tf + b_c + b_w + 64;
         if (hipMalloc(&plan->rqmem, b_all) != hipSuccess || hipMemset(plan->rqmem, 0, b_all) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
@@ -441,13 +447,17 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         unsigned char* base = reinterpret_cast<unsigned char*>(plan->rqmem);
         P.rq_x = reinterpret_cast<unsigned long long*>(base);
         P.rq_xf = reinterpret_cast<unsigned long long*>(base + b_x);
-        P.rq_c = reinterpret_cast<double*>(base + b_x + b_xf);
-        P.rq_w = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_c);
-        P.rq_n = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_c + b_w);
+        P.rq_t = reinterpret_cast<unsigned long long*>(base + b_x + b_xf);
+        P.rq_tf = reinterpret_cast<unsigned long long*>(base + b_x + b_xf + b_t);
+        P.rq_c = reinterpret_cast<double*>(base + b_x + b_xf + b_t + b_tf);
+        P.rq_w = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c);
+        P.rq_n = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w);
         P.rq_cap = max_walkers;
         P.rq_xgroups = (int32_t)xg;
         if (const char* sp = getenv("RVM_REFINE_SPLIT"))  // (A/B knob: 0 keeps both directions in one block)
             if (sp[0] == '0') P.rq_x = nullptr;
+        if (const char* tp = getenv("RVM_REFINE_TEAMS"))  // (A/B knob: 0 runs the passes one after the other)
+            if (tp[0] == '0') P.rq_t = nullptr;
     }
     *out = plan;
     return 0;

@@ -95,6 +95,13 @@ struct DevPlan {
     unsigned long long* rq_x;
     unsigned long long* rq_xf;
     int32_t rq_xgroups;
+    // (both [groups][2 teams] since round 4: team A runs pass 1, team B pass 2 at the same time, then
+    // the rest, rvm_refine.hip) team A's walker state after pass 1 for team B, rq_t [groups][16][64],
+    // and its flag rq_tf [groups] (launch generation << 8 | 1, or 2 when the group is done)
+    unsigned long long* rq_t;
+    unsigned long long* rq_tf;
+    // team B's own RV per pass (as rvp)
+    double* rvp2;
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
     // [3] walker-direction refinement passes (extension + halvings), [4] refinements cut short as

@@ -34,6 +34,17 @@
 // Each wave re-derives its lanes' state at t = 0 from the walker's parameters (rvm_walker.h, the
 // same bits as the likelihood kernel's prologue) and finishes the walker as it would have
 // (rvm_walker.h walker_out: logl, status, counters, the fused accept).
+//
+// Two teams (round 4).  At the steady state about one walker slot in a launch needs a second
+// halving pass, and that launch then waited pass 1 (14 steps per base step on the longest level)
+// and pass 2 (28) one after the other.  When every task fits the grid, each group has team A,
+// which runs pass 1, and team B on other CUs, which runs pass 2 at the same time, before pass 1's
+// outcome is known.  A decides after pass 1 and publishes its walkers' state (write-through
+// granules and a flag tagged with the launch generation).  If every walker of the group is done,
+// A finishes them and B, which polls the flag at every epoch, stops.  Otherwise B, at the end of its
+// pass, takes A's state and applies pass 2's results to the walkers still open: their step-doubling
+// change is against pass 1's RV, which A stored write-through.  It then goes on alone, rf = 3, ...,
+// and finishes the group.  Decisions and values are the sequential passes' bit for bit.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -81,7 +92,13 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     const int ntask_split = 2 * gq0 + gq1 + gq2;
     const bool split = P.rq_x != nullptr && gq0 <= P.rq_xgroups && ((int)gridDim.x & 1) == 0 &&
                        ntask_split <= (int)gridDim.x;
-    const int ntask = split ? ntask_split : ng;
+    // teams: A (pass 1) and B (pass 2 concurrently, then the rest) per group -- when the split
+    // layout holds, every team task fits the grid, and no RV curve is wanted (both teams would
+    // write it)
+    const int ntask_team = 4 * gq0 + 2 * (gq1 + gq2);
+    const bool team = split && P.rq_t != nullptr && P.rvp != nullptr && P.rvp2 != nullptr && P.rmax >= 2 &&
+                      rv_out == nullptr && ng <= P.rq_xgroups && ntask_team <= (int)gridDim.x;
+    const int ntask = team ? ntask_team : (split ? ntask_split : ng);
     if ((int)blockIdx.x >= ntask) return;
 
     // LDS: both directions' schedules ([d][seg_h1 | obs_rv | obs_s2 | (seg_n, obs_idx)], E_d each),
@@ -101,6 +118,11 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     __shared__ int s_dmode[64];
     __shared__ unsigned long long s_mask[2];
     __shared__ int s_xfault;  // a split task's exchange gave up (its walkers end NONFINITE)
+    // team B's first pass: its results per direction and walker slot (chi2, estimate, encounter),
+    // applied once team A's state after pass 1 is in; the cancel poll, by epoch parity
+    __shared__ double s_tc2[2][64], s_te2[2][64];
+    __shared__ int s_ter[2][64];
+    __shared__ int s_cancel[2];
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     for (int dd = 0; dd < 2; dd++) {
         const DirSched& SD = dd ? P.bwd : P.fwd;
@@ -121,8 +143,18 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
 
     for (int t = blockIdx.x; t < ntask; t += gridDim.x) {
         // the task's group, and (split both-direction group) the direction this workgroup integrates
-        int g = t, own = -1;
-        if (split) {
+        int g = t, own = -1, tm = 0;  // tm: the task's team (0 = A, 1 = B; always A without teams)
+        if (team) {
+            if (t < 4 * gq0) {
+                g = t >> 2;
+                own = t & 1;
+                tm = (t >> 1) & 1;
+            } else {
+                const int u = t - 4 * gq0;
+                g = gq0 + (u >> 1);
+                tm = u & 1;
+            }
+        } else if (split) {
             if (t < 2 * gq0) {
                 g = t >> 1;
                 own = t & 1;
@@ -181,6 +213,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 s_mask[0] = m0;
                 s_mask[1] = m1;
                 s_xfault = 0;
+                s_cancel[0] = s_cancel[1] = 0;
             }
         }
         // the decision lanes' accept inputs (wave 0, lane = walker slot), kept in LDS through the passes
@@ -196,7 +229,46 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         }
         __syncthreads();
 
-        for (int rf = 1; rf <= P.rmax; rf++) {
+        // team A publishes after pass 1 at rq_t[g] (16 rows of 64 values: live, status, logl, then per
+        // direction open, chi2, lb, previous / best estimate, best chi2), its flag at rq_tf[g] =
+        // (launch generation << 8) | 1 (walkers left for B) or 2 (all done: B stops)
+        gu64* tpub = team ? (gu64*)(P.rq_t + (size_t)g * 16 * 64) : nullptr;
+        gu64* tflag = team ? (gu64*)(P.rq_tf + g) : nullptr;
+        bool cancelled = false;  // (team B: A finished the group)
+        // a pass's outcome for direction dd of walker slot `lane` (its combiner lane): encounter,
+        // settled (estimate within the bound), settled at the roundoff floor, or still open with the
+        // pass's lower bound on its chi2
+        auto pass_result = [&](const int dd, const int rfp, const double c2, const double e2, const double d2,
+                               const int er) __attribute__((always_inline)) {
+            const bool fin = isfinite(c2) && isfinite(e2);
+            const double en = e2 / P.npoints;
+            // (the roundoff floor: this pass's estimate no longer falls; the best pass's estimate is
+            // e2 / npoints units too)
+            const bool stall = fin && rfp >= 2 && !(en < 0.5 * s_pest[dd][lane]);
+            if (fin && en < s_best[dd][lane]) {
+                s_best[dd][lane] = en;
+                s_bchi[dd][lane] = c2;
+            }
+            s_pest[dd][lane] = fin ? en : INFINITY;
+            if (er) {
+                s_open[dd][lane] = 2;
+            } else if (fin && !(en > P.rtol_dir)) {
+                s_open[dd][lane] = 0;
+                s_chi[dd][lane] = c2;
+                s_lb[dd][lane] = c2;
+            } else if (stall && s_best[dd][lane] <= RVM_FLOOR_BOUND * P.rtol_dir) {
+                s_open[dd][lane] = 0;
+                s_chi[dd][lane] = s_bchi[dd][lane];
+                s_lb[dd][lane] = s_bchi[dd][lane];
+                __hip_atomic_fetch_add(P.counters + 5, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                s_chi[dd][lane] = fin ? c2 : __builtin_nan("");
+                s_lb[dd][lane] = fin ? open_lb(c2, d2, e2) : 0.0;
+            }
+        };
+        bool finisher = !team && own <= 0;  // the workgroup that finishes the walkers
+        for (int rf = 1 + tm; rf <= P.rmax; rf++) {
+            const bool bfirst = tm == 1 && rf == 2;  // team B's pass concurrent with A's
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
             const int amw = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);  // directions a live walker still needs
             if (amw == 0) break;
@@ -255,17 +327,29 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 const bool cmb = work && k == 0 && lane < WPB && ((need >> lane) & 1);
                 const bool hasp = P.rvp != nullptr;
                 double c2 = 0.0, e2 = 0.0, d2 = hasp ? 0.0 : INFINITY;  // (the combiner lanes)
-                double* pp = hasp ? P.rvp + (size_t)dd_u * P.lvx_emax * P.lvx_stride + (cmb ? wme : 0) : nullptr;
+                // the previous pass's RV, replaced by this pass's: P.rvp (team B: P.rvp2, its own;
+                // its first pass only writes it -- pass 1's RV is still being written by team A)
+                double* pbuf = tm ? P.rvp2 : P.rvp;
+                double* pp = hasp ? pbuf + (size_t)dd_u * P.lvx_emax * P.lvx_stride + (cmb ? wme : 0) : nullptr;
                 for (int e = 0; e < eb; e++) {
                     const bool here = e < Er;
-                    const double pv = cmb && here && hasp ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued early)
+                    const double pv = cmb && here && hasp && !bfirst ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued early)
                     const int ns = __builtin_amdgcn_readfirstlane(work && here ? r_n[e] * m_r : 0);
                     if (ns > 0) segment_gated<D3, NP, L>(s, kq, r_len[e] * sc, ns, nt_r);
                     if (work && here) {  // (star_vx gathers over the walker's lanes by DPP: outside the lane branch)
                         const double v0 = star_vx<NP, L>(s);
                         if (pl_idx == 0) s_rv[dd_u][e & 1][k_u][slot] = v0;
                     }
+                    // team B polls A's flag (one load per epoch; the result by epoch parity, read by
+                    // every wave after the barrier and rewritten only two barriers later)
+                    if (bfirst && wv == 0 && lane == 0)
+                        s_cancel[e & 1] = __hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                          ((gen << 8) | 2ull);
                     __syncthreads();
+                    if (bfirst && s_cancel[e & 1]) {
+                        cancelled = true;
+                        break;
+                    }
                     if (cmb && here) {
                         double rvx = 0.0, rv3 = 0.0;
                         for (int q = 0; q < nl; q++) rvx += P.lw[q] * s_rv[dd_u][e & 1][q][lane];
@@ -275,50 +359,122 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                         e2 += fabs((rvx - rv3) * (r + (rv3 - r_rv[e]))) / r_s2[e];
                         if (hasp) {
                             d2 += fabs((rvx - pv) * (r + (pv - r_rv[e]))) / r_s2[e];
-                            pp[(size_t)e * P.lvx_stride] = rvx;
+                            if (team && tm == 0)  // (write-through: team B reads pass 1's RV)
+                                __hip_atomic_store((gu64*)(pp + (size_t)e * P.lvx_stride),
+                                                   (unsigned long long)__double_as_longlong(rvx), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+                            else
+                                pp[(size_t)e * P.lvx_stride] = rvx;
                         }
                         if (rv_out != nullptr) rv_out[(size_t)r_idx[e] * W + wme] = rvx;
                     }
                 }
+                if (cancelled) break;
                 if (work && pl_idx == 0) s_enc[dd_u][k_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
                 __syncthreads();
+                if (bfirst) {
+                    // team B: this pass's results aside until team A's state is in
+                    if (work && k == 0 && lane < WPB) {
+                        int er = 0;
+                        for (int q = 0; q < nl; q++) er |= s_enc[dd_u][q][lane];
+                        s_tc2[dd_u][lane] = c2;
+                        s_te2[dd_u][lane] = e2;
+                        s_ter[dd_u][lane] = er;
+                    }
+                    continue;
+                }
                 // the direction's combiner lanes: settle, open (with the pass's lower bound) or encounter
                 if (work && k == 0 && lane < WPB) {
                     if ((need >> lane) & 1) {
                         int er = 0;
                         for (int q = 0; q < nl; q++) er |= s_enc[dd_u][q][lane];
-                        const bool fin = isfinite(c2) && isfinite(e2);
-                        const double en = e2 / P.npoints;
-                        // (the roundoff floor: this pass's estimate no longer falls; the best pass's
-                        // estimate is e2 / npoints units too)
-                        const bool stall = fin && rf >= 2 && !(en < 0.5 * s_pest[dd_u][lane]);
-                        if (fin && en < s_best[dd_u][lane]) {
-                            s_best[dd_u][lane] = en;
-                            s_bchi[dd_u][lane] = c2;
-                        }
-                        s_pest[dd_u][lane] = fin ? en : INFINITY;
-                        if (er) {
-                            s_open[dd_u][lane] = 2;
-                        } else if (fin && !(en > P.rtol_dir)) {
-                            s_open[dd_u][lane] = 0;
-                            s_chi[dd_u][lane] = c2;
-                            s_lb[dd_u][lane] = c2;
-                        } else if (stall && s_best[dd_u][lane] <= RVM_FLOOR_BOUND * P.rtol_dir) {
-                            s_open[dd_u][lane] = 0;
-                            s_chi[dd_u][lane] = s_bchi[dd_u][lane];
-                            s_lb[dd_u][lane] = s_bchi[dd_u][lane];
-                            __hip_atomic_fetch_add(P.counters + 5, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        } else {
-                            s_chi[dd_u][lane] = fin ? c2 : __builtin_nan("");
-                            s_lb[dd_u][lane] = fin ? open_lb(c2, d2, e2) : 0.0;
-                        }
+                        pass_result(dd_u, rf, c2, e2, d2, er);
                     }
                     if (lane == 0 && need)
                         __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(need),
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
+            if (cancelled) break;  // (team B: team A finished the group; every wave saw the same flag)
             __syncthreads();
+            if (bfirst) {
+                // team B: team A's state after pass 1 (wave 0; the flag is in by now unless A is
+                // late), then this pass's results for the walkers still open
+                if (wv == 0) {
+                    SpinClock clk;
+                    clk.restart();
+                    unsigned long long f = 0;
+                    bool ok = true;
+                    while (((f = __hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 8) != gen) {
+                        if (clk.expired(P.spin_ticks)) {
+                            ok = false;
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                    ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
+                    f = __builtin_amdgcn_readfirstlane(f);
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    if (!ok) {
+                        if (lane == 0) {
+                            s_xfault = 1;
+                            __hip_atomic_fetch_add(P.counters, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    } else if ((f & 0xFF) == 2) {
+                        if (lane == 0) s_cancel[0] = 1;  // (A finished the group after all)
+                    } else if (lane < WPB) {
+                        auto ld = [&](int row) {
+                            return __hip_atomic_load(tpub + row * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        };
+                        s_live[lane] = (int)ld(0);
+                        s_stw[lane] = (int)ld(1);
+                        s_lpw[lane] = __longlong_as_double((long long)ld(2));
+                        for (int d3 = 0; d3 < 2; d3++) {
+                            s_open[d3][lane] = (int)ld(3 + 6 * d3);
+                            s_chi[d3][lane] = __longlong_as_double((long long)ld(4 + 6 * d3));
+                            s_lb[d3][lane] = __longlong_as_double((long long)ld(5 + 6 * d3));
+                            s_pest[d3][lane] = __longlong_as_double((long long)ld(6 + 6 * d3));
+                            s_best[d3][lane] = __longlong_as_double((long long)ld(7 + 6 * d3));
+                            s_bchi[d3][lane] = __longlong_as_double((long long)ld(8 + 6 * d3));
+                        }
+                    }
+                }
+                __syncthreads();
+                if (s_cancel[0]) {
+                    cancelled = true;
+                    break;
+                }
+                // the directions this workgroup integrated: the walkers still live and open there
+                // take pass 2's chi2 and estimate, and the step-doubling change against pass 1's RV
+                // (team A's, write-through) and this pass's (P.rvp2)
+                for (int d3 = 0; d3 < 2; d3++) {
+                    const bool mine = own < 0 ? (((d3 == 0 ? mk0 : mk1) != 0)) : d3 == own;
+                    if (!mine || wv != 0 || lane >= WPB) continue;
+                    const bool open_here = s_xfault == 0 && s_live[lane] != 0 && s_open[d3][lane] == 1;
+                    const uint64_t needb = ballot(open_here);
+                    if (open_here) {
+                        const DirSched& SB = d3 ? P.bwd : P.fwd;
+                        const int Eb = SB.n_epochs;
+                        const double* b_dir = s_sched + (size_t)d3 * 4 * emax;
+                        const double* b_rv = b_dir + Eb;
+                        const double* b_s2 = b_dir + 2 * Eb;
+                        const size_t off = (size_t)d3 * P.lvx_emax * P.lvx_stride + wme;
+                        double d2b = 0.0;
+                        for (int e = 0; e < Eb; e++) {
+                            const double pv = __longlong_as_double((long long)__hip_atomic_load(
+                                (gu64*)(P.rvp + off + (size_t)e * P.lvx_stride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                            const double rvx = P.rvp2[off + (size_t)e * P.lvx_stride];
+                            const double r = rvx - b_rv[e];
+                            d2b += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
+                        }
+                        pass_result(d3, 2, s_tc2[d3][lane], s_te2[d3][lane], d2b, s_ter[d3][lane]);
+                    }
+                    if (lane == 0 && needb)
+                        __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(needb),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                __syncthreads();
+            }
             if (own >= 0 && wv == 0) {
                 // split: publish this direction's state of every walker (the meeting slot's encoding,
                 // rvm_walker.h: chi2, -lb, or the ENCOUNTER status) as write-through granules, drain,
@@ -326,7 +482,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 // flag and one agent-scope acquire (cdna_hip_programming.md §6 Guideline 16, R1).
                 // Double-buffered by the pass's parity: a partner reads pass rf's values before it
                 // publishes rf + 1, which this workgroup awaits before it writes rf + 2.
-                const size_t xb = ((size_t)g * 2) * 2 * 64;
+                // (each team of a group its own slots and flags)
+                const size_t xb = ((size_t)(g * 2 + tm) * 2) * 2 * 64;
                 gu64* mine = (gu64*)(P.rq_x + xb + ((size_t)own * 2 + (rf & 1)) * 64);
                 gu64* theirs = (gu64*)(P.rq_x + xb + ((size_t)(own ^ 1) * 2 + (rf & 1)) * 64);
                 if (lane < WPB) {
@@ -339,9 +496,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const unsigned long long tag = (gen << 8) | (unsigned long long)rf;
                 if (lane == 0)
-                    __hip_atomic_store((gu64*)(P.rq_xf + (size_t)g * 2 + own), tag, __ATOMIC_RELAXED,
+                    __hip_atomic_store((gu64*)(P.rq_xf + ((size_t)g * 2 + tm) * 2 + own), tag, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                gu64* tf = (gu64*)(P.rq_xf + (size_t)g * 2 + (own ^ 1));
+                gu64* tf = (gu64*)(P.rq_xf + ((size_t)g * 2 + tm) * 2 + (own ^ 1));
                 SpinClock clk;
                 clk.restart();
                 bool ok = true;
@@ -417,12 +574,43 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     s_mask[0] = m0;
                     s_mask[1] = m1;
                 }
+                if (team && tm == 0 && own <= 0) {
+                    // team A after pass 1: publish the walkers' state for team B (write-through
+                    // granules, drain, then the flag: 2 when the group is done and B may stop)
+                    if (lane < WPB) {
+                        auto st = [&](int row, unsigned long long v) {
+                            __hip_atomic_store(tpub + row * 64 + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        };
+                        auto bits = [](double v) { return (unsigned long long)__double_as_longlong(v); };
+                        st(0, (unsigned long long)s_live[lane]);
+                        st(1, (unsigned long long)(unsigned)s_stw[lane]);
+                        st(2, bits(s_lpw[lane]));
+                        for (int d3 = 0; d3 < 2; d3++) {
+                            st(3 + 6 * d3, (unsigned long long)(unsigned)s_open[d3][lane]);
+                            st(4 + 6 * d3, bits(s_chi[d3][lane]));
+                            st(5 + 6 * d3, bits(s_lb[d3][lane]));
+                            st(6 + 6 * d3, bits(s_pest[d3][lane]));
+                            st(7 + 6 * d3, bits(s_best[d3][lane]));
+                            st(8 + 6 * d3, bits(s_bchi[d3][lane]));
+                        }
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0)
+                        __hip_atomic_store(tflag, (gen << 8) | ((m0 | m1) == 0 ? 2ull : 1ull), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             __syncthreads();
+            if (team && tm == 0) {
+                // team A ends after pass 1; it finishes the group only when no walker is left for B
+                finisher = own <= 0 && (s_mask[0] | s_mask[1]) == 0;
+                break;
+            }
         }
+        if (team && tm == 1) finisher = own <= 0 && !cancelled;
         // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h;
-        // a split group's by its forward-direction workgroup)
-        if (own <= 0 && wv == 0 && lane < WPB && lane < cnt) {
+        // a split group's by its forward-direction workgroup, of team A or B)
+        if (finisher && wv == 0 && lane < WPB && lane < cnt) {
             int k2 = 0, wk2 = wme, j2 = 0, jp2 = 0;
             double z2 = 0.0, zp2 = 0.0;
             if (stretch) stretch_slot(sa, wme, k2, wk2, z2, j2, zp2, jp2);

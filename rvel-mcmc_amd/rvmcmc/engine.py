@@ -214,8 +214,13 @@ class LoglPlan:
         vals = (C.c_int64 * _lib.RVM_N_COUNTERS)()
         _lib.check(self.lib.rvm_plan_counters(self._h, int(bool(reset)), vals, _lib.RVM_N_COUNTERS,
                                               _lib.stream_handle(stream)), "rvm_plan_counters")
-        return dict(handoff_timeouts=vals[0], nonfinite=vals[1], unresolved=vals[2], refined=vals[3],
-                    truncated=vals[4], floor_settled=vals[5])
+        f = dict(handoff_timeouts=vals[0], nonfinite=vals[1], unresolved=vals[2], refined=vals[3],
+                 truncated=vals[4], floor_settled=vals[5])
+        if reset:  # (running totals over every reset: the samplers' periodic checks reset the counters)
+            tot = self.__dict__.setdefault("totals", dict.fromkeys(f, 0))
+            for k, v in f.items():
+                tot[k] += v
+        return f
 
     def check_faults(self, what="plan", stream=None, group=None) -> dict:
         """Raise RvmError on hand-off timeouts, NONFINITE results, or (a plan that refines, resolve_max
