@@ -477,7 +477,8 @@ def plan_for(obs, n_planets, dt, levels, max_walkers, device=None, period_hint=0
     cache = obs.__dict__.setdefault("_rvm_plans", {})
     mult = level_multipliers(levels)
     stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0
-    resolve = (float(resolve[0]), int(resolve[1]), float(resolve[2]) if len(resolve) > 2 else 0.0)
+    resolve = (float(resolve[0]), int(resolve[1]), float(resolve[2]) if len(resolve) > 2 else 0.0,
+               bool(resolve[3]) if len(resolve) > 3 else True)
     key = (str(dev), int(stream), int(n_planets), float(dt), mult, float(period_hint), bool(inclined), resolve)
     plan = cache.pop(key, None)
     if plan is None or plan.max_walkers < max_walkers:

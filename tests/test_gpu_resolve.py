@@ -356,3 +356,71 @@ def test_t1_eccentricity_guard(W):
     rf0 = O.logl_whx_adapt_batch(_oracle_P(X), 2, obs, dt, mult, TOL, RMAX)[2]
     print(f"W={W}: directions extended {int((rf == 1).sum())} with the guard, {int((rf0 == 1).sum())} without")
     assert (rf >= 1).sum() > (rf0 >= 1).sum()
+
+
+def test_refinement_layouts_bit_identical():
+    """The refinement kernel's layouts -- two teams (pass 1 and pass 2 at once, the default), one
+    team with each direction on its own workgroup (RVM_REFINE_TEAMS=0), both directions in one
+    workgroup (RVM_REFINE_SPLIT=0) -- take the same decisions with the same bits: four speculative
+    iterations of the sampler at the bench chain's steady state (extensions, halving passes,
+    certain rejects, two-pass walkers), positions, log-probabilities and plan counters compared."""
+    import os
+
+    from conftest import ROOT
+    from rvmcmc.ensemble import EnsembleSampler
+    from rvmcmc.state import State
+
+    torch = _torch()
+    X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_it2000.npy"))
+    runs = []
+    for env in ({}, {"RVM_REFINE_TEAMS": "0"}, {"RVM_REFINE_SPLIT": "0"}):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            s = State(planets=[dict(p) for p in S2_PLANETS])
+            ens = EnsembleSampler(len(X0), s, s2_obs_oracle(), seed=2017)  # (a fresh observation set: fresh plans)
+            ens.set_positions(X0)
+            ens.compute_lnprob()
+            ens.plan.faults(reset=True)
+            for _ in range(4):
+                ens.step()
+            torch.cuda.synchronize()
+            runs.append((ens.gather_positions(), np.concatenate([l.cpu().numpy() for l in ens.lnp]),
+                         ens.plan.faults(reset=True)))
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+    assert runs[0][2]["refined"] > 0 and runs[0][2]["truncated"] > 0
+    for X, lp, f in runs[1:]:
+        np.testing.assert_array_equal(X, runs[0][0])
+        np.testing.assert_array_equal(lp, runs[0][1])
+        assert f == runs[0][2], (f, runs[0][2])
+
+
+def test_certain_reject_can_be_switched_off():
+    """IntegratorConfig.certain_reject = False (rvm_plan_set_certain_reject): no refinement is cut
+    short -- every open walker refines to the bound -- and the sampler still runs at the steady
+    state."""
+    import dataclasses
+    import os
+
+    from conftest import ROOT
+    from rvmcmc.ensemble import EnsembleSampler
+    from rvmcmc.state import State
+
+    torch = _torch()
+    X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_it2000.npy"))
+    s = State(planets=[dict(p) for p in S2_PLANETS])
+    s.integrator = dataclasses.replace(s.integrator, certain_reject=False)
+    ens = EnsembleSampler(len(X0), s, s2_obs_oracle(), seed=2017)
+    assert not ens.plan.certain_reject
+    ens.set_positions(X0)
+    ens.compute_lnprob()
+    for _ in range(2):
+        ens.step()
+    torch.cuda.synchronize()
+    f = ens.plan.faults(reset=True)
+    assert f["refined"] > 0 and f["truncated"] == 0 and f["unresolved"] == 0, f
