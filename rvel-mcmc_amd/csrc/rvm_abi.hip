@@ -19,8 +19,9 @@ namespace rvm {
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
                        double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
 hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen,
+                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen, int eager,
                          hipStream_t stream);
+hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t stream);
 hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
                                   uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
                                   double* z, hipStream_t st);
@@ -74,6 +75,9 @@ struct rvm_plan {
     mutable std::vector<hipEvent_t> tev;
     mutable int32_t tcap = 0, tn = 0;
     mutable unsigned long long gen = 0;  // refinement launches so far (the split exchange's flag tag)
+    void* emem = nullptr;                // eager passes' results (DevPlan::rve, esum), small plans
+    hipStream_t side = nullptr;          // their stream, forked from and joined to the caller's
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 // One likelihood evaluation as every entry point runs it: the likelihood kernel, then (adaptive
@@ -81,11 +85,25 @@ struct rvm_plan {
 static hipError_t run_logl(const rvm_plan* plan, int W, const double* params, double hill_factor, double* logl,
                            int32_t* status, double* rv_out, const rvm::StretchArgs& sa, hipStream_t st) {
     const bool tm = plan->tn < plan->tcap;
+    // eager halving passes (rvm_refine.hip): plain launches of few walkers, no RV curve wanted; on
+    // the plan's side stream, forked from the caller's and joined before the refinement kernel
+    const bool mapped = sa.c != nullptr || sa.mh_scale != nullptr || sa.fd_x != nullptr;
+    const int eager = plan->emem != nullptr && !mapped && rv_out == nullptr && params != nullptr &&
+                      W <= plan->dev.eager_max;
+    hipError_t e = hipSuccess;
+    if (eager) {
+        e = hipEventRecord(plan->ev_fork, st);
+        if (e == hipSuccess) e = hipStreamWaitEvent(plan->side, plan->ev_fork, 0);
+        if (e == hipSuccess) e = rvm::launch_eager(plan->dev, W, params, hill_factor, plan->side);
+        if (e == hipSuccess) e = hipEventRecord(plan->ev_join, plan->side);
+        if (e != hipSuccess) return e;
+    }
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn], st);
-    hipError_t e = rvm::launch_logl(plan->dev, W, params, hill_factor, plan->slots, logl, status, rv_out, sa, st);
+    e = rvm::launch_logl(plan->dev, W, params, hill_factor, plan->slots, logl, status, rv_out, sa, st);
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 1], st);
+    if (e == hipSuccess && eager) e = hipStreamWaitEvent(st, plan->ev_join, 0);
     if (e == hipSuccess)
-        e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, ++plan->gen, st);
+        e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, ++plan->gen, eager, st);
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 2], st);
     if (tm) plan->tn++;
     return e;
@@ -363,12 +381,17 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.lvx = nullptr;
     P.rvp = nullptr;
     P.rvp2 = nullptr;
+    P.rve = nullptr;
+    P.esum = nullptr;
+    P.eager_max = 0;
     P.e2_guard = INFINITY;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
     P.ext_spec = 0;
     for (int k = 0; k <= RVM_MAX_LEVELS; k++) P.lw5[k] = 0.0;
-    if (P.rmax > 0 && cfg->n_levels >= 2 && cfg->n_levels < RVM_MAX_LEVELS) {
+    // (A/B knob RVM_NO_EXTENSION=1: no extension stage, flagged directions go straight to halving passes)
+    const char* noext = getenv("RVM_NO_EXTENSION");
+    if (P.rmax > 0 && cfg->n_levels >= 2 && cfg->n_levels < RVM_MAX_LEVELS && !(noext && noext[0] == '1')) {
         const int nl = cfg->n_levels;
         const size_t emax = std::max<size_t>(std::max(nf, nb), 1);
         const size_t bl = 2 * emax * (size_t)max_walkers * sizeof(double);  // partial sums
@@ -459,12 +482,44 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         if (const char* tp = getenv("RVM_REFINE_TEAMS"))  // (A/B knob: 0 runs the passes one after the other)
             if (tp[0] == '0') P.rq_t = nullptr;
     }
+    // eager halving passes for the plan's small plain launches (SMALA's centres, the scalar State
+    // API): results of passes 1 and 2 of up to RVM_EAGER_MAX walkers, a side stream and two events
+    // (any failure: no eager passes, the refinement kernel integrates as usual)
+    {
+        const char* eg = getenv("RVM_EAGER");  // (A/B knob: 0 turns the eager passes off)
+        const int emw = std::min<int>(max_walkers, rvm::RVM_EAGER_MAX);
+        if (P.rmax >= 2 && P.rvp != nullptr && cfg->n_levels <= 4 && !(eg && eg[0] == '0')) {
+            const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
+            const size_t b = (4 * plane + 12 * (size_t)P.lvx_stride) * sizeof(double);
+            if (hipMalloc(&plan->emem, b) == hipSuccess &&
+                hipStreamCreateWithFlags(&plan->side, hipStreamNonBlocking) == hipSuccess &&
+                hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming) == hipSuccess &&
+                hipEventCreateWithFlags(&plan->ev_join, hipEventDisableTiming) == hipSuccess) {
+                P.rve = reinterpret_cast<double*>(plan->emem);
+                P.esum = P.rve + 4 * plane;
+                P.eager_max = emw;
+            } else {
+                (void)hipGetLastError();
+                if (plan->ev_fork) (void)hipEventDestroy(plan->ev_fork);
+                if (plan->side) (void)hipStreamDestroy(plan->side);
+                if (plan->emem) (void)hipFree(plan->emem);
+                plan->emem = nullptr;
+                plan->side = nullptr;
+                plan->ev_fork = plan->ev_join = nullptr;
+            }
+        }
+    }
     *out = plan;
     return 0;
 }
 
 void rvm_plan_destroy(rvm_plan* plan) {
     if (!plan) return;
+    if (plan->side) (void)hipStreamSynchronize(plan->side);
+    if (plan->ev_fork) (void)hipEventDestroy(plan->ev_fork);
+    if (plan->ev_join) (void)hipEventDestroy(plan->ev_join);
+    if (plan->side) (void)hipStreamDestroy(plan->side);
+    if (plan->emem) (void)hipFree(plan->emem);
     for (hipEvent_t ev : plan->tev) (void)hipEventDestroy(ev);
     if (plan->rqmem) (void)hipFree(plan->rqmem);
     if (plan->lvmem) (void)hipFree(plan->lvmem);

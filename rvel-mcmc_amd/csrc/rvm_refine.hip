@@ -60,7 +60,8 @@ template <int NP, bool D3>
 __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int W, const double* __restrict__ params,
                                                      const double hill_factor, double* __restrict__ rv_out,
                                                      double* __restrict__ logl_out, int32_t* __restrict__ status_out,
-                                                     const StretchArgs sa, const unsigned long long gen) {
+                                                     const StretchArgs sa, const unsigned long long gen,
+                                                     const int eager) {
     constexpr int L = LanesPerWalker<NP>::value;
     constexpr int WPB = 64 / L;
     constexpr int PR = D3 ? 7 : 5;
@@ -90,7 +91,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     // after every pass; only when every task has a workgroup of its own in the grid (all co-resident
     // once dispatched; in-order dispatch leaves at most one workgroup waiting for its partner)
     const int ntask_split = 2 * gq0 + gq1 + gq2;
-    const bool split = P.rq_x != nullptr && gq0 <= P.rq_xgroups && ((int)gridDim.x & 1) == 0 &&
+    // (eager: passes 1 and 2 are replays of eager_kernel's results, both directions in one block)
+    const bool split = !eager && P.rq_x != nullptr && gq0 <= P.rq_xgroups && ((int)gridDim.x & 1) == 0 &&
                        ntask_split <= (int)gridDim.x;
     // teams: A (pass 1) and B (pass 2 concurrently, then the rest) per group -- when the split
     // layout holds, every team task fits the grid, and no RV curve is wanted (both teams would
@@ -272,10 +274,41 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
             const int amw = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);  // directions a live walker still needs
             if (amw == 0) break;
+            if (eager && rf <= 2) {
+                // eager_kernel ran passes 1 and 2 of every walker beside the likelihood kernel: the
+                // walkers' combiner values of pass rf, their step-doubling change against the
+                // previous pass's RV (the main pass's in P.rvp, or pass 1's), then as after a pass
+                if (wv == 0 && lane < WPB) {
+                    for (int d3 = 0; d3 < 2; d3++) {
+                        const uint64_t need = d3 ? mk1 : mk0;
+                        if (!((need >> lane) & 1)) continue;
+                        const DirSched& SB = d3 ? P.bwd : P.fwd;
+                        const int Eb = SB.n_epochs;
+                        const double* b_dir = s_sched + (size_t)d3 * 4 * emax;
+                        const double* b_rv = b_dir + Eb;
+                        const double* b_s2 = b_dir + 2 * Eb;
+                        const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
+                        const double* cur = P.rve + ((size_t)(rf - 1) * 2 + d3) * plane + wme;
+                        const double* prv = rf == 1 ? P.rvp + (size_t)d3 * plane + wme : P.rve + (size_t)d3 * plane + wme;
+                        double d2 = 0.0;
+                        for (int e = 0; e < Eb; e++) {
+                            const double rvx = cur[(size_t)e * P.lvx_stride], pv = prv[(size_t)e * P.lvx_stride];
+                            const double r = rvx - b_rv[e];
+                            d2 += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
+                        }
+                        const double* es = P.esum + ((size_t)(rf - 1) * 2 + d3) * 3 * P.lvx_stride + wme;
+                        pass_result(d3, rf, es[0], es[P.lvx_stride], d2, (int)es[2 * (size_t)P.lvx_stride]);
+                    }
+                }
+                if (wv == 0 && lane == 0) {
+                    const unsigned long long nd = __builtin_popcountll(mk0) + __builtin_popcountll(mk1);
+                    if (nd) __hip_atomic_fetch_add(P.counters + 3, nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             const int am = own < 0 ? amw : (amw & (1 << own));  // the ones this workgroup integrates
             // sub-passes: both directions at once (up to four levels), else one after the other;
             // none when a split task's own direction is done (the partner's pass only)
-            const int nsub = am == 0 ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
+            const int nsub = (am == 0 || (eager && rf <= 2)) ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
             for (int sp = 0; sp < nsub; sp++) {
                 // this wave's (direction, level) task, or none
                 const bool both = am == 3 && nl <= 4;
@@ -329,7 +362,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 double c2 = 0.0, e2 = 0.0, d2 = hasp ? 0.0 : INFINITY;  // (the combiner lanes)
                 // the previous pass's RV, replaced by this pass's: P.rvp (team B: P.rvp2, its own;
                 // its first pass only writes it -- pass 1's RV is still being written by team A)
-                double* pbuf = tm ? P.rvp2 : P.rvp;
+                // (eager: pass 2's RV in P.rve, replaced in place from pass 3 on)
+                double* pbuf = eager ? P.rve + (size_t)2 * P.lvx_emax * P.lvx_stride : (tm ? P.rvp2 : P.rvp);
                 double* pp = hasp ? pbuf + (size_t)dd_u * P.lvx_emax * P.lvx_stride + (cmb ? wme : 0) : nullptr;
                 for (int e = 0; e < eb; e++) {
                     const bool here = e < Er;
@@ -623,10 +657,115 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     }
 }
 
+// Eager halving passes (round 4): for a plain launch of few walkers (SMALA's centres, the scalar
+// State API), the first two halving passes of EVERY walker run on a side stream at the same time
+// as the likelihood kernel, on CUs the launch leaves idle; the refinement kernel then replays them
+// for the walkers it gets (their chi2, estimate, encounter flag and RV per epoch, stored here)
+// instead of integrating them after the likelihood kernel -- the same decisions and bits as the
+// sequential passes, one likelihood-kernel time instead of it plus one or two passes.
+// Grid: (groups of WPB walkers) x 2 directions x 2 passes, four waves per block (one per level).
+template <int NP, bool D3>
+__global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W, const double* __restrict__ params,
+                                                    const double hill_factor) {
+    constexpr int L = LanesPerWalker<NP>::value;
+    constexpr int WPB = 64 / L;
+    constexpr int PR = D3 ? 7 : 5;
+    constexpr int R = PR * NP;
+    const int wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int slot = lane / L;
+    const int pl_idx = lane % L;
+    const int nl = P.n_levels;
+    const int g = blockIdx.x >> 2, dd = (blockIdx.x >> 1) & 1, rf = 1 + (blockIdx.x & 1);
+    const DirSched& SR = dd ? P.bwd : P.fwd;
+    const int Er = SR.n_epochs;
+    __shared__ double s_rv[2][RVM_MAX_LEVELS][64];
+    __shared__ int s_enc[RVM_MAX_LEVELS][64];
+    const int w0 = g * WPB;
+    const int wo = w0 + slot < W ? w0 + slot : w0;  // (lanes past the last walker repeat the group's first)
+    double rowv[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) rowv[r] = params[(size_t)r * W + wo];
+    Lane<NP> s;
+    int status = RVM_STATUS_OK;
+    double e2w;
+    walker_setup<NP, D3, L>(rowv, pl_idx, hill_factor, s, status, e2w);
+    int k = wv < nl ? wv : -1;
+    k = __builtin_amdgcn_readfirstlane(k);
+    const int k_u = k < 0 ? 0 : k;
+    const bool work = k >= 0;
+    KickPrep<NP> kq{};
+    if (work && Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
+    const int m_r = P.mult[k_u] << rf;
+    const int nt_r = P.nt[k_u];
+    const double sc = ldexp(P.inv_mult[k_u], -rf);
+    const bool cmb = work && k == 0 && lane < WPB && w0 + lane < W;
+    const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
+    double* rvo = P.rve + ((size_t)(rf - 1) * 2 + dd) * plane + (cmb ? w0 + lane : 0);
+    double c2 = 0.0, e2 = 0.0;
+    for (int e = 0; e < Er; e++) {
+        const int ns = __builtin_amdgcn_readfirstlane(work ? SR.seg_n[e] * m_r : 0);
+        if (ns > 0) segment_gated<D3, NP, L>(s, kq, SR.seg_h1[e] * sc, ns, nt_r);
+        if (work) {
+            const double v0 = star_vx<NP, L>(s);
+            if (pl_idx == 0) s_rv[e & 1][k_u][slot] = v0;
+        }
+        __syncthreads();
+        if (cmb) {  // (the refinement kernel's combiner, expression for expression)
+            double rvx = 0.0, rv3 = 0.0;
+            for (int q = 0; q < nl; q++) rvx += P.lw[q] * s_rv[e & 1][q][lane];
+            for (int q = 1; q < nl; q++) rv3 += P.lw3[q] * s_rv[e & 1][q][lane];
+            const double ob = SR.obs_rv[e], s2 = SR.obs_s2[e];
+            const double r = rvx - ob;
+            c2 += (r * r) / s2;
+            e2 += fabs((rvx - rv3) * (r + (rv3 - ob))) / s2;
+            rvo[(size_t)e * P.lvx_stride] = rvx;
+        }
+    }
+    if (work && pl_idx == 0) s_enc[k_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
+    __syncthreads();
+    if (cmb) {
+        int er = 0;
+        for (int q = 0; q < nl; q++) er |= s_enc[q][lane];
+        double* es = P.esum + ((size_t)(rf - 1) * 2 + dd) * 3 * P.lvx_stride + w0 + lane;
+        es[0] = c2;
+        es[P.lvx_stride] = e2;
+        es[2 * (size_t)P.lvx_stride] = (double)er;
+    }
+}
+
+template <int NPV, bool D3V>
+static hipError_t launch_eager_t(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t st) {
+    constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
+    const int groups = (W + wpb - 1) / wpb;
+    eager_kernel<NPV, D3V><<<dim3(4 * groups), dim3(256), 0, st>>>(P, W, params, hill_factor);
+    return hipGetLastError();
+}
+
+hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t stream) {
+    const bool inc = P.inclined != 0;
+    switch (P.n_planets) {
+        case 1:
+            return inc ? launch_eager_t<1, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<1, false>(P, W, params, hill_factor, stream);
+        case 2:
+            return inc ? launch_eager_t<2, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<2, false>(P, W, params, hill_factor, stream);
+        case 3:
+            return inc ? launch_eager_t<3, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<3, false>(P, W, params, hill_factor, stream);
+        case 4:
+            return inc ? launch_eager_t<4, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<4, false>(P, W, params, hill_factor, stream);
+        default:
+            return hipErrorInvalidValue;
+    }
+}
+
 template <int NPV, bool D3V>
 static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
                                   int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen,
-                                  hipStream_t stream) {
+                                  int eager, hipStream_t stream) {
     constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t smem = (size_t)emax * 8 * sizeof(double);
@@ -652,18 +791,18 @@ static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params,
     int nb = std::max(2, std::min(P.n_cu > 0 ? P.n_cu : 256, 2 * groups));
     nb &= ~1;
     refine_kernel<NPV, D3V><<<dim3(nb), dim3(512), smem, stream>>>(P, W, params, hill_factor, rv_out, logl, status, sa,
-                                                                   gen);
+                                                                   gen, eager);
     return hipGetLastError();
 }
 
 hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen,
+                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen, int eager,
                          hipStream_t stream) {
     if (P.rmax <= 0 || P.rq_n == nullptr) return hipSuccess;
     const bool inc = P.inclined != 0;
 #define RVM_LAUNCH_R(NPV)                                                                             \
-    (inc ? launch_refine_t<NPV, true>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, stream) \
-         : launch_refine_t<NPV, false>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, stream))
+    (inc ? launch_refine_t<NPV, true>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, eager, stream) \
+         : launch_refine_t<NPV, false>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, eager, stream))
     switch (P.n_planets) {
         case 1:
             return RVM_LAUNCH_R(1);
