@@ -15,13 +15,19 @@
 
 #include "rvm_internal.h"
 
+// the eager first halving pass for small plain launches (rvm_refine.hip), unless RVM_EAGER says otherwise
+#ifndef RVM_EAGER_DEFAULT
+#define RVM_EAGER_DEFAULT false
+#endif
+
 namespace rvm {
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
                        double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
 hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
                          int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen, int eager,
                          hipStream_t stream);
-hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t stream);
+hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long gen,
+                        hipStream_t stream);
 hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
                                   uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
                                   double* z, hipStream_t st);
@@ -85,25 +91,25 @@ struct rvm_plan {
 static hipError_t run_logl(const rvm_plan* plan, int W, const double* params, double hill_factor, double* logl,
                            int32_t* status, double* rv_out, const rvm::StretchArgs& sa, hipStream_t st) {
     const bool tm = plan->tn < plan->tcap;
-    // eager halving passes (rvm_refine.hip): plain launches of few walkers, no RV curve wanted; on
-    // the plan's side stream, forked from the caller's and joined before the refinement kernel
+    // eager first halving pass (rvm_refine.hip): plain launches of few walkers, no RV curve wanted;
+    // on the plan's side stream, forked from the caller's (it reads the walkers), never joined: the
+    // refinement kernel waits for the groups it needs by their flags and cancels the others
     const bool mapped = sa.c != nullptr || sa.mh_scale != nullptr || sa.fd_x != nullptr;
     const int eager = plan->emem != nullptr && !mapped && rv_out == nullptr && params != nullptr &&
                       W <= plan->dev.eager_max;
+    const unsigned long long gen = ++plan->gen;  // (the launch generation: flags of both kernels)
     hipError_t e = hipSuccess;
     if (eager) {
         e = hipEventRecord(plan->ev_fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(plan->side, plan->ev_fork, 0);
-        if (e == hipSuccess) e = rvm::launch_eager(plan->dev, W, params, hill_factor, plan->side);
-        if (e == hipSuccess) e = hipEventRecord(plan->ev_join, plan->side);
+        if (e == hipSuccess) e = rvm::launch_eager(plan->dev, W, params, hill_factor, gen, plan->side);
         if (e != hipSuccess) return e;
     }
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn], st);
     e = rvm::launch_logl(plan->dev, W, params, hill_factor, plan->slots, logl, status, rv_out, sa, st);
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 1], st);
-    if (e == hipSuccess && eager) e = hipStreamWaitEvent(st, plan->ev_join, 0);
     if (e == hipSuccess)
-        e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, ++plan->gen, eager, st);
+        e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, gen, eager, st);
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 2], st);
     if (tm) plan->tn++;
     return e;
@@ -383,6 +389,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.rvp2 = nullptr;
     P.rve = nullptr;
     P.esum = nullptr;
+    P.eflag = nullptr;
     P.eager_max = 0;
     P.e2_guard = INFINITY;
     P.lvx_emax = 0;
@@ -486,17 +493,22 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     // API): results of passes 1 and 2 of up to RVM_EAGER_MAX walkers, a side stream and two events
     // (any failure: no eager passes, the refinement kernel integrates as usual)
     {
-        const char* eg = getenv("RVM_EAGER");  // (A/B knob: 0 turns the eager passes off)
+        const char* eg = getenv("RVM_EAGER");  // (A/B knob: 0 turns the eager pass off, 1 on)
+        const bool eager_on = eg ? eg[0] == '1' : RVM_EAGER_DEFAULT;
         const int emw = std::min<int>(max_walkers, rvm::RVM_EAGER_MAX);
-        if (P.rmax >= 2 && P.rvp != nullptr && cfg->n_levels <= 4 && !(eg && eg[0] == '0')) {
+        if (P.rmax >= 2 && P.rvp != nullptr && cfg->n_levels <= 4 && eager_on) {
+            // pass 1's RV [2][emax][stride] and sums [2][3][stride], the flags [groups][4] (zeroed)
             const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-            const size_t b = (4 * plane + 12 * (size_t)P.lvx_stride) * sizeof(double);
-            if (hipMalloc(&plan->emem, b) == hipSuccess &&
+            const size_t nflag = 4 * (size_t)((rvm::RVM_EAGER_MAX + 15) / 16) + 4;
+            const size_t b = (2 * plane + 6 * (size_t)P.lvx_stride + nflag) * sizeof(double);
+            if (hipMalloc(&plan->emem, b) == hipSuccess && hipMemset(plan->emem, 0, b) == hipSuccess &&
+                hipDeviceSynchronize() == hipSuccess &&
                 hipStreamCreateWithFlags(&plan->side, hipStreamNonBlocking) == hipSuccess &&
                 hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming) == hipSuccess &&
                 hipEventCreateWithFlags(&plan->ev_join, hipEventDisableTiming) == hipSuccess) {
                 P.rve = reinterpret_cast<double*>(plan->emem);
-                P.esum = P.rve + 4 * plane;
+                P.esum = P.rve + 2 * plane;
+                P.eflag = reinterpret_cast<unsigned long long*>(P.esum + 6 * (size_t)P.lvx_stride);
                 P.eager_max = emw;
             } else {
                 (void)hipGetLastError();

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     // after every pass; only when every task has a workgroup of its own in the grid (all co-resident
     // once dispatched; in-order dispatch leaves at most one workgroup waiting for its partner)
     const int ntask_split = 2 * gq0 + gq1 + gq2;
-    // (eager: passes 1 and 2 are replays of eager_kernel's results, both directions in one block)
+    // (eager: pass 1 is a replay of eager_kernel's results, both directions in one block)
     const bool split = !eager && P.rq_x != nullptr && gq0 <= P.rq_xgroups && ((int)gridDim.x & 1) == 0 &&
                        ntask_split <= (int)gridDim.x;
     // teams: A (pass 1) and B (pass 2 concurrently, then the rest) per group -- when the split
@@ -101,6 +101,25 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     const bool team = split && P.rq_t != nullptr && P.rvp != nullptr && P.rvp2 != nullptr && P.rmax >= 2 &&
                       rv_out == nullptr && ng <= P.rq_xgroups && ntask_team <= (int)gridDim.x;
     const int ntask = team ? ntask_team : (split ? ntask_split : ng);
+    if (eager && blockIdx.x == 0) {
+        // eager pass 1 ran for every group of walkers: cancel the groups none of whose walkers is
+        // listed here (their blocks stop at the next epoch, or before reading their walkers)
+        constexpr int EG = (RVM_EAGER_MAX + WPB - 1) / WPB;
+        __shared__ int s_need[EG];
+        const int ngw = (W + WPB - 1) / WPB;
+        for (int i = threadIdx.x; i < EG; i += blockDim.x) s_need[i] = 0;
+        __syncthreads();
+        for (int li2 = 0; li2 < 3; li2++)
+            for (int i = threadIdx.x; i < nq[li2]; i += blockDim.x) {
+                const int wl = P.rq_w[(size_t)li2 * P.rq_cap + i];
+                if (wl >= 0 && wl / WPB < EG) s_need[wl / WPB] = 1;
+            }
+        __syncthreads();
+        for (int i = threadIdx.x; i < ngw && i < EG; i += blockDim.x)
+            if (!s_need[i])
+                __hip_atomic_store((gu64*)(P.eflag + (size_t)i * 4), (gen << 8) | 1ull, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
     if ((int)blockIdx.x >= ntask) return;
 
     // LDS: both directions' schedules ([d][seg_h1 | obs_rv | obs_s2 | (seg_n, obs_idx)], E_d each),
@@ -274,30 +293,60 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
             const int amw = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);  // directions a live walker still needs
             if (amw == 0) break;
-            if (eager && rf <= 2) {
-                // eager_kernel ran passes 1 and 2 of every walker beside the likelihood kernel: the
-                // walkers' combiner values of pass rf, their step-doubling change against the
-                // previous pass's RV (the main pass's in P.rvp, or pass 1's), then as after a pass
-                if (wv == 0 && lane < WPB) {
-                    for (int d3 = 0; d3 < 2; d3++) {
-                        const uint64_t need = d3 ? mk1 : mk0;
-                        if (!((need >> lane) & 1)) continue;
-                        const DirSched& SB = d3 ? P.bwd : P.fwd;
-                        const int Eb = SB.n_epochs;
-                        const double* b_dir = s_sched + (size_t)d3 * 4 * emax;
-                        const double* b_rv = b_dir + Eb;
-                        const double* b_s2 = b_dir + 2 * Eb;
-                        const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-                        const double* cur = P.rve + ((size_t)(rf - 1) * 2 + d3) * plane + wme;
-                        const double* prv = rf == 1 ? P.rvp + (size_t)d3 * plane + wme : P.rve + (size_t)d3 * plane + wme;
-                        double d2 = 0.0;
-                        for (int e = 0; e < Eb; e++) {
-                            const double rvx = cur[(size_t)e * P.lvx_stride], pv = prv[(size_t)e * P.lvx_stride];
-                            const double r = rvx - b_rv[e];
-                            d2 += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
+            if (eager && rf == 1) {
+                // eager_kernel ran pass 1 of every walker beside the likelihood kernel: once its
+                // walker's group has flagged both directions done (write-through values), each
+                // combiner lane takes pass 1's chi2, estimate and encounter flag, and its step-doubling
+                // change against the main pass's RV (P.rvp), which pass 1's RV then replaces there
+                if (wv == 0) {
+                    const bool mine0 = lane < WPB && ((mk0 >> lane) & 1), mine1 = lane < WPB && ((mk1 >> lane) & 1);
+                    gu64* f0 = (gu64*)(P.eflag + (size_t)(wme / WPB) * 4 + 1);
+                    SpinClock clk;
+                    clk.restart();
+                    bool ok = true;
+                    for (;;) {
+                        const bool rdy = (!mine0 || __hip_atomic_load(f0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) &&
+                                         (!mine1 || __hip_atomic_load(f0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen);
+                        if (ballot(!rdy) == 0) break;
+                        if (clk.expired(P.spin_ticks)) {
+                            ok = false;
+                            break;
                         }
-                        const double* es = P.esum + ((size_t)(rf - 1) * 2 + d3) * 3 * P.lvx_stride + wme;
-                        pass_result(d3, rf, es[0], es[P.lvx_stride], d2, (int)es[2 * (size_t)P.lvx_stride]);
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    if (!ok) {
+                        if (lane == 0) {
+                            s_xfault = 1;
+                            __hip_atomic_fetch_add(P.counters, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                    } else {
+                        for (int d3 = 0; d3 < 2; d3++) {
+                            if (!(d3 ? mine1 : mine0)) continue;
+                            const DirSched& SB = d3 ? P.bwd : P.fwd;
+                            const int Eb = SB.n_epochs;
+                            const double* b_dir = s_sched + (size_t)d3 * 4 * emax;
+                            const double* b_rv = b_dir + Eb;
+                            const double* b_s2 = b_dir + 2 * Eb;
+                            const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
+                            gu64* cur = (gu64*)(P.rve + (size_t)d3 * plane + wme);
+                            double* prv = P.rvp + (size_t)d3 * plane + wme;
+                            double d2 = 0.0;
+                            for (int e = 0; e < Eb; e++) {
+                                const double rvx = __longlong_as_double((long long)__hip_atomic_load(
+                                    cur + (size_t)e * P.lvx_stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                                const double pv = prv[(size_t)e * P.lvx_stride];
+                                const double r = rvx - b_rv[e];
+                                d2 += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
+                                prv[(size_t)e * P.lvx_stride] = rvx;
+                            }
+                            gu64* es = (gu64*)(P.esum + (size_t)d3 * 3 * P.lvx_stride + wme);
+                            auto ld = [&](size_t o) {
+                                return __longlong_as_double((long long)__hip_atomic_load(es + o, __ATOMIC_RELAXED,
+                                                                                         __HIP_MEMORY_SCOPE_AGENT));
+                            };
+                            pass_result(d3, rf, ld(0), ld(P.lvx_stride), d2, (int)ld(2 * (size_t)P.lvx_stride));
+                        }
                     }
                 }
                 if (wv == 0 && lane == 0) {
@@ -308,7 +357,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             const int am = own < 0 ? amw : (amw & (1 << own));  // the ones this workgroup integrates
             // sub-passes: both directions at once (up to four levels), else one after the other;
             // none when a split task's own direction is done (the partner's pass only)
-            const int nsub = (am == 0 || (eager && rf <= 2)) ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
+            const int nsub = (am == 0 || (eager && rf == 1)) ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
             for (int sp = 0; sp < nsub; sp++) {
                 // this wave's (direction, level) task, or none
                 const bool both = am == 3 && nl <= 4;
@@ -362,8 +411,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 double c2 = 0.0, e2 = 0.0, d2 = hasp ? 0.0 : INFINITY;  // (the combiner lanes)
                 // the previous pass's RV, replaced by this pass's: P.rvp (team B: P.rvp2, its own;
                 // its first pass only writes it -- pass 1's RV is still being written by team A)
-                // (eager: pass 2's RV in P.rve, replaced in place from pass 3 on)
-                double* pbuf = eager ? P.rve + (size_t)2 * P.lvx_emax * P.lvx_stride : (tm ? P.rvp2 : P.rvp);
+                double* pbuf = tm ? P.rvp2 : P.rvp;
                 double* pp = hasp ? pbuf + (size_t)dd_u * P.lvx_emax * P.lvx_stride + (cmb ? wme : 0) : nullptr;
                 for (int e = 0; e < eb; e++) {
                     const bool here = e < Er;
@@ -657,16 +705,19 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     }
 }
 
-// Eager halving passes (round 4): for a plain launch of few walkers (SMALA's centres, the scalar
-// State API), the first two halving passes of EVERY walker run on a side stream at the same time
-// as the likelihood kernel, on CUs the launch leaves idle; the refinement kernel then replays them
-// for the walkers it gets (their chi2, estimate, encounter flag and RV per epoch, stored here)
-// instead of integrating them after the likelihood kernel -- the same decisions and bits as the
-// sequential passes, one likelihood-kernel time instead of it plus one or two passes.
-// Grid: (groups of WPB walkers) x 2 directions x 2 passes, four waves per block (one per level).
+// Eager first halving pass (round 4): for a plain launch of few walkers (SMALA's centres, the
+// scalar State API), pass 1 of EVERY walker runs on the plan's side stream at the same time as the
+// likelihood kernel, on CUs the launch leaves idle.  It stores each walker-direction's chi2,
+// estimate, encounter flag and RV per epoch write-through, then a per-(group, direction) flag
+// tagged with the launch generation; the refinement kernel waits only for the groups its walkers
+// are in and replays pass 1 for them instead of integrating it after the likelihood kernel (the
+// same decisions and bits), and at its start cancels every other group (a flag the blocks check
+// before reading their walkers and once per epoch).  Grid: (groups of WPB walkers) x 2
+// directions, four waves per block (one per level).  P.eflag [groups][4]: [0] cancel tag
+// (generation << 8 | 1), [1 + d] direction d done (generation).
 template <int NP, bool D3>
 __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W, const double* __restrict__ params,
-                                                    const double hill_factor) {
+                                                    const double hill_factor, const unsigned long long gen) {
     constexpr int L = LanesPerWalker<NP>::value;
     constexpr int WPB = 64 / L;
     constexpr int PR = D3 ? 7 : 5;
@@ -676,11 +727,17 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     const int slot = lane / L;
     const int pl_idx = lane % L;
     const int nl = P.n_levels;
-    const int g = blockIdx.x >> 2, dd = (blockIdx.x >> 1) & 1, rf = 1 + (blockIdx.x & 1);
+    const int g = blockIdx.x >> 1, dd = blockIdx.x & 1;
     const DirSched& SR = dd ? P.bwd : P.fwd;
     const int Er = SR.n_epochs;
     __shared__ double s_rv[2][RVM_MAX_LEVELS][64];
     __shared__ int s_enc[RVM_MAX_LEVELS][64];
+    __shared__ int s_cancel[2];
+    gu64* cflag = (gu64*)(P.eflag + (size_t)g * 4);
+    const unsigned long long ctag = (gen << 8) | 1ull;
+    if (threadIdx.x == 0) s_cancel[0] = __hip_atomic_load(cflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag;
+    __syncthreads();
+    if (s_cancel[0]) return;  // (before the walkers are read: the caller may be done with them)
     const int w0 = g * WPB;
     const int wo = w0 + slot < W ? w0 + slot : w0;  // (lanes past the last walker repeat the group's first)
     double rowv[R];
@@ -696,13 +753,14 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     const bool work = k >= 0;
     KickPrep<NP> kq{};
     if (work && Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
-    const int m_r = P.mult[k_u] << rf;
+    const int m_r = P.mult[k_u] << 1;
     const int nt_r = P.nt[k_u];
-    const double sc = ldexp(P.inv_mult[k_u], -rf);
+    const double sc = ldexp(P.inv_mult[k_u], -1);
     const bool cmb = work && k == 0 && lane < WPB && w0 + lane < W;
     const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-    double* rvo = P.rve + ((size_t)(rf - 1) * 2 + dd) * plane + (cmb ? w0 + lane : 0);
+    gu64* rvo = (gu64*)(P.rve + (size_t)dd * plane + (cmb ? w0 + lane : 0));
     double c2 = 0.0, e2 = 0.0;
+    bool cancelled = false;
     for (int e = 0; e < Er; e++) {
         const int ns = __builtin_amdgcn_readfirstlane(work ? SR.seg_n[e] * m_r : 0);
         if (ns > 0) segment_gated<D3, NP, L>(s, kq, SR.seg_h1[e] * sc, ns, nt_r);
@@ -710,7 +768,13 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
             const double v0 = star_vx<NP, L>(s);
             if (pl_idx == 0) s_rv[e & 1][k_u][slot] = v0;
         }
+        if (wv == 0 && lane == 0)
+            s_cancel[e & 1] = __hip_atomic_load(cflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag;
         __syncthreads();
+        if (s_cancel[e & 1]) {
+            cancelled = true;
+            break;
+        }
         if (cmb) {  // (the refinement kernel's combiner, expression for expression)
             double rvx = 0.0, rv3 = 0.0;
             for (int q = 0; q < nl; q++) rvx += P.lw[q] * s_rv[e & 1][q][lane];
@@ -719,44 +783,56 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
             const double r = rvx - ob;
             c2 += (r * r) / s2;
             e2 += fabs((rvx - rv3) * (r + (rv3 - ob))) / s2;
-            rvo[(size_t)e * P.lvx_stride] = rvx;
+            __hip_atomic_store(rvo + (size_t)e * P.lvx_stride, (unsigned long long)__double_as_longlong(rvx),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    if (cancelled) return;
     if (work && pl_idx == 0) s_enc[k_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
     __syncthreads();
-    if (cmb) {
-        int er = 0;
-        for (int q = 0; q < nl; q++) er |= s_enc[q][lane];
-        double* es = P.esum + ((size_t)(rf - 1) * 2 + dd) * 3 * P.lvx_stride + w0 + lane;
-        es[0] = c2;
-        es[P.lvx_stride] = e2;
-        es[2 * (size_t)P.lvx_stride] = (double)er;
+    if (wv == 0) {
+        if (cmb) {
+            int er = 0;
+            for (int q = 0; q < nl; q++) er |= s_enc[q][lane];
+            gu64* es = (gu64*)(P.esum + (size_t)dd * 3 * P.lvx_stride + w0 + lane);
+            auto bits = [](double v) { return (unsigned long long)__double_as_longlong(v); };
+            __hip_atomic_store(es, bits(c2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(es + P.lvx_stride, bits(e2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(es + 2 * (size_t)P.lvx_stride, bits((double)er), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            __hip_atomic_store((gu64*)(P.eflag + (size_t)g * 4 + 1 + dd), gen, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 template <int NPV, bool D3V>
-static hipError_t launch_eager_t(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t st) {
+static hipError_t launch_eager_t(const DevPlan& P, int W, const double* params, double hill_factor,
+                                 unsigned long long gen, hipStream_t st) {
     constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
     const int groups = (W + wpb - 1) / wpb;
-    eager_kernel<NPV, D3V><<<dim3(4 * groups), dim3(256), 0, st>>>(P, W, params, hill_factor);
+    eager_kernel<NPV, D3V><<<dim3(2 * groups), dim3(256), 0, st>>>(P, W, params, hill_factor, gen);
     return hipGetLastError();
 }
 
-hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t stream) {
+hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long gen,
+                        hipStream_t stream) {
     const bool inc = P.inclined != 0;
     switch (P.n_planets) {
         case 1:
-            return inc ? launch_eager_t<1, true>(P, W, params, hill_factor, stream)
-                       : launch_eager_t<1, false>(P, W, params, hill_factor, stream);
+            return inc ? launch_eager_t<1, true>(P, W, params, hill_factor, gen, stream)
+                       : launch_eager_t<1, false>(P, W, params, hill_factor, gen, stream);
         case 2:
-            return inc ? launch_eager_t<2, true>(P, W, params, hill_factor, stream)
-                       : launch_eager_t<2, false>(P, W, params, hill_factor, stream);
+            return inc ? launch_eager_t<2, true>(P, W, params, hill_factor, gen, stream)
+                       : launch_eager_t<2, false>(P, W, params, hill_factor, gen, stream);
         case 3:
-            return inc ? launch_eager_t<3, true>(P, W, params, hill_factor, stream)
-                       : launch_eager_t<3, false>(P, W, params, hill_factor, stream);
+            return inc ? launch_eager_t<3, true>(P, W, params, hill_factor, gen, stream)
+                       : launch_eager_t<3, false>(P, W, params, hill_factor, gen, stream);
         case 4:
-            return inc ? launch_eager_t<4, true>(P, W, params, hill_factor, stream)
-                       : launch_eager_t<4, false>(P, W, params, hill_factor, stream);
+            return inc ? launch_eager_t<4, true>(P, W, params, hill_factor, gen, stream)
+                       : launch_eager_t<4, false>(P, W, params, hill_factor, gen, stream);
         default:
             return hipErrorInvalidValue;
     }
