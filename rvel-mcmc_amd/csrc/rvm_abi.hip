@@ -17,7 +17,7 @@
 
 // the eager first halving pass for small plain launches (rvm_refine.hip), unless RVM_EAGER says otherwise
 #ifndef RVM_EAGER_DEFAULT
-#define RVM_EAGER_DEFAULT false
+#define RVM_EAGER_DEFAULT true
 #endif
 
 namespace rvm {
@@ -96,7 +96,7 @@ static hipError_t run_logl(const rvm_plan* plan, int W, const double* params, do
     // refinement kernel waits for the groups it needs by their flags and cancels the others
     const bool mapped = sa.c != nullptr || sa.mh_scale != nullptr || sa.fd_x != nullptr;
     const int eager = plan->emem != nullptr && !mapped && rv_out == nullptr && params != nullptr &&
-                      W <= plan->dev.eager_max;
+                      W >= rvm::RVM_EAGER_MIN && W <= plan->dev.eager_max;
     const unsigned long long gen = ++plan->gen;  // (the launch generation: flags of both kernels)
     hipError_t e = hipSuccess;
     if (eager) {

@@ -35,6 +35,9 @@ constexpr int RVM_CX_MIN_WALKERS = 32;
 // plain launches of at most this many walkers run the first halving pass of every walker beside
 // the likelihood kernel (rvm_refine.hip eager_kernel): 2 x 512 / 32 = 32 blocks of 4 waves
 constexpr int RVM_EAGER_MAX = 512;
+// ... and at least this many (a launch of a few walkers rarely refines, and the fork costs the
+// scalar State API ~7 %: config 1, profiles/r04x_configs_eager_ab.jsonl)
+constexpr int RVM_EAGER_MIN = 32;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {

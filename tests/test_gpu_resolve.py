@@ -426,7 +426,7 @@ def test_certain_reject_can_be_switched_off():
     assert f["refined"] > 0 and f["truncated"] == 0 and f["unresolved"] == 0, f
 
 
-@pytest.mark.parametrize("W", [24, 256, 512])
+@pytest.mark.parametrize("W", [32, 256, 512])
 def test_eager_halving_passes_bit_identical(W):
     """Plain launches of few walkers run the first two halving passes of every walker beside the
     likelihood kernel (rvm_refine.hip eager_kernel) and the refinement kernel replays them: the same
