@@ -19,6 +19,12 @@
 #ifndef RVM_EAGER_DEFAULT
 #define RVM_EAGER_DEFAULT true
 #endif
+// eager halving passes run beside the likelihood kernel: pass 1 only (pass 2 as well, RVM_EAGER_PASSES=2,
+// measured slower: config 4 at 0.90 -> 1.07 ms per step -- the side stream's next launch queues behind
+// the longer eager kernel)
+#ifndef RVM_EAGER_PASSES_DEFAULT
+#define RVM_EAGER_PASSES_DEFAULT 1
+#endif
 
 namespace rvm {
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
@@ -91,7 +97,7 @@ struct rvm_plan {
 static hipError_t run_logl(const rvm_plan* plan, int W, const double* params, double hill_factor, double* logl,
                            int32_t* status, double* rv_out, const rvm::StretchArgs& sa, hipStream_t st) {
     const bool tm = plan->tn < plan->tcap;
-    // eager first halving pass (rvm_refine.hip): plain launches of few walkers, no RV curve wanted;
+    // eager halving passes 1 and 2 (rvm_refine.hip): plain launches of few walkers, no RV curve wanted;
     // on the plan's side stream, forked from the caller's (it reads the walkers), never joined: the
     // refinement kernel waits for the groups it needs by their flags and cancels the others
     const bool mapped = sa.c != nullptr || sa.mh_scale != nullptr || sa.fd_x != nullptr;
@@ -391,6 +397,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.esum = nullptr;
     P.eflag = nullptr;
     P.eager_max = 0;
+    P.eager_passes = 0;
     P.e2_guard = INFINITY;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
@@ -497,19 +504,21 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const bool eager_on = eg ? eg[0] == '1' : RVM_EAGER_DEFAULT;
         const int emw = std::min<int>(max_walkers, rvm::RVM_EAGER_MAX);
         if (P.rmax >= 2 && P.rvp != nullptr && cfg->n_levels <= 4 && eager_on) {
-            // pass 1's RV [2][emax][stride] and sums [2][3][stride], the flags [groups][4] (zeroed)
+            // passes 1 and 2: RV [2][2][emax][stride], sums [2][2][3][stride]; flags [groups][8] (zeroed)
             const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-            const size_t nflag = 4 * (size_t)((rvm::RVM_EAGER_MAX + 15) / 16) + 4;
-            const size_t b = (2 * plane + 6 * (size_t)P.lvx_stride + nflag) * sizeof(double);
+            const size_t nflag = 8 * (size_t)((rvm::RVM_EAGER_MAX + 15) / 16) + 8;
+            const size_t b = (4 * plane + 12 * (size_t)P.lvx_stride + nflag) * sizeof(double);
             if (hipMalloc(&plan->emem, b) == hipSuccess && hipMemset(plan->emem, 0, b) == hipSuccess &&
                 hipDeviceSynchronize() == hipSuccess &&
                 hipStreamCreateWithFlags(&plan->side, hipStreamNonBlocking) == hipSuccess &&
                 hipEventCreateWithFlags(&plan->ev_fork, hipEventDisableTiming) == hipSuccess &&
                 hipEventCreateWithFlags(&plan->ev_join, hipEventDisableTiming) == hipSuccess) {
                 P.rve = reinterpret_cast<double*>(plan->emem);
-                P.esum = P.rve + 2 * plane;
-                P.eflag = reinterpret_cast<unsigned long long*>(P.esum + 6 * (size_t)P.lvx_stride);
+                P.esum = P.rve + 4 * plane;
+                P.eflag = reinterpret_cast<unsigned long long*>(P.esum + 12 * (size_t)P.lvx_stride);
                 P.eager_max = emw;
+                const char* ep = getenv("RVM_EAGER_PASSES");  // (A/B knob: 1 or 2)
+                P.eager_passes = ep && ep[0] == '1' ? 1 : (ep && ep[0] == '2' ? 2 : RVM_EAGER_PASSES_DEFAULT);
             } else {
                 (void)hipGetLastError();
                 if (plan->ev_fork) (void)hipEventDestroy(plan->ev_fork);

@@ -32,8 +32,8 @@ constexpr double RVM_FLOOR_BOUND = 4.0;
 // launches of fewer walkers than this run the extension after the main pass (only when a walker is
 // flagged) instead of as a concurrent fifth wave of the one-group-per-block layout (launch_logl_t)
 constexpr int RVM_CX_MIN_WALKERS = 32;
-// plain launches of at most this many walkers run the first halving pass of every walker beside
-// the likelihood kernel (rvm_refine.hip eager_kernel): 2 x 512 / 32 = 32 blocks of 4 waves
+// plain launches of at most this many walkers run the first two halving passes of every walker
+// beside the likelihood kernel (rvm_refine.hip eager_kernel): 4 x 512 / 32 = 64 blocks of 4 waves
 constexpr int RVM_EAGER_MAX = 512;
 // ... and at least this many (a launch of a few walkers rarely refines, and the fork costs the
 // scalar State API ~7 %: config 1, profiles/r04x_configs_eager_ab.jsonl)
@@ -108,14 +108,15 @@ struct DevPlan {
     unsigned long long* rq_tf;
     // team B's own RV per pass (as rvp)
     double* rvp2;
-    // eager first halving pass (rvm_refine.hip eager_kernel; plain launches of at most eager_max
-    // walkers, 0: none): pass 1 of every walker beside the likelihood kernel -- rve [2 directions]
-    // [lvx_emax][lvx_stride] its RV per epoch, esum [2][3][lvx_stride] its chi2, estimate and
-    // encounter flag
+    // eager halving passes (rvm_refine.hip eager_kernel; plain launches of at most eager_max
+    // walkers, 0: none): passes 1 and 2 of every walker beside the likelihood kernel -- rve [2
+    // passes][2 directions][lvx_emax][lvx_stride] their RV per epoch, esum [2][2][3][lvx_stride]
+    // their chi2, estimate and encounter flag
     double* rve;
     double* esum;
-    unsigned long long* eflag;  // [groups][4]: cancel tag, pass 1 done per direction (rvm_refine.hip)
+    unsigned long long* eflag;  // [groups][8]: cancel tags, passes done per direction (rvm_refine.hip)
     int32_t eager_max;
+    int32_t eager_passes;  // (1 or 2: how many halving passes eager_kernel runs)
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
     // [3] walker-direction refinement passes (extension + halvings), [4] refinements cut short as

@@ -100,26 +100,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     const int ntask_team = 4 * gq0 + 2 * (gq1 + gq2);
     const bool team = split && P.rq_t != nullptr && P.rvp != nullptr && P.rvp2 != nullptr && P.rmax >= 2 &&
                       rv_out == nullptr && ng <= P.rq_xgroups && ntask_team <= (int)gridDim.x;
-    const int ntask = team ? ntask_team : (split ? ntask_split : ng);
-    if (eager && blockIdx.x == 0) {
-        // eager pass 1 ran for every group of walkers: cancel the groups none of whose walkers is
-        // listed here (their blocks stop at the next epoch, or before reading their walkers)
-        constexpr int EG = (RVM_EAGER_MAX + WPB - 1) / WPB;
-        __shared__ int s_need[EG];
-        const int ngw = (W + WPB - 1) / WPB;
-        for (int i = threadIdx.x; i < EG; i += blockDim.x) s_need[i] = 0;
-        __syncthreads();
-        for (int li2 = 0; li2 < 3; li2++)
-            for (int i = threadIdx.x; i < nq[li2]; i += blockDim.x) {
-                const int wl = P.rq_w[(size_t)li2 * P.rq_cap + i];
-                if (wl >= 0 && wl / WPB < EG) s_need[wl / WPB] = 1;
-            }
-        __syncthreads();
-        for (int i = threadIdx.x; i < ngw && i < EG; i += blockDim.x)
-            if (!s_need[i])
-                __hip_atomic_store((gu64*)(P.eflag + (size_t)i * 4), (gen << 8) | 1ull, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // (eager: one task per group of the launch's walkers, as eager_kernel grouped them)
+    const int ngw = (W + WPB - 1) / WPB;
+    const int ntask = eager ? ngw : (team ? ntask_team : (split ? ntask_split : ng));
     if ((int)blockIdx.x >= ntask) return;
 
     // LDS: both directions' schedules ([d][seg_h1 | obs_rv | obs_s2 | (seg_n, obs_idx)], E_d each),
@@ -144,6 +127,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     __shared__ double s_tc2[2][64], s_te2[2][64];
     __shared__ int s_ter[2][64];
     __shared__ int s_cancel[2];
+    // eager tasks: the group's walker indices and each slot's list (-1: not listed, the likelihood
+    // kernel finished it), and whether any slot is listed
+    __shared__ int s_eitems[64], s_eli[64], s_eany;
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     for (int dd = 0; dd < 2; dd++) {
         const DirSched& SD = dd ? P.bwd : P.fwd;
@@ -183,10 +169,38 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 g = t - gq0;
             }
         }
-        const int li = g < gq0 ? 0 : (g < gq0 + gq1 ? 1 : 2);
+        int li = g < gq0 ? 0 : (g < gq0 + gq1 ? 1 : 2);
         const int base = (li == 0 ? g : (li == 1 ? g - gq0 : g - gq0 - gq1)) * WPB;
-        const int cnt = nq[li] - base < WPB ? nq[li] - base : WPB;
+        int cnt = nq[li] - base < WPB ? nq[li] - base : WPB;
         const int* items = P.rq_w + (size_t)li * P.rq_cap + base;
+        gu64* ef = eager ? (gu64*)(P.eflag + (size_t)g * 8) : nullptr;  // (the eager group's flags)
+        if (eager) {
+            // the launch's walkers g * WPB ..: which of them the lists hold, and in which
+            const int w0 = g * WPB;
+            __syncthreads();  // (the previous task's LDS state is no longer read)
+            if (threadIdx.x < 64) {
+                s_eitems[threadIdx.x] = w0 + (int)threadIdx.x < W ? w0 + (int)threadIdx.x : w0;
+                s_eli[threadIdx.x] = -1;
+            }
+            if (threadIdx.x == 0) s_eany = 0;
+            __syncthreads();
+            for (int l2 = 0; l2 < 3; l2++)
+                for (int i = threadIdx.x; i < nq[l2]; i += blockDim.x) {
+                    const int wl = P.rq_w[(size_t)l2 * P.rq_cap + i];
+                    if (wl >= w0 && wl < w0 + WPB) {
+                        s_eli[wl - w0] = l2;
+                        s_eany = 1;
+                    }
+                }
+            __syncthreads();
+            if (!s_eany) {  // nothing to refine here: eager_kernel's blocks of the group stop
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(ef, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
+            items = s_eitems;
+            cnt = WPB;
+        }
         // this lane's walker (lanes past the group's last repeat its first walker: benign values)
         const int wo = items[slot < cnt ? slot : 0];
         int kind = 0, wk = wo, jst = 0, jp = 0;
@@ -210,9 +224,10 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             s_init[6][lane] = s.r;
             s_init[7][lane] = s.ir;
             if (lane < WPB) {
-                const bool v = lane < cnt;
-                const int wl = items[v ? lane : 0];
-                const bool of = v && li != 2, ob = v && li != 1;
+                const int lli = eager ? s_eli[lane] : li;  // (eager: this slot's list, -1 none)
+                const bool v = lane < cnt && lli >= 0;
+                const int wl = items[lane < cnt ? lane : 0];
+                const bool of = v && lli != 2, ob = v && lli != 1;
                 s_open[0][lane] = of ? 1 : 0;
                 s_open[1][lane] = ob ? 1 : 0;
                 s_chi[0][lane] = of ? 0.0 : P.rq_c[wl];
@@ -228,8 +243,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 s_stw[lane] = RVM_STATUS_NONFINITE;  // (every pass loop ends with a decision)
                 s_lpw[lane] = -INFINITY;
             }
-            const uint64_t m0 = ballot(lane < WPB && lane < cnt && li != 2);
-            const uint64_t m1 = ballot(lane < WPB && lane < cnt && li != 1);
+            const int lli = lane < WPB ? (eager ? s_eli[lane] : li) : -1;
+            const uint64_t m0 = ballot(lane < WPB && lane < cnt && lli >= 0 && lli != 2);
+            const uint64_t m1 = ballot(lane < WPB && lane < cnt && lli >= 0 && lli != 1);
             if (lane == 0) {
                 s_mask[0] = m0;
                 s_mask[1] = m1;
@@ -242,7 +258,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         if (wv == 0 && lane < WPB) {
             int dmode = 0;
             double dz = 0.0, du = 0.0, dl = 0.0;
-            if (lane < cnt && P.ext_mult > 0 && P.cut) accept_inputs(sa, wme, dmode, dz, du, dl);
+            if (lane < cnt && (!eager || s_eli[lane] >= 0) && P.ext_mult > 0 && P.cut)
+                accept_inputs(sa, wme, dmode, dz, du, dl);
             s_dmode[lane] = dmode;
             s_acc[0][lane] = dz;
             s_acc[1][lane] = du;
@@ -293,14 +310,15 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
             const int amw = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);  // directions a live walker still needs
             if (amw == 0) break;
-            if (eager && rf == 1) {
-                // eager_kernel ran pass 1 of every walker beside the likelihood kernel: once its
-                // walker's group has flagged both directions done (write-through values), each
-                // combiner lane takes pass 1's chi2, estimate and encounter flag, and its step-doubling
-                // change against the main pass's RV (P.rvp), which pass 1's RV then replaces there
+            if (eager && rf <= P.eager_passes) {
+                // eager_kernel ran passes 1 and 2 of every walker beside the likelihood kernel: once
+                // the group has flagged pass rf done in the directions its open walkers need
+                // (write-through values), each combiner lane takes that pass's chi2, estimate and
+                // encounter flag, and its step-doubling change against the previous pass's RV
+                // (P.rvp: the main pass's, then pass 1's), which this pass's RV then replaces there
                 if (wv == 0) {
                     const bool mine0 = lane < WPB && ((mk0 >> lane) & 1), mine1 = lane < WPB && ((mk1 >> lane) & 1);
-                    gu64* f0 = (gu64*)(P.eflag + (size_t)(wme / WPB) * 4 + 1);
+                    gu64* f0 = ef + 2 + 2 * (rf - 1);
                     SpinClock clk;
                     clk.restart();
                     bool ok = true;
@@ -329,7 +347,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                             const double* b_rv = b_dir + Eb;
                             const double* b_s2 = b_dir + 2 * Eb;
                             const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-                            gu64* cur = (gu64*)(P.rve + (size_t)d3 * plane + wme);
+                            gu64* cur = (gu64*)(P.rve + ((size_t)(rf - 1) * 2 + d3) * plane + wme);
                             double* prv = P.rvp + (size_t)d3 * plane + wme;
                             double d2 = 0.0;
                             for (int e = 0; e < Eb; e++) {
@@ -340,7 +358,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                                 d2 += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
                                 prv[(size_t)e * P.lvx_stride] = rvx;
                             }
-                            gu64* es = (gu64*)(P.esum + (size_t)d3 * 3 * P.lvx_stride + wme);
+                            gu64* es = (gu64*)(P.esum + ((size_t)(rf - 1) * 2 + d3) * 3 * P.lvx_stride + wme);
                             auto ld = [&](size_t o) {
                                 return __longlong_as_double((long long)__hip_atomic_load(es + o, __ATOMIC_RELAXED,
                                                                                          __HIP_MEMORY_SCOPE_AGENT));
@@ -357,7 +375,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             const int am = own < 0 ? amw : (amw & (1 << own));  // the ones this workgroup integrates
             // sub-passes: both directions at once (up to four levels), else one after the other;
             // none when a split task's own direction is done (the partner's pass only)
-            const int nsub = (am == 0 || (eager && rf == 1)) ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
+            const int nsub = (am == 0 || (eager && rf <= P.eager_passes)) ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
             for (int sp = 0; sp < nsub; sp++) {
                 // this wave's (direction, level) task, or none
                 const bool both = am == 3 && nl <= 4;
@@ -683,6 +701,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 }
             }
             __syncthreads();
+            if (eager && rf == 1 && threadIdx.x == 0 && (s_mask[0] | s_mask[1]) == 0)
+                __hip_atomic_store(ef + 1, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (pass 2 unneeded)
             if (team && tm == 0) {
                 // team A ends after pass 1; it finishes the group only when no walker is left for B
                 finisher = own <= 0 && (s_mask[0] | s_mask[1]) == 0;
@@ -692,7 +712,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         if (team && tm == 1) finisher = own <= 0 && !cancelled;
         // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h;
         // a split group's by its forward-direction workgroup, of team A or B)
-        if (finisher && wv == 0 && lane < WPB && lane < cnt) {
+        if (finisher && wv == 0 && lane < WPB && lane < cnt && (!eager || s_eli[lane] >= 0)) {
             int k2 = 0, wk2 = wme, j2 = 0, jp2 = 0;
             double z2 = 0.0, zp2 = 0.0;
             if (stretch) stretch_slot(sa, wme, k2, wk2, z2, j2, zp2, jp2);
@@ -705,16 +725,17 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     }
 }
 
-// Eager first halving pass (round 4): for a plain launch of few walkers (SMALA's centres, the
-// scalar State API), pass 1 of EVERY walker runs on the plan's side stream at the same time as the
-// likelihood kernel, on CUs the launch leaves idle.  It stores each walker-direction's chi2,
-// estimate, encounter flag and RV per epoch write-through, then a per-(group, direction) flag
-// tagged with the launch generation; the refinement kernel waits only for the groups its walkers
-// are in and replays pass 1 for them instead of integrating it after the likelihood kernel (the
-// same decisions and bits), and at its start cancels every other group (a flag the blocks check
-// before reading their walkers and once per epoch).  Grid: (groups of WPB walkers) x 2
-// directions, four waves per block (one per level).  P.eflag [groups][4]: [0] cancel tag
-// (generation << 8 | 1), [1 + d] direction d done (generation).
+// Eager halving passes (round 4): for a plain launch of 32..512 walkers (SMALA's centres),
+// passes 1 and 2 of EVERY walker run on the plan's side stream at the same time as the likelihood
+// kernel, on CUs the launch leaves idle.  Each stores its walker-directions' chi2, estimate,
+// encounter flag and RV per epoch write-through, then a per-(group, pass, direction) flag tagged
+// with the launch generation.  The refinement kernel, one task per group, cancels a group none of
+// whose walkers it holds, waits by flag for the passes its open walkers need and replays them
+// instead of integrating them after the likelihood kernel (the same decisions and bits), and
+// cancels pass 2 when pass 1 settles the group (flags the blocks check before reading their walkers
+// and once per epoch).  Grid: (groups of WPB walkers) x 2 directions x 2 passes, four waves per
+// block (one per level).  P.eflag [groups][8]: [0] cancel the group, [1] cancel its pass 2
+// (generation << 8 | 1), [2 + 2 (rf - 1) + d] pass rf done in direction d (generation).
 template <int NP, bool D3>
 __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W, const double* __restrict__ params,
                                                     const double hill_factor, const unsigned long long gen) {
@@ -727,15 +748,20 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     const int slot = lane / L;
     const int pl_idx = lane % L;
     const int nl = P.n_levels;
-    const int g = blockIdx.x >> 1, dd = blockIdx.x & 1;
+    const int np2 = P.eager_passes == 2;  // (blocks per group: 2 directions x eager_passes)
+    const int g = blockIdx.x >> (1 + np2), dd = (blockIdx.x >> np2) & 1, rf = 1 + (np2 & blockIdx.x);
     const DirSched& SR = dd ? P.bwd : P.fwd;
     const int Er = SR.n_epochs;
     __shared__ double s_rv[2][RVM_MAX_LEVELS][64];
     __shared__ int s_enc[RVM_MAX_LEVELS][64];
     __shared__ int s_cancel[2];
-    gu64* cflag = (gu64*)(P.eflag + (size_t)g * 4);
+    gu64* cflag = (gu64*)(P.eflag + (size_t)g * 8);  // [0] cancel the group, [1] cancel its pass 2
     const unsigned long long ctag = (gen << 8) | 1ull;
-    if (threadIdx.x == 0) s_cancel[0] = __hip_atomic_load(cflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag;
+    auto cancelled_now = [&]() {
+        return __hip_atomic_load(cflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag ||
+               (rf == 2 && __hip_atomic_load(cflag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag);
+    };
+    if (threadIdx.x == 0) s_cancel[0] = cancelled_now();
     __syncthreads();
     if (s_cancel[0]) return;  // (before the walkers are read: the caller may be done with them)
     const int w0 = g * WPB;
@@ -753,12 +779,12 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     const bool work = k >= 0;
     KickPrep<NP> kq{};
     if (work && Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
-    const int m_r = P.mult[k_u] << 1;
+    const int m_r = P.mult[k_u] << rf;
     const int nt_r = P.nt[k_u];
-    const double sc = ldexp(P.inv_mult[k_u], -1);
+    const double sc = ldexp(P.inv_mult[k_u], -rf);
     const bool cmb = work && k == 0 && lane < WPB && w0 + lane < W;
     const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-    gu64* rvo = (gu64*)(P.rve + (size_t)dd * plane + (cmb ? w0 + lane : 0));
+    gu64* rvo = (gu64*)(P.rve + ((size_t)(rf - 1) * 2 + dd) * plane + (cmb ? w0 + lane : 0));
     double c2 = 0.0, e2 = 0.0;
     bool cancelled = false;
     for (int e = 0; e < Er; e++) {
@@ -768,8 +794,7 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
             const double v0 = star_vx<NP, L>(s);
             if (pl_idx == 0) s_rv[e & 1][k_u][slot] = v0;
         }
-        if (wv == 0 && lane == 0)
-            s_cancel[e & 1] = __hip_atomic_load(cflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag;
+        if (wv == 0 && lane == 0) s_cancel[e & 1] = cancelled_now();
         __syncthreads();
         if (s_cancel[e & 1]) {
             cancelled = true;
@@ -794,7 +819,7 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
         if (cmb) {
             int er = 0;
             for (int q = 0; q < nl; q++) er |= s_enc[q][lane];
-            gu64* es = (gu64*)(P.esum + (size_t)dd * 3 * P.lvx_stride + w0 + lane);
+            gu64* es = (gu64*)(P.esum + ((size_t)(rf - 1) * 2 + dd) * 3 * P.lvx_stride + w0 + lane);
             auto bits = [](double v) { return (unsigned long long)__double_as_longlong(v); };
             __hip_atomic_store(es, bits(c2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(es + P.lvx_stride, bits(e2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -803,8 +828,7 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0)
-            __hip_atomic_store((gu64*)(P.eflag + (size_t)g * 4 + 1 + dd), gen, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(cflag + 2 + 2 * (rf - 1) + dd, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -813,7 +837,7 @@ static hipError_t launch_eager_t(const DevPlan& P, int W, const double* params, 
                                  unsigned long long gen, hipStream_t st) {
     constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
     const int groups = (W + wpb - 1) / wpb;
-    eager_kernel<NPV, D3V><<<dim3(2 * groups), dim3(256), 0, st>>>(P, W, params, hill_factor, gen);
+    eager_kernel<NPV, D3V><<<dim3(2 * P.eager_passes * groups), dim3(256), 0, st>>>(P, W, params, hill_factor, gen);
     return hipGetLastError();
 }
 

@@ -426,30 +426,32 @@ def test_certain_reject_can_be_switched_off():
     assert f["refined"] > 0 and f["truncated"] == 0 and f["unresolved"] == 0, f
 
 
-@pytest.mark.parametrize("W", [32, 256, 512])
-def test_eager_halving_passes_bit_identical(W):
-    """Plain launches of few walkers run the first two halving passes of every walker beside the
-    likelihood kernel (rvm_refine.hip eager_kernel) and the refinement kernel replays them: the same
-    logL, status bits and plan counters as the refinement kernel integrating them after the
-    likelihood kernel (RVM_EAGER=0), on wide-ball walkers (extensions, one- and two-pass walkers,
-    deeper ones, encounters, prior rejections)."""
+@pytest.mark.parametrize("W,passes", [(32, "1"), (256, "1"), (512, "1"), (32, "2"), (256, "2")])
+def test_eager_halving_passes_bit_identical(W, passes):
+    """Plain launches of few walkers run the first halving pass (RVM_EAGER_PASSES=2: the first two)
+    of every walker beside the likelihood kernel (rvm_refine.hip eager_kernel) and the refinement
+    kernel replays them: the same logL, status bits and plan counters as the refinement kernel
+    integrating them after the likelihood kernel (RVM_EAGER=0), on wide-ball walkers (extensions,
+    one- and two-pass walkers, deeper ones, encounters, prior rejections)."""
     import os
 
     obs = s2_obs_oracle()
     X = wide_walkers(W, ball=0.3, seed=5)
     res = []
     for env in ("1", "0"):
-        old = os.environ.get("RVM_EAGER")
+        old = {k: os.environ.get(k) for k in ("RVM_EAGER", "RVM_EAGER_PASSES")}
         os.environ["RVM_EAGER"] = env
+        os.environ["RVM_EAGER_PASSES"] = passes
         try:
             plan, _, _ = _plan(obs, W)
             got, st = _run(plan, X)
             res.append((got, st, plan.faults(reset=True)))
         finally:
-            if old is None:
-                os.environ.pop("RVM_EAGER", None)
-            else:
-                os.environ["RVM_EAGER"] = old
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
     np.testing.assert_array_equal(res[0][1], res[1][1])
     np.testing.assert_array_equal(res[0][0], res[1][0])
     assert res[0][2] == res[1][2], (res[0][2], res[1][2])
