@@ -339,6 +339,23 @@ int rvm_smala_derive_accept(int32_t n_params, int32_t n_chains, int64_t chain_be
                             double npoints_norm, double alpha, double eps, const rvm_smala_cache* cur,
                             const rvm_smala_cache* prop, uint64_t seed, uint64_t iteration, const double* draws,
                             int32_t* accepted, int32_t* failures, void* stream);
+/* The fused step with the centres' logp on a second (adaptive) plan, launched on another stream
+ * (mcmc.py:167-187; the reference's logp is IAS15's):
+ *   rvm_smala_derive_sides    rvm_smala_derive of x* without the stencil's centre row (its status and
+ *                             logp are not read): gradient, Hessian, metric, drift, Cholesky into prop,
+ *                             on the stencil's stream while the centres' launch still runs
+ *   rvm_smala_center_accept   prop's logp from lp_center, prop ok only if status_center is 0, then
+ *                             rvm_smala_accept, once the centres' launch is done
+ * bit-identical to copying the centres' logp / status into the stencil's row 0 and calling
+ * rvm_smala_derive_accept (the other cache entries do not depend on that row). */
+int rvm_smala_derive_sides(int32_t n_params, int32_t n_chains, int32_t n_obs, const double* x, double rel_step,
+                           const double* floor_, const double* lp_stencil, const int32_t* status_stencil,
+                           const double* rv_stencil, const double* inv_sigma2, double npoints_norm, double alpha,
+                           double eps, const rvm_smala_cache* out, void* stream);
+int rvm_smala_center_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const double* x_prop,
+                            const double* lp_center, const int32_t* status_center, const rvm_smala_cache* cur,
+                            const rvm_smala_cache* prop, double eps, uint64_t seed, uint64_t iteration,
+                            const double* draws, int32_t* accepted, int32_t* failures, void* stream);
 int rvm_smala_metric_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const double* x_prop,
                             const double* lp, const int32_t* status, const double* grad, const double* hess,
                             double alpha, double eps, const rvm_smala_cache* cur, const rvm_smala_cache* prop,

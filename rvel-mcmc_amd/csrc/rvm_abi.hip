@@ -48,7 +48,12 @@ hipError_t launch_stretch_iteration_end(const IterEndArgs& g, hipStream_t st);
 hipError_t launch_fd_params(int P, int n, const double* x, double rel, const double* fl, double* out, hipStream_t st);
 hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,
                                const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
-                               double npoints, double alpha, double eps, const SmalaCache& out, hipStream_t st);
+                               double npoints, double alpha, double eps, const SmalaCache& out, int sides,
+                               hipStream_t st);
+hipError_t launch_smala_center_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
+                                      const SmalaCache& prop, const double* lpc, const int32_t* stc, double eps,
+                                      uint64_t seed, uint64_t it, const double* draws, int32_t* accepted,
+                                      int32_t* failures, hipStream_t st);
 hipError_t launch_smala_metric(int P, int C, const double* x, const double* lp, const int32_t* status,
                                const double* grad, const double* hess, double alpha, double eps, const SmalaCache& out,
                                hipStream_t st);
@@ -951,8 +956,37 @@ int rvm_smala_derive(int32_t n_params, int32_t n_chains, int32_t n_obs, const do
         return fail(-1, "rvm_smala_derive: bad arguments");
     hipError_t e = rvm::launch_smala_derive(n_params, n_chains, n_obs, x, rel_step, floor_, lp_stencil,
                                             status_stencil, rv_stencil, inv_sigma2, npoints_norm, alpha, eps,
-                                            smala_cache(out), (hipStream_t)stream);
+                                            smala_cache(out), 0, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_derive");
+}
+
+int rvm_smala_derive_sides(int32_t n_params, int32_t n_chains, int32_t n_obs, const double* x, double rel_step,
+                           const double* floor_, const double* lp_stencil, const int32_t* status_stencil,
+                           const double* rv_stencil, const double* inv_sigma2, double npoints_norm, double alpha,
+                           double eps, const rvm_smala_cache* out, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || n_obs < 0 || !x || !floor_ ||
+        !lp_stencil || !status_stencil || (n_obs > 0 && (!rv_stencil || !inv_sigma2)) || !smala_cache_ok(out) ||
+        !(rel_step > 0.0) || !(npoints_norm != 0.0) || !(alpha > 0.0))
+        return fail(-1, "rvm_smala_derive_sides: bad arguments");
+    hipError_t e = rvm::launch_smala_derive(n_params, n_chains, n_obs, x, rel_step, floor_, lp_stencil,
+                                            status_stencil, rv_stencil, inv_sigma2, npoints_norm, alpha, eps,
+                                            smala_cache(out), 1, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_derive_sides");
+}
+
+int rvm_smala_center_accept(int32_t n_params, int32_t n_chains, int64_t chain_begin, double* x, const double* x_prop,
+                            const double* lp_center, const int32_t* status_center, const rvm_smala_cache* cur,
+                            const rvm_smala_cache* prop, double eps, uint64_t seed, uint64_t iteration,
+                            const double* draws, int32_t* accepted, int32_t* failures, void* stream) {
+    if (n_chains == 0) return 0;
+    if (n_params < 1 || n_params > RVM_SMALA_MAX_PARAMS || n_chains < 0 || !x || !x_prop || !lp_center ||
+        !status_center || !smala_cache_ok(cur) || !smala_cache_ok(prop))
+        return fail(-1, "rvm_smala_center_accept: bad arguments");
+    hipError_t e = rvm::launch_smala_center_accept(n_params, n_chains, chain_begin, x, smala_cache(cur), x_prop,
+                                                   smala_cache(prop), lp_center, status_center, eps, seed, iteration,
+                                                   draws, accepted, failures, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "rvm_smala_center_accept");
 }
 
 int rvm_smala_metric(int32_t n_params, int32_t n_chains, const double* x, const double* lp, const int32_t* status,

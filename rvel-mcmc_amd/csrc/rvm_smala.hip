@@ -213,7 +213,7 @@ __device__ __forceinline__ void smala_derive_chain(int P, int C, int E, const do
                                                    const double* __restrict__ fl, const double* __restrict__ lp_st,
                                                    const int32_t* __restrict__ st_st, const double* __restrict__ rv,
                                                    const double* __restrict__ w, double npoints, double alpha,
-                                                   double eps, const SmalaCache& out) {
+                                                   double eps, const SmalaCache& out, bool sides = false) {
     constexpr int PM = RVM_SMALA_MAX_PARAMS;
     constexpr int NTRI = PM * (PM + 1) / 2;        // upper-triangle entries
     constexpr int PER_LANE = (NTRI + 63) / 64;     // accumulators per lane
@@ -231,7 +231,9 @@ __device__ __forceinline__ void smala_derive_chain(int P, int C, int E, const do
     const int ntri = P * (P + 1) / 2;
     if (lane == 0) okflag = 1;
     __syncthreads();
-    for (int s = lane; s < S; s += 64)
+    // (sides: the centre row's status and logp are not read -- rvm_smala_center_accept brings the
+    // centre's own, the only things of the cache that depend on them)
+    for (int s = lane + (sides ? 1 : 0); s < S; s += 64)
         if (st_st[(size_t)s * C + c] != 0) okflag = 0;
     // realised steps exactly as rvm_fd_params formed the stencil; gradient
     if (lane < P) {
@@ -294,7 +296,8 @@ __device__ __forceinline__ void smala_derive_chain(int P, int C, int E, const do
             A[tq[j] * P + tp[j]] = a;
         }
     }
-    smala_metric_stage(P, C, c, lane, A, Qm, gr, xv, lt, inv, ra, rb, dn, rp, okflag, lp_st[c], alpha, eps, out);
+    smala_metric_stage(P, C, c, lane, A, Qm, gr, xv, lt, inv, ra, rb, dn, rp, okflag, sides ? 0.0 : lp_st[c], alpha,
+                       eps, out);
 }
 
 __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, const double* __restrict__ x,
@@ -303,8 +306,8 @@ __global__ __launch_bounds__(64) void smala_derive_kernel(int P, int C, int E, c
                                                           const int32_t* __restrict__ st_st,
                                                           const double* __restrict__ rv,
                                                           const double* __restrict__ w, double npoints,
-                                                          double alpha, double eps, SmalaCache out) {
-    smala_derive_chain(P, C, E, x, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, out);
+                                                          double alpha, double eps, SmalaCache out, int sides) {
+    smala_derive_chain(P, C, E, x, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, out, sides != 0);
 }
 
 // rvm_smala_metric: the same metric pipeline from exact derivatives (rvm_logl_derivs)
@@ -476,6 +479,26 @@ __global__ __launch_bounds__(64) void smala_derive_accept_kernel(
     smala_accept_chain(P, C, begin, x, cur, xs, prop, eps, seed, iteration, draws, accepted, failures);
 }
 
+// The accept after rvm_smala_derive_sides (rvm_smala_center_accept): the centre's own logp and status
+// (the adaptive plan's, on its side stream) complete the proposal's cache -- its logp, and ok only if
+// the centre's status is -- then the accept, as smala_derive_accept_kernel after the whole stencil.
+__global__ __launch_bounds__(64) void smala_center_accept_kernel(int P, int C, int64_t begin, double* __restrict__ x,
+                                                                 SmalaCache cur, const double* __restrict__ xs,
+                                                                 SmalaCache prop, const double* __restrict__ lpc,
+                                                                 const int32_t* __restrict__ stc, double eps,
+                                                                 uint64_t seed, uint64_t iteration,
+                                                                 const double* __restrict__ draws,
+                                                                 int32_t* __restrict__ accepted,
+                                                                 int32_t* __restrict__ failures) {
+    const int c = blockIdx.x;
+    if (threadIdx.x == 0) {
+        prop.lp[c] = lpc[c];
+        if (stc[c] != 0) prop.ok[c] = 0;
+    }
+    __syncthreads();
+    smala_accept_chain(P, C, begin, x, cur, xs, prop, eps, seed, iteration, draws, accepted, failures);
+}
+
 __global__ __launch_bounds__(64) void smala_metric_accept_kernel(
     int P, int C, const double* __restrict__ xs, const double* __restrict__ lp, const int32_t* __restrict__ status,
     const double* __restrict__ grad, const double* __restrict__ hess, double alpha, double eps, SmalaCache prop,
@@ -515,8 +538,18 @@ hipError_t launch_smala_metric(int P, int C, const double* x, const double* lp, 
 
 hipError_t launch_smala_derive(int P, int C, int E, const double* x, double rel, const double* fl,
                                const double* lp_st, const int32_t* st_st, const double* rv, const double* w,
-                               double npoints, double alpha, double eps, const SmalaCache& out, hipStream_t st) {
-    smala_derive_kernel<<<C, 64, 0, st>>>(P, C, E, x, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, out);
+                               double npoints, double alpha, double eps, const SmalaCache& out, int sides,
+                               hipStream_t st) {
+    smala_derive_kernel<<<C, 64, 0, st>>>(P, C, E, x, rel, fl, lp_st, st_st, rv, w, npoints, alpha, eps, out, sides);
+    return hipGetLastError();
+}
+
+hipError_t launch_smala_center_accept(int P, int C, int64_t begin, double* x, const SmalaCache& cur, const double* xs,
+                                      const SmalaCache& prop, const double* lpc, const int32_t* stc, double eps,
+                                      uint64_t seed, uint64_t it, const double* draws, int32_t* accepted,
+                                      int32_t* failures, hipStream_t st) {
+    smala_center_accept_kernel<<<C, 64, 0, st>>>(P, C, begin, x, cur, xs, prop, lpc, stc, eps, seed, it, draws, accepted,
+                                                 failures);
     return hipGetLastError();
 }
 

@@ -73,6 +73,11 @@ SIGNATURES = {
     "rvm_smala_derive_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, C.c_int32, _dp, _dp, C.c_double, _dp, _dp,
                                           _dp, _dp, _dp, C.c_double, C.c_double, C.c_double, C.POINTER(SmalaCache),
                                           C.POINTER(SmalaCache), C.c_uint64, C.c_uint64, _dp, _dp, _dp, _dp]),
+    "rvm_smala_derive_sides": (C.c_int, [C.c_int32, C.c_int32, C.c_int32, _dp, C.c_double, _dp, _dp, _dp, _dp, _dp,
+                                         C.c_double, C.c_double, C.c_double, C.POINTER(SmalaCache), _dp]),
+    "rvm_smala_center_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, _dp, _dp, _dp, C.POINTER(SmalaCache),
+                                          C.POINTER(SmalaCache), C.c_double, C.c_uint64, C.c_uint64, _dp, _dp, _dp,
+                                          _dp]),
     "rvm_smala_metric_accept": (C.c_int, [C.c_int32, C.c_int32, C.c_int64, _dp, _dp, _dp, _dp, _dp, _dp, C.c_double,
                                           C.c_double, C.POINTER(SmalaCache), C.POINTER(SmalaCache), C.c_uint64,
                                           C.c_uint64, _dp, _dp, _dp, _dp]),

@@ -201,11 +201,12 @@ class SmalaChains:
     def _center_logl(self, X, lp, st):
         self._center_join(self._center_start(X), lp, st)
 
-    def _stencil_logl(self, X, fused=True):
+    def _stencil_logl(self, X, fused=True, join=True):
         """logp, status [(2P+1) C] and model RVs [n_obs][(2P+1) C] over the central-difference
         stencil of X: one launch that forms the stencil in the likelihood kernel's prologue
         (rvm_smala_stencil_logl), or rvm_fd_params + rvm_logl_batch (fused=False; same bits), both
-        on the fixed-step plan (_fixed_plan); the centres' logp then from the adaptive plan."""
+        on the fixed-step plan (_fixed_plan); the centres' logp then from the adaptive plan
+        (join=False, fused only: not copied in; returned as the pending launch, or None)."""
         torch = _torch()
         S = 2 * self.P + 1
         plan = self._fixed_plan(S * self.n)
@@ -228,6 +229,8 @@ class SmalaChains:
                                                        lp.data_ptr(), st.data_ptr(), rv.data_ptr(),
                                                        _lib.stream_handle()), "rvm_smala_stencil_logl")
         self._plan_keep = plan  # the launch's plan stays alive with the sampler
+        if not join:
+            return lp, st, rv, pending
         self._center_join(pending, lp, st)
         return lp, st, rv
 
@@ -276,8 +279,9 @@ class SmalaChains:
 
         fused=True (default): three launches -- rvm_smala_propose, the stencil likelihood launch
         (rvm_smala_stencil_logl; exact: rvm_logl_derivs) and rvm_smala_derive_accept
-        (rvm_smala_metric_accept); fused=False runs the separate fd / logl / derive / accept
-        launches (bit-identical; 256 chains: 523k vs 485k chain-steps/s fused vs separate,
+        (rvm_smala_metric_accept) -- with the centres on the adaptive plan, rvm_smala_derive_sides
+        beside the centres' launch and rvm_smala_center_accept after it; fused=False runs the separate
+        fd / logl / derive / accept launches (bit-identical; 256 chains: 523k vs 485k chain-steps/s fused vs separate,
         profiles/r02h_configs.jsonl).  The plan is looked up per step for the current stream
         (State._plan -> engine.plan_for), so any stream is safe."""
         st_h = _lib.stream_handle()
@@ -307,7 +311,28 @@ class SmalaChains:
             self._periodic_faults()
             return
         if fused:
-            lp, st, rv = self._stencil_logl(self.Xs)
+            lp, st, rv, pending = self._stencil_logl(self.Xs, join=False)
+            if pending is not None:
+                # the proposal's derivatives and metric from the stencil's sides while the centres'
+                # adaptive launch (and its halving passes) still runs on the side stream; the accept
+                # once it is done, with the centres' own logp and status (no copies; same bits)
+                torch = _torch()
+                _lib.check(self.lib.rvm_smala_derive_sides(
+                    self.P, self.n, self.n_obs, self.Xs.data_ptr(), self.rel_step, self.floor.data_ptr(),
+                    lp.data_ptr(), st.data_ptr(), rv.data_ptr(), self.inv_sigma2.data_ptr(),
+                    float(self.obs.Npoints), self.alpha, self.eps, prop, st_h), "rvm_smala_derive_sides")
+                lpc, stc, done = pending
+                main = torch.cuda.current_stream(self.device)
+                main.wait_event(done)
+                _lib.check(self.lib.rvm_smala_center_accept(
+                    self.P, self.n, 0, self.X.data_ptr(), self.Xs.data_ptr(), lpc.data_ptr(), stc.data_ptr(), cur,
+                    prop, self.eps, self.seed, self.iteration, up, self.accepted.data_ptr(),
+                    self.failures.data_ptr(), st_h), "rvm_smala_center_accept")
+                lpc.record_stream(main)  # (allocated on the side stream, last read on this one)
+                stc.record_stream(main)
+                self.iteration += 1
+                self._periodic_faults()
+                return
             _lib.check(self.lib.rvm_smala_derive_accept(
                 self.P, self.n, 0, self.n_obs, self.X.data_ptr(), self.Xs.data_ptr(), self.rel_step,
                 self.floor.data_ptr(), lp.data_ptr(), st.data_ptr(), rv.data_ptr(), self.inv_sigma2.data_ptr(),

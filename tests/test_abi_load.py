@@ -19,7 +19,7 @@ def test_header_declares_expected_surface():
     fns = header_functions()
     for f in ("rvm_plan_create", "rvm_logl_batch", "rvm_stretch_propose", "rvm_stretch_accept",
               "rvm_mh_propose", "rvm_mh_accept", "rvm_fd_params", "rvm_smala_derive", "rvm_smala_propose",
-              "rvm_smala_accept", "rvm_stretch_half_step", "rvm_stretch_iteration_begin",
+              "rvm_smala_accept", "rvm_smala_derive_sides", "rvm_smala_center_accept", "rvm_stretch_half_step", "rvm_stretch_iteration_begin",
               "rvm_stretch_iteration_end", "rvm_logl_derivs", "rvm_logl_derivs_workspace_bytes", "rvm_smala_metric",
               "rvm_last_error", "rvm_abi_version"):
         assert f in fns
