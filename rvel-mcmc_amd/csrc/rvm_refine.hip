@@ -538,9 +538,12 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     } else if ((f & 0xFF) == 2) {
                         if (lane == 0) s_cancel[0] = 1;  // (A finished the group after all)
                     } else if (lane < WPB) {
-                        auto ld = [&](int row) {
-                            return __hip_atomic_load(tpub + row * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        };
+                        // (every row's load in flight before the first LDS store)
+                        unsigned long long row_v[15];
+#pragma unroll
+                        for (int rw = 0; rw < 15; rw++)
+                            row_v[rw] = __hip_atomic_load(tpub + rw * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        auto ld = [&](int row) { return row_v[row]; };
                         s_live[lane] = (int)ld(0);
                         s_stw[lane] = (int)ld(1);
                         s_lpw[lane] = __longlong_as_double((long long)ld(2));
@@ -575,12 +578,26 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                         const double* b_s2 = b_dir + 2 * Eb;
                         const size_t off = (size_t)d3 * P.lvx_emax * P.lvx_stride + wme;
                         double d2b = 0.0;
-                        for (int e = 0; e < Eb; e++) {
-                            const double pv = __longlong_as_double((long long)__hip_atomic_load(
-                                (gu64*)(P.rvp + off + (size_t)e * P.lvx_stride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                            const double rvx = P.rvp2[off + (size_t)e * P.lvx_stride];
-                            const double r = rvx - b_rv[e];
-                            d2b += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
+                        constexpr int RCH = 16;  // (epochs' loads in flight at once, as the eager replay)
+                        for (int e0 = 0; e0 < Eb; e0 += RCH) {
+                            double pvc[RCH], rvc[RCH];
+#pragma unroll
+                            for (int j = 0; j < RCH; j++) {
+                                const int e = e0 + j < Eb ? e0 + j : Eb - 1;
+                                pvc[j] = __longlong_as_double((long long)__hip_atomic_load(
+                                    (gu64*)(P.rvp + off + (size_t)e * P.lvx_stride), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT));
+                                rvc[j] = P.rvp2[off + (size_t)e * P.lvx_stride];
+                            }
+#pragma unroll
+                            for (int j = 0; j < RCH; j++) {
+                                const int e = e0 + j;
+                                if (e < Eb) {
+                                    const double pv = pvc[j], rvx = rvc[j];
+                                    const double r = rvx - b_rv[e];
+                                    d2b += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
+                                }
+                            }
                         }
                         pass_result(d3, 2, s_tc2[d3][lane], s_te2[d3][lane], d2b, s_ter[d3][lane]);
                     }
