@@ -27,9 +27,14 @@
  * Conventions
  *   - All array pointers passed to launch functions are DEVICE pointers (hipMalloc / torch CUDA
  *     tensors), caller-owned.  Launch functions never allocate, never synchronise, and are
- *     stream-ordered on `stream` (a hipStream_t; NULL = the null stream), so they are capturable
- *     into a hipGraph.  rvm_plan_create is the only call that allocates (device buffers owned by
- *     the plan) and it synchronises once.
+ *     stream-ordered on `stream` (a hipStream_t; NULL = the null stream): everything a launch
+ *     enqueues is complete once `stream` is -- including the eager halving pass a plain launch of
+ *     32..512 walkers runs on the plan's own side stream, which is forked from `stream` and joined
+ *     back into it within the launch -- so inputs may be reused right after `stream` is synchronised.
+ *     They are capturable into a hipGraph: no host-side state changes per launch (the launch
+ *     generation that tags the kernels' hand-off flags advances on the device) and kernel
+ *     attributes are set by rvm_plan_create.  rvm_plan_create is the only call that allocates
+ *     (device buffers owned by the plan) and it synchronises once.
  *   - A plan is single-stream: it owns per-launch workspace (the direction-exchange slots and the
  *     level-split hand-off slots, left empty by every completed launch), so launches that use one plan must be
  *     serialised on one stream at a time.  Concurrent launches on two streams need two plans (the
@@ -52,13 +57,14 @@
 extern "C" {
 #endif
 
-#define RVM_ABI_VERSION 11
+#define RVM_ABI_VERSION 12
 
 /* per-walker status codes (status_out) */
 #define RVM_STATUS_OK 0
 #define RVM_STATUS_PRIOR 1     /* State.priorHard() true (state.py:299-315) -> logl = -inf        */
 #define RVM_STATUS_ENCOUNTER 2 /* pair distance < exit_min_distance (REBOUND Encounter) -> -inf   */
-#define RVM_STATUS_NONFINITE 3 /* non-finite chi2, or a level-split hand-off that gave up -> -inf     */
+#define RVM_STATUS_NONFINITE 3 /* non-finite chi2 (a main pass that blows up is refined; a halving pass
+                                  that blows up ends the walker), or a hand-off that gave up -> -inf */
 #define RVM_STATUS_UNRESOLVED 4 /* adaptive resolution: the extrapolation-error estimate still above
                                    rvm_config.resolve_tol after resolve_max refinements -> -inf      */
 

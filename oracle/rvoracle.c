@@ -1023,7 +1023,8 @@ void rvo_logl_whx_seq_batch(int W, int np, const double* pl, int has_hk, int has
 /* direction's chi2 := its lb): rejected whatever further passes would give.                    */
 /* ecc_guard > 0: a walker with a planet of e > ecc_guard counts as open after the main pass     */
 /* whatever its estimate (it gets the extension; the estimate under-reads there).               */
-/* A non-finite pass (the fixed step blowing up on an extreme orbit) counts as open (lb 0).     */
+/* A non-finite main pass or extension (the fixed step blowing up on an extreme orbit) counts as   */
+/* open (lb 0); a non-finite halving pass ends the walker NONFINITE (round 5).                    */
 /* ------------------------------------------------------------------------------------------ */
 enum { RVO_UNRESOLVED = 4 };
 #ifndef EXT_ACCEPT /* (overridable for studies of the rule: -DEXT_ACCEPT=...) */
@@ -1181,10 +1182,9 @@ static void dir_halve(const rvo_plan_ctx* X, rvo_dir* D, int rf) {
         D->open = 0;
         return;
     }
-    if (st != RVO_OK) { /* a non-finite pass refines on */
-        D->chi2 = D->est = D->est_raw = NAN;
-        D->lb = 0.0;
-        for (int i = 0; i < D->cnt; i++) D->prev[i] = NAN;
+    if (st != RVO_OK) { /* a non-finite halving pass ends the walker (round 5, ADVICE r4: refining on */
+        D->st = RVO_NONFINITE; /* would run the last pass at 2^rf_max x the base steps) */
+        D->open = 0;
         return;
     }
     double c2 = 0.0, e2 = 0.0, d2 = 0.0;
@@ -1200,8 +1200,13 @@ static void dir_halve(const rvo_plan_ctx* X, rvo_dir* D, int rf) {
     D->chi2 = c2;
     D->est_raw = e2;
     D->est = e2 / X->npoints;
-    if (margin_of(D->est, X->tol_dir) < D->margin) D->margin = margin_of(D->est, X->tol_dir);
     const int fin = isfinite(c2) && isfinite(e2);
+    if (!fin) { /* (finite RVs whose sums overflow: non-finite all the same) */
+        D->st = RVO_NONFINITE;
+        D->open = 0;
+        return;
+    }
+    if (margin_of(D->est, X->tol_dir) < D->margin) D->margin = margin_of(D->est, X->tol_dir);
     const int stall = fin && rf >= 2 && !(D->est < 0.5 * D->pest);
     if (fin && rf >= 2 && D->best <= FLOOR_BOUND * X->tol_dir && D->est > X->tol_dir &&
         margin_of(D->est, 0.5 * D->pest) < D->margin)
@@ -1244,6 +1249,10 @@ static int walker_cut(const rvo_plan_ctx* X, rvo_dir* D, const rvo_decide* dc) {
 }
 
 static int any_enc(const rvo_dir* D) { return D[0].st == RVO_ENCOUNTER || D[1].st == RVO_ENCOUNTER; }
+/* a direction whose halving pass ended the walker: an encounter or a non-finite pass */
+static int any_end(const rvo_dir* D) {
+    return any_enc(D) || D[0].st == RVO_NONFINITE || D[1].st == RVO_NONFINITE;
+}
 static int any_open(const rvo_dir* D) { return D[0].open || D[1].open; }
 
 /* logp with adaptive resolution: rf_used[2] / est[2] (fwd, bwd) report the stage reached (0 the
@@ -1353,9 +1362,9 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
                 break;
             }
             rf++;
-            for (int dir = 0; dir < 2 && !any_enc(D); dir++)
+            for (int dir = 0; dir < 2 && !any_end(D); dir++)
                 if (D[dir].open) dir_halve(&X, &D[dir], rf);
-            if (any_enc(D)) break;
+            if (any_end(D)) break;
         }
     }
     for (int dir = 0; dir < 2; dir++) {

@@ -30,10 +30,11 @@ namespace rvm {
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
                        double* logl, int32_t* status, double* rv_out, const StretchArgs& sa, hipStream_t stream);
 hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen, int eager,
-                         hipStream_t stream);
-hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long gen,
-                        hipStream_t stream);
+                         int32_t* status, double* rv_out, const StretchArgs& sa, int eager, hipStream_t stream);
+hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t stream);
+hipError_t launch_gen_bump(const DevPlan& P, hipStream_t stream);
+hipError_t prepare_logl(const DevPlan& P);
+hipError_t prepare_refine(const DevPlan& P);
 hipError_t launch_stretch_propose(int P, int n0, int64_t s0b, const double* x, int n1, const double* c, double a,
                                   uint64_t seed, uint64_t it, uint32_t half, const double* draws, double* q,
                                   double* z, hipStream_t st);
@@ -91,38 +92,49 @@ struct rvm_plan {
     // `cap` launches (the kernels' own durations on their stream, for the bench's roofline)
     mutable std::vector<hipEvent_t> tev;
     mutable int32_t tcap = 0, tn = 0;
-    mutable unsigned long long gen = 0;  // refinement launches so far (the split exchange's flag tag)
     void* emem = nullptr;                // eager passes' results (DevPlan::rve, esum), small plans
     hipStream_t side = nullptr;          // their stream, forked from and joined to the caller's
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 // One likelihood evaluation as every entry point runs it: the likelihood kernel, then (adaptive
-// plans) the refinement kernel for the walkers it handed on, stream-ordered.
+// plans) the refinement kernel for the walkers it handed on, stream-ordered.  Everything it enqueues
+// is complete when the caller's stream is (the header's conventions): an eager launch forks the
+// plan's side stream from the caller's and joins it back after the refinement kernel, which by then
+// has stopped every eager block it did not wait for (rvm_refine.hip).  No host-side state changes
+// per launch -- the launch generation lives on the device -- so a captured hipGraph replays it.
 static hipError_t run_logl(const rvm_plan* plan, int W, const double* params, double hill_factor, double* logl,
                            int32_t* status, double* rv_out, const rvm::StretchArgs& sa, hipStream_t st) {
     const bool tm = plan->tn < plan->tcap;
-    // eager halving passes 1 and 2 (rvm_refine.hip): plain launches of few walkers, no RV curve wanted;
-    // on the plan's side stream, forked from the caller's (it reads the walkers), never joined: the
-    // refinement kernel waits for the groups it needs by their flags and cancels the others
+    // eager halving passes (rvm_refine.hip): plain launches of 32..512 walkers, no RV curve wanted
     const bool mapped = sa.c != nullptr || sa.mh_scale != nullptr || sa.fd_x != nullptr;
-    const int eager = plan->emem != nullptr && !mapped && rv_out == nullptr && params != nullptr &&
+    const int eager = plan->side != nullptr && !mapped && rv_out == nullptr && params != nullptr &&
                       W >= rvm::RVM_EAGER_MIN && W <= plan->dev.eager_max;
-    const unsigned long long gen = ++plan->gen;  // (the launch generation: flags of both kernels)
     hipError_t e = hipSuccess;
     if (eager) {
         e = hipEventRecord(plan->ev_fork, st);
         if (e == hipSuccess) e = hipStreamWaitEvent(plan->side, plan->ev_fork, 0);
-        if (e == hipSuccess) e = rvm::launch_eager(plan->dev, W, params, hill_factor, gen, plan->side);
-        if (e != hipSuccess) return e;
+        if (e == hipSuccess) e = rvm::launch_eager(plan->dev, W, params, hill_factor, plan->side);
+        if (e != hipSuccess) {
+            // (join whatever was enqueued on the side stream before reporting)
+            if (hipEventRecord(plan->ev_join, plan->side) == hipSuccess) (void)hipStreamWaitEvent(st, plan->ev_join, 0);
+            return e;
+        }
     }
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn], st);
     e = rvm::launch_logl(plan->dev, W, params, hill_factor, plan->slots, logl, status, rv_out, sa, st);
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 1], st);
-    if (e == hipSuccess)
-        e = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, gen, eager, st);
+    // (the refinement kernel runs even after a failed likelihood launch: it resets the work lists)
+    const hipError_t er = rvm::launch_refine(plan->dev, W, params, hill_factor, logl, status, rv_out, sa, eager, st);
+    if (e == hipSuccess) e = er;
     if (tm) (void)hipEventRecord(plan->tev[3 * plan->tn + 2], st);
     if (tm) plan->tn++;
+    if (eager) {
+        hipError_t ej = hipEventRecord(plan->ev_join, plan->side);
+        if (ej == hipSuccess) ej = hipStreamWaitEvent(st, plan->ev_join, 0);
+        if (ej == hipSuccess) ej = rvm::launch_gen_bump(plan->dev, st);
+        if (e == hipSuccess) e = ej;
+    }
     return e;
 }
 
@@ -469,6 +481,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.rq_xgroups = 0;
     P.rq_t = nullptr;
     P.rq_tf = nullptr;
+    P.gen_dev = nullptr;
     if (P.rmax > 0) {
         // (+ the split exchange: flags and double-buffered values per both-direction group of up to 64
         // walkers and team; groups of 16 walkers at 3-4 planets; + team A's published state and flag)
@@ -479,7 +492,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const size_t b_tf = (size_t)xg * sizeof(unsigned long long);
         const size_t b_c = 2 * (size_t)max_walkers * sizeof(double);
         const size_t b_w = 3 * (size_t)max_walkers * sizeof(int32_t);
-        const size_t b_all = b_x + b_xf + b_t + b_tf + b_c + b_w + 64;
+        const size_t b_all = b_x + b_xf + b_t + b_tf + b_c + b_w + 64;  // (+ rq_n [4] and the launch generation)
         if (hipMalloc(&plan->rqmem, b_all) != hipSuccess || hipMemset(plan->rqmem, 0, b_all) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
@@ -494,6 +507,13 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.rq_c = reinterpret_cast<double*>(base + b_x + b_xf + b_t + b_tf);
         P.rq_w = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c);
         P.rq_n = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w);
+        P.gen_dev = reinterpret_cast<unsigned long long*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w + 32);
+        const unsigned long long gen1 = 1;  // (every flag word starts at generation 0)
+        if (hipMemcpy(P.gen_dev, &gen1, sizeof(gen1), hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipGetLastError();
+            rvm_plan_destroy(plan);
+            return fail(-3, "rvm_plan_create: initialising the launch generation failed");
+        }
         P.rq_cap = max_walkers;
         P.rq_xgroups = (int32_t)xg;
         if (const char* sp = getenv("RVM_REFINE_SPLIT"))  // (A/B knob: 0 keeps both directions in one block)
@@ -501,17 +521,20 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         if (const char* tp = getenv("RVM_REFINE_TEAMS"))  // (A/B knob: 0 runs the passes one after the other)
             if (tp[0] == '0') P.rq_t = nullptr;
     }
-    // eager halving passes for the plan's small plain launches (SMALA's centres, the scalar State
-    // API): results of passes 1 and 2 of up to RVM_EAGER_MAX walkers, a side stream and two events
-    // (any failure: no eager passes, the refinement kernel integrates as usual)
+    // eager halving passes for the plan's plain launches of RVM_EAGER_MIN..RVM_EAGER_MAX walkers
+    // (SMALA's centres, batched State evaluations): results of passes 1 and 2, a side stream and two
+    // events -- only for plans that can make such a launch (a one-walker scalar plan never does, and
+    // its stream would only add to the hardware queues).  Any failure: no eager passes,
+    // the refinement kernel integrates as usual.
     {
         const char* eg = getenv("RVM_EAGER");  // (A/B knob: 0 turns the eager pass off, 1 on)
         const bool eager_on = eg ? eg[0] == '1' : RVM_EAGER_DEFAULT;
         const int emw = std::min<int>(max_walkers, rvm::RVM_EAGER_MAX);
-        if (P.rmax >= 2 && P.rvp != nullptr && cfg->n_levels <= 4 && eager_on) {
+        if (P.rmax >= 2 && P.rvp != nullptr && P.gen_dev != nullptr && cfg->n_levels <= 4 && eager_on &&
+            max_walkers >= rvm::RVM_EAGER_MIN) {
             // passes 1 and 2: RV [2][2][emax][stride], sums [2][2][3][stride]; flags [groups][8] (zeroed)
             const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-            const size_t nflag = 8 * (size_t)((rvm::RVM_EAGER_MAX + 15) / 16) + 8;
+            const size_t nflag = rvm::RVM_EFLAG_WORDS * (size_t)((rvm::RVM_EAGER_MAX + 15) / 16) + 8;
             const size_t b = (4 * plane + 12 * (size_t)P.lvx_stride + nflag) * sizeof(double);
             if (hipMalloc(&plan->emem, b) == hipSuccess && hipMemset(plan->emem, 0, b) == hipSuccess &&
                 hipDeviceSynchronize() == hipSuccess &&
@@ -534,6 +557,17 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
                 plan->ev_fork = plan->ev_join = nullptr;
             }
         }
+    }
+    // kernel attributes (dynamic LDS) set once here, so launches stay capturable; a schedule the
+    // refinement kernel cannot stage is refused now rather than failing every launch
+    if (rvm::prepare_logl(P) != hipSuccess) {
+        rvm_plan_destroy(plan);
+        return fail(-1, "rvm_plan_create: n_planets has no kernel instantiation");
+    }
+    if (rvm::prepare_refine(P) != hipSuccess) {
+        rvm_plan_destroy(plan);
+        return fail(-1, "rvm_plan_create: the epoch schedule does not fit the refinement kernel's LDS "
+                        "(too many epochs in one direction for the adaptive resolution)");
     }
     *out = plan;
     return 0;

@@ -38,6 +38,8 @@ constexpr int RVM_EAGER_MAX = 512;
 // ... and at least this many (a launch of a few walkers rarely refines, and the fork costs the
 // scalar State API ~7 %: config 1, profiles/r04x_configs_eager_ab.jsonl)
 constexpr int RVM_EAGER_MIN = 32;
+// eflag words per eager group (rvm_refine.hip)
+constexpr int RVM_EFLAG_WORDS = 8;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
@@ -114,9 +116,17 @@ struct DevPlan {
     // their chi2, estimate and encounter flag
     double* rve;
     double* esum;
-    unsigned long long* eflag;  // [groups][8]: cancel tags, passes done per direction (rvm_refine.hip)
+    // [groups][8] (rvm_refine.hip): [0] cancel the group, [2 + 2 (rf - 1) + d] the claim word of
+    // pass rf in direction d (generation << 8 | 1 eager block running, 2 its results stored, 3 the
+    // refinement kernel integrates it itself), [6 + d] cancel direction d
+    unsigned long long* eflag;
     int32_t eager_max;
     int32_t eager_passes;  // (1 or 2: how many halving passes eager_kernel runs)
+    // the launch generation (device word, >= 1): the tag of the refinement kernel's exchange flags and
+    // the eager blocks' claim words.  Read on the device by both kernels and advanced on the device
+    // after every launch (the refinement kernel's last block, or gen_bump_kernel after an eager
+    // launch), so a launch sequence captured into a hipGraph tags every replay afresh.
+    unsigned long long* gen_dev;
     // plan-owned device counters (rvm_plan_faults): [0] level-split hand-offs given up (the
     // workspace is dirty until reset), [1] NONFINITE results, [2] UNRESOLVED results,
     // [3] walker-direction refinement passes (extension + halvings), [4] refinements cut short as

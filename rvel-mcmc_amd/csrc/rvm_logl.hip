@@ -627,10 +627,15 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 // to the refinement kernel: list 0 both directions open, 1 forward only, 2 backward only
                 const int li = of && ob ? 0 : (of ? 1 : 2);
                 const int ix = __hip_atomic_fetch_add(P.rq_n + li, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                P.rq_w[(size_t)li * P.rq_cap + ix] = wo;
-                P.rq_c[wo] = of ? 0.0 : cf;
-                P.rq_c[(size_t)P.rq_cap + wo] = ob ? 0.0 : cb;
-                return;
+                if (ix < P.rq_cap) {
+                    P.rq_w[(size_t)li * P.rq_cap + ix] = wo;
+                    P.rq_c[wo] = of ? 0.0 : cf;
+                    P.rq_c[(size_t)P.rq_cap + wo] = ob ? 0.0 : cb;
+                    return;
+                }
+                // (never past the lists: counts left over from a launch whose refinement kernel did
+                // not run make the walker a counted NONFINITE, not an out-of-bounds store)
+                stw = RVM_STATUS_NONFINITE;
             }
         }
         if (stw == RVM_STATUS_OK && !isfinite(lp0)) stw = RVM_STATUS_NONFINITE;
@@ -1282,6 +1287,33 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
                                                                     status, sa, nA, 8);
     }
     return hipGetLastError();
+}
+
+// rvm_plan_create: set the likelihood kernel's LDS attribute for the plan's instantiations once, so
+// that launches never change function attributes (they stay capturable into a hipGraph)
+hipError_t prepare_logl(const DevPlan& P) {
+    const bool inc = P.inclined != 0;
+#define RVM_PREP(NPV)                                                                      \
+    (inc ? (lds_budget<NPV, true, true>(), lds_budget<NPV, true, false>())                 \
+         : (lds_budget<NPV, false, true>(), lds_budget<NPV, false, false>()))
+    switch (P.n_planets) {
+        case 1:
+            (void)RVM_PREP(1);
+            break;
+        case 2:
+            (void)RVM_PREP(2);
+            break;
+        case 3:
+            (void)RVM_PREP(3);
+            break;
+        case 4:
+            (void)RVM_PREP(4);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef RVM_PREP
+    return hipSuccess;
 }
 
 // the likelihood kernel (main pass + extension); an adaptive plan's walkers it hands on are

@@ -56,12 +56,35 @@
 
 namespace rvm {
 
+// Claim word of one eager (pass, direction) item (DevPlan::eflag): set it to gen << 8 | code unless
+// this launch generation already holds it.  Returns whether the caller now owns the item.  The eager
+// block claims at its start (code 1), the refinement kernel when it needs the pass (code 3): whoever
+// comes second leaves the item to the first -- so the refinement kernel only ever waits on an eager
+// block that is already running, never on one that may not have been dispatched.
+__device__ __forceinline__ bool claim_item(gu64* w, unsigned long long gen, unsigned long long code) {
+    unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+        if ((v >> 8) == gen) return false;
+        unsigned long long expect = v;
+        if (__hip_atomic_compare_exchange_strong(w, &expect, (gen << 8) | code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return true;
+        v = expect;
+    }
+}
+
+// Bounded wait of a refinement pass's hand-off (split exchange, team B for team A): the partner
+// integrates a pass of 2^rf x the base steps without publishing progress, so the allowance scales
+// with the pass (a deep pass is no timeout; the timeout stays a last-resort fault)
+__device__ __forceinline__ unsigned long long pass_ticks(const DevPlan& P, int rf) {
+    return P.spin_ticks << (rf < RVM_RESOLVE_MAX_LIMIT ? rf : RVM_RESOLVE_MAX_LIMIT);
+}
+
 template <int NP, bool D3>
 __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int W, const double* __restrict__ params,
                                                      const double hill_factor, double* __restrict__ rv_out,
                                                      double* __restrict__ logl_out, int32_t* __restrict__ status_out,
-                                                     const StretchArgs sa, const unsigned long long gen,
-                                                     const int eager) {
+                                                     const StretchArgs sa, const int eager) {
     constexpr int L = LanesPerWalker<NP>::value;
     constexpr int WPB = 64 / L;
     constexpr int PR = D3 ? 7 : 5;
@@ -73,15 +96,22 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     const int nl = P.n_levels;
 
     // the list sizes are final (the likelihood kernel has ended); the last block to read them
-    // resets them for the plan's next launch
+    // resets them for the plan's next launch and (no eager blocks in this launch: they read the
+    // generation too) advances the launch generation -- every block has read it by then
     __shared__ int s_n[3];
+    __shared__ unsigned long long s_gen;
     if (threadIdx.x == 0) {
         for (int i = 0; i < 3; i++) s_n[i] = __hip_atomic_load(P.rq_n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long g0 = __hip_atomic_load(P.gen_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_gen = g0;
         const int done = __hip_atomic_fetch_add(P.rq_n + 3, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == (int)gridDim.x - 1)
+        if (done == (int)gridDim.x - 1) {
             for (int i = 0; i < 4; i++) __hip_atomic_store(P.rq_n + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!eager) __hip_atomic_store(P.gen_dev, g0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     __syncthreads();
+    const unsigned long long gen = s_gen;
     const int nq[3] = {s_n[0], s_n[1], s_n[2]};
     const int gq0 = (nq[0] + WPB - 1) / WPB, gq1 = (nq[1] + WPB - 1) / WPB, gq2 = (nq[2] + WPB - 1) / WPB;
     const int ng = gq0 + gq1 + gq2;
@@ -114,7 +144,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     __shared__ double s_init[8][64];
     __shared__ double s_chi[2][64], s_lb[2][64];
     __shared__ double s_pest[2][64], s_best[2][64], s_bchi[2][64];  // previous / best estimate, best chi2
-    __shared__ int s_open[2][64];  // 1 open, 0 settled, 2 encounter
+    __shared__ int s_open[2][64];  // 1 open, 0 settled, 2 encounter, 3 non-finite pass
     __shared__ int s_live[64];     // the walker is still refining
     __shared__ int s_stw[64];      // its final status and logl (finished after the passes)
     __shared__ double s_lpw[64];
@@ -130,6 +160,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     // eager tasks: the group's walker indices and each slot's list (-1: not listed, the likelihood
     // kernel finished it), and whether any slot is listed
     __shared__ int s_eitems[64], s_eli[64], s_eany;
+    __shared__ int s_emask;  // (eager) directions of the current pass an eager block runs
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     for (int dd = 0; dd < 2; dd++) {
         const DirSched& SD = dd ? P.bwd : P.fwd;
@@ -274,11 +305,17 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         gu64* tflag = team ? (gu64*)(P.rq_tf + g) : nullptr;
         bool cancelled = false;  // (team B: A finished the group)
         // a pass's outcome for direction dd of walker slot `lane` (its combiner lane): encounter,
+        // non-finite (the walker ends NONFINITE: a halving pass that blows up is not refined further,
+        // oracle/rvoracle.c dir_halve -- the last pass would run 2^rmax x the base steps),
         // settled (estimate within the bound), settled at the roundoff floor, or still open with the
         // pass's lower bound on its chi2
         auto pass_result = [&](const int dd, const int rfp, const double c2, const double e2, const double d2,
                                const int er) __attribute__((always_inline)) {
             const bool fin = isfinite(c2) && isfinite(e2);
+            if (!er && !fin) {
+                s_open[dd][lane] = 3;
+                return;
+            }
             const double en = e2 / P.npoints;
             // (the roundoff floor: this pass's estimate no longer falls; the best pass's estimate is
             // e2 / npoints units too)
@@ -310,87 +347,31 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
             const int amw = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);  // directions a live walker still needs
             if (amw == 0) break;
-            if (eager && rf <= P.eager_passes) {
-                // eager_kernel ran passes 1 and 2 of every walker beside the likelihood kernel: once
-                // the group has flagged pass rf done in the directions its open walkers need
-                // (write-through values), each combiner lane takes that pass's chi2, estimate and
-                // encounter flag, and its step-doubling change against the previous pass's RV
-                // (P.rvp: the main pass's, then pass 1's), which this pass's RV then replaces there
-                if (wv == 0) {
-                    const bool mine0 = lane < WPB && ((mk0 >> lane) & 1), mine1 = lane < WPB && ((mk1 >> lane) & 1);
-                    gu64* f0 = ef + 2 + 2 * (rf - 1);
-                    SpinClock clk;
-                    clk.restart();
-                    bool ok = true;
-                    for (;;) {
-                        const bool rdy = (!mine0 || __hip_atomic_load(f0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen) &&
-                                         (!mine1 || __hip_atomic_load(f0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen);
-                        if (ballot(!rdy) == 0) break;
-                        if (clk.expired(P.spin_ticks)) {
-                            ok = false;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
+            int emask = 0;  // (eager) the directions whose pass rf an eager block runs: replayed below
+            if (eager) {
+                // eager_kernel's blocks of directions no open walker needs stop (every pass), and each
+                // pass it runs is claimed per needed direction: a direction whose eager block has
+                // started is left to it (its stored results are replayed after this workgroup's own
+                // sub-passes), any other one this workgroup integrates itself -- it never waits on a
+                // block that may not have been dispatched
+                if (threadIdx.x == 0) {
+                    int em = 0;
+                    for (int d3 = 0; d3 < 2; d3++) {
+                        if (!((amw >> d3) & 1))
+                            __hip_atomic_store(ef + 6 + d3, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        else if (rf <= P.eager_passes && !claim_item(ef + 2 + 2 * (rf - 1) + d3, gen, 3ull))
+                            em |= 1 << d3;
                     }
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    if (!ok) {
-                        if (lane == 0) {
-                            s_xfault = 1;
-                            __hip_atomic_fetch_add(P.counters, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                    } else {
-                        for (int d3 = 0; d3 < 2; d3++) {
-                            if (!(d3 ? mine1 : mine0)) continue;
-                            const DirSched& SB = d3 ? P.bwd : P.fwd;
-                            const int Eb = SB.n_epochs;
-                            const double* b_dir = s_sched + (size_t)d3 * 4 * emax;
-                            const double* b_rv = b_dir + Eb;
-                            const double* b_s2 = b_dir + 2 * Eb;
-                            const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
-                            gu64* cur = (gu64*)(P.rve + ((size_t)(rf - 1) * 2 + d3) * plane + wme);
-                            double* prv = P.rvp + (size_t)d3 * plane + wme;
-                            double d2 = 0.0;
-                            // (RCH epochs' loads in flight at once: one epoch at a time, each store
-                            // waiting for its load, cost ~0.4 us per epoch on the step's critical path)
-                            constexpr int RCH = 16;
-                            for (int e0 = 0; e0 < Eb; e0 += RCH) {
-                                double rvc[RCH], pvc[RCH];
-#pragma unroll
-                                for (int j = 0; j < RCH; j++) {
-                                    const int e = e0 + j < Eb ? e0 + j : Eb - 1;
-                                    rvc[j] = __longlong_as_double((long long)__hip_atomic_load(
-                                        cur + (size_t)e * P.lvx_stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                                    pvc[j] = prv[(size_t)e * P.lvx_stride];
-                                }
-#pragma unroll
-                                for (int j = 0; j < RCH; j++) {
-                                    const int e = e0 + j;
-                                    if (e < Eb) {
-                                        const double rvx = rvc[j], pv = pvc[j];
-                                        const double r = rvx - b_rv[e];
-                                        d2 += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
-                                        prv[(size_t)e * P.lvx_stride] = rvx;
-                                    }
-                                }
-                            }
-                            gu64* es = (gu64*)(P.esum + ((size_t)(rf - 1) * 2 + d3) * 3 * P.lvx_stride + wme);
-                            auto ld = [&](size_t o) {
-                                return __longlong_as_double((long long)__hip_atomic_load(es + o, __ATOMIC_RELAXED,
-                                                                                         __HIP_MEMORY_SCOPE_AGENT));
-                            };
-                            pass_result(d3, rf, ld(0), ld(P.lvx_stride), d2, (int)ld(2 * (size_t)P.lvx_stride));
-                        }
-                    }
+                    s_emask = em;
                 }
-                if (wv == 0 && lane == 0) {
-                    const unsigned long long nd = __builtin_popcountll(mk0) + __builtin_popcountll(mk1);
-                    if (nd) __hip_atomic_fetch_add(P.counters + 3, nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+                __syncthreads();
+                emask = s_emask;
             }
-            const int am = own < 0 ? amw : (amw & (1 << own));  // the ones this workgroup integrates
+            // the ones this workgroup integrates
+            const int am = (own < 0 ? amw : (amw & (1 << own))) & ~emask;
             // sub-passes: both directions at once (up to four levels), else one after the other;
             // none when a split task's own direction is done (the partner's pass only)
-            const int nsub = (am == 0 || (eager && rf <= P.eager_passes)) ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
+            const int nsub = am == 0 ? 0 : ((am == 3 && nl > 4) ? 2 : 1);
             for (int sp = 0; sp < nsub; sp++) {
                 // this wave's (direction, level) task, or none
                 const bool both = am == 3 && nl <= 4;
@@ -512,6 +493,84 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             }
             if (cancelled) break;  // (team B: team A finished the group; every wave saw the same flag)
             __syncthreads();
+            if (emask != 0 && wv == 0) {
+                // the eager-run directions: once their blocks have stored pass rf (write-through values,
+                // then the claim word = gen << 8 | 2), each combiner lane takes that pass's chi2,
+                // estimate and encounter flag, and its step-doubling change against the previous pass's
+                // RV (P.rvp: the main pass's, then pass 1's), which this pass's RV then replaces there
+                const bool mine0 = (emask & 1) && lane < WPB && ((mk0 >> lane) & 1);
+                const bool mine1 = (emask & 2) && lane < WPB && ((mk1 >> lane) & 1);
+                gu64* f0 = ef + 2 + 2 * (rf - 1);
+                const unsigned long long done = (gen << 8) | 2ull;
+                SpinClock clk;
+                clk.restart();
+                bool ok = true;
+                for (;;) {
+                    const bool rdy = (!mine0 || __hip_atomic_load(f0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == done) &&
+                                     (!mine1 || __hip_atomic_load(f0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == done);
+                    if (ballot(!rdy) == 0) break;
+                    // (a claimed block is running: the wait ends; the allowance is a last-resort fault)
+                    if (clk.expired(pass_ticks(P, rf))) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (!ok) {
+                    if (lane == 0) {
+                        s_xfault = 1;
+                        __hip_atomic_fetch_add(P.counters, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                } else {
+                    for (int d3 = 0; d3 < 2; d3++) {
+                        if (!(d3 ? mine1 : mine0)) continue;
+                        const DirSched& SB = d3 ? P.bwd : P.fwd;
+                        const int Eb = SB.n_epochs;
+                        const double* b_dir = s_sched + (size_t)d3 * 4 * emax;
+                        const double* b_rv = b_dir + Eb;
+                        const double* b_s2 = b_dir + 2 * Eb;
+                        const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
+                        gu64* cur = (gu64*)(P.rve + ((size_t)(rf - 1) * 2 + d3) * plane + wme);
+                        double* prv = P.rvp + (size_t)d3 * plane + wme;
+                        double d2 = 0.0;
+                        // (RCH epochs' loads in flight at once: one epoch at a time, each store
+                        // waiting for its load, cost ~0.4 us per epoch on the step's critical path)
+                        constexpr int RCH = 16;
+                        for (int e0 = 0; e0 < Eb; e0 += RCH) {
+                            double rvc[RCH], pvc[RCH];
+#pragma unroll
+                            for (int j = 0; j < RCH; j++) {
+                                const int e = e0 + j < Eb ? e0 + j : Eb - 1;
+                                rvc[j] = __longlong_as_double((long long)__hip_atomic_load(
+                                    cur + (size_t)e * P.lvx_stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                                pvc[j] = prv[(size_t)e * P.lvx_stride];
+                            }
+#pragma unroll
+                            for (int j = 0; j < RCH; j++) {
+                                const int e = e0 + j;
+                                if (e < Eb) {
+                                    const double rvx = rvc[j], pv = pvc[j];
+                                    const double r = rvx - b_rv[e];
+                                    d2 += fabs((rvx - pv) * (r + (pv - b_rv[e]))) / b_s2[e];
+                                    prv[(size_t)e * P.lvx_stride] = rvx;
+                                }
+                            }
+                        }
+                        gu64* es = (gu64*)(P.esum + ((size_t)(rf - 1) * 2 + d3) * 3 * P.lvx_stride + wme);
+                        auto ld = [&](size_t o) {
+                            return __longlong_as_double((long long)__hip_atomic_load(es + o, __ATOMIC_RELAXED,
+                                                                                     __HIP_MEMORY_SCOPE_AGENT));
+                        };
+                        pass_result(d3, rf, ld(0), ld(P.lvx_stride), d2, (int)ld(2 * (size_t)P.lvx_stride));
+                    }
+                }
+                if (lane == 0) {
+                    const unsigned long long nd = ((emask & 1) ? __builtin_popcountll(mk0) : 0) +
+                                                  ((emask & 2) ? __builtin_popcountll(mk1) : 0);
+                    __hip_atomic_fetch_add(P.counters + 3, nd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
             if (bfirst) {
                 // team B: team A's state after pass 1 (wave 0; the flag is in by now unless A is
                 // late), then this pass's results for the walkers still open
@@ -521,7 +580,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     unsigned long long f = 0;
                     bool ok = true;
                     while (((f = __hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 8) != gen) {
-                        if (clk.expired(P.spin_ticks)) {
+                        if (clk.expired(pass_ticks(P, 1))) {
                             ok = false;
                             break;
                         }
@@ -621,7 +680,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 if (lane < WPB) {
                     const int o = s_open[own][lane];
                     const unsigned long long b =
-                        o == 2 ? slot_status(RVM_STATUS_ENCOUNTER)
+                        o >= 2 ? slot_status(o == 2 ? RVM_STATUS_ENCOUNTER : RVM_STATUS_NONFINITE)
                                : (unsigned long long)__double_as_longlong(o == 1 ? -s_lb[own][lane] : s_chi[own][lane]);
                     __hip_atomic_store(mine + lane, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
@@ -635,7 +694,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 clk.restart();
                 bool ok = true;
                 while (__hip_atomic_load(tf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) {
-                    if (clk.expired(P.spin_ticks)) {
+                    if (clk.expired(pass_ticks(P, rf))) {
                         ok = false;
                         break;
                     }
@@ -652,7 +711,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     const unsigned long long b = __hip_atomic_load(theirs + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const int od = own ^ 1;
                     if (slot_is_status(b)) {
-                        s_open[od][lane] = 2;
+                        s_open[od][lane] = (b & 0xFF) == RVM_STATUS_NONFINITE ? 3 : 2;
                     } else {
                         const double v = __longlong_as_double((long long)b);
                         s_open[od][lane] = signbit(v) ? 1 : 0;
@@ -672,8 +731,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     bool done = true;
                     if (s_xfault) {
                         stw = RVM_STATUS_NONFINITE;
-                    } else if (of == 2 || ob == 2) {
-                        stw = RVM_STATUS_ENCOUNTER;
+                    } else if (of >= 2 || ob >= 2) {
+                        // (the forward direction's end first, as the oracle integrates it first)
+                        stw = (of >= 2 ? of : ob) == 2 ? RVM_STATUS_ENCOUNTER : RVM_STATUS_NONFINITE;
                     } else if (of == 0 && ob == 0) {
                         lp = -((s_chi[1][lane] + s_chi[0][lane]) / P.npoints);  // state.py:98, 109
                         if (!isfinite(lp)) stw = RVM_STATUS_NONFINITE;
@@ -733,8 +793,6 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 }
             }
             __syncthreads();
-            if (eager && rf == 1 && threadIdx.x == 0 && (s_mask[0] | s_mask[1]) == 0)
-                __hip_atomic_store(ef + 1, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (pass 2 unneeded)
             if (team && tm == 0) {
                 // team A ends after pass 1; it finishes the group only when no walker is left for B
                 finisher = own <= 0 && (s_mask[0] | s_mask[1]) == 0;
@@ -754,23 +812,30 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             const double lnp0 = (stretch && k2 == 0) || mh ? sa.lnp[wme] : 0.0;
             walker_out<R>(P, sa, wme, s_stw[lane], s_lpw[lane], logl_out, status_out, row, z2, u3, lnp0);
         }
+        // (eager) the group is done: any of its eager blocks still running stops at its next epoch
+        // (the caller's stream joins eager_kernel's after this kernel, rvm_abi.hip run_logl)
+        if (eager && threadIdx.x == 0)
+            __hip_atomic_store(ef, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-// Eager halving passes (round 4): for a plain launch of 32..512 walkers (SMALA's centres),
-// passes 1 and 2 of EVERY walker run on the plan's side stream at the same time as the likelihood
-// kernel, on CUs the launch leaves idle.  Each stores its walker-directions' chi2, estimate,
-// encounter flag and RV per epoch write-through, then a per-(group, pass, direction) flag tagged
-// with the launch generation.  The refinement kernel, one task per group, cancels a group none of
-// whose walkers it holds, waits by flag for the passes its open walkers need and replays them
-// instead of integrating them after the likelihood kernel (the same decisions and bits), and
-// cancels pass 2 when pass 1 settles the group (flags the blocks check before reading their walkers
-// and once per epoch).  Grid: (groups of WPB walkers) x 2 directions x 2 passes, four waves per
-// block (one per level).  P.eflag [groups][8]: [0] cancel the group, [1] cancel its pass 2
-// (generation << 8 | 1), [2 + 2 (rf - 1) + d] pass rf done in direction d (generation).
+// Eager halving passes (round 4): for a plain launch of 32..512 walkers (SMALA's centres, batched
+// State evaluations), halving pass 1 (and 2 with RVM_EAGER_PASSES=2) of EVERY walker runs on the
+// plan's side stream at the same time as the likelihood kernel, on CUs the launch leaves idle.
+// Grid: (groups of WPB walkers) x 2 directions x eager_passes, four waves per block (one per level).
+// A block first claims its (pass, direction) item of its group (DevPlan::eflag; claim_item) -- if the
+// refinement kernel has claimed it, that kernel integrates the pass itself and the block exits --
+// then stores its walker-directions' chi2, estimate, encounter flag and RV per epoch write-through,
+// and finally the claim word gen << 8 | 2.  The refinement kernel, one task per group, replays the
+// items it finds claimed by an eager block instead of integrating them (the same decisions and
+// bits), and stops every block it does not need: a group none of whose walkers it holds at once
+// (eflag[0]), the directions no open walker needs (eflag[6 + d]), and, when it has finished the
+// group, whatever of it still runs (eflag[0]) -- blocks check these before reading their walkers and
+// once per epoch.  run_logl joins the side stream back into the caller's after the refinement
+// kernel (rvm_abi.hip): the launch is complete, eager blocks included, when the caller's stream is.
 template <int NP, bool D3>
 __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W, const double* __restrict__ params,
-                                                    const double hill_factor, const unsigned long long gen) {
+                                                    const double hill_factor) {
     constexpr int L = LanesPerWalker<NP>::value;
     constexpr int WPB = 64 / L;
     constexpr int PR = D3 ? 7 : 5;
@@ -787,15 +852,20 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     __shared__ double s_rv[2][RVM_MAX_LEVELS][64];
     __shared__ int s_enc[RVM_MAX_LEVELS][64];
     __shared__ int s_cancel[2];
-    gu64* cflag = (gu64*)(P.eflag + (size_t)g * 8);  // [0] cancel the group, [1] cancel its pass 2
+    __shared__ unsigned long long s_gen;
+    gu64* ef = (gu64*)(P.eflag + (size_t)g * RVM_EFLAG_WORDS);
+    if (threadIdx.x == 0) s_gen = __hip_atomic_load(P.gen_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned long long gen = s_gen;
     const unsigned long long ctag = (gen << 8) | 1ull;
     auto cancelled_now = [&]() {
-        return __hip_atomic_load(cflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag ||
-               (rf == 2 && __hip_atomic_load(cflag + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag);
+        return __hip_atomic_load(ef, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag ||
+               __hip_atomic_load(ef + 6 + dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag;
     };
-    if (threadIdx.x == 0) s_cancel[0] = cancelled_now();
+    gu64* item = ef + 2 + 2 * (rf - 1) + dd;
+    if (threadIdx.x == 0) s_cancel[0] = cancelled_now() || !claim_item(item, gen, 1ull);
     __syncthreads();
-    if (s_cancel[0]) return;  // (before the walkers are read: the caller may be done with them)
+    if (s_cancel[0]) return;  // (before the walkers are read)
     const int w0 = g * WPB;
     const int wo = w0 + slot < W ? w0 + slot : w0;  // (lanes past the last walker repeat the group's first)
     double rowv[R];
@@ -859,51 +929,61 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_store(cflag + 2 + 2 * (rf - 1) + dd, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(item, (gen << 8) | 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-template <int NPV, bool D3V>
-static hipError_t launch_eager_t(const DevPlan& P, int W, const double* params, double hill_factor,
-                                 unsigned long long gen, hipStream_t st) {
-    constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
-    const int groups = (W + wpb - 1) / wpb;
-    eager_kernel<NPV, D3V><<<dim3(2 * P.eager_passes * groups), dim3(256), 0, st>>>(P, W, params, hill_factor, gen);
+// After an eager launch (run_logl, once the side stream has joined): the next launch generation
+// (the refinement kernel advances it itself when no eager blocks share its generation)
+__global__ void gen_bump_kernel(unsigned long long* gen_dev) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(gen_dev, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t launch_gen_bump(const DevPlan& P, hipStream_t stream) {
+    gen_bump_kernel<<<dim3(1), dim3(64), 0, stream>>>(P.gen_dev);
     return hipGetLastError();
 }
 
-hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long gen,
-                        hipStream_t stream) {
+template <int NPV, bool D3V>
+static hipError_t launch_eager_t(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t st) {
+    constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
+    const int groups = (W + wpb - 1) / wpb;
+    eager_kernel<NPV, D3V><<<dim3(2 * P.eager_passes * groups), dim3(256), 0, st>>>(P, W, params, hill_factor);
+    return hipGetLastError();
+}
+
+hipError_t launch_eager(const DevPlan& P, int W, const double* params, double hill_factor, hipStream_t stream) {
     const bool inc = P.inclined != 0;
     switch (P.n_planets) {
         case 1:
-            return inc ? launch_eager_t<1, true>(P, W, params, hill_factor, gen, stream)
-                       : launch_eager_t<1, false>(P, W, params, hill_factor, gen, stream);
+            return inc ? launch_eager_t<1, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<1, false>(P, W, params, hill_factor, stream);
         case 2:
-            return inc ? launch_eager_t<2, true>(P, W, params, hill_factor, gen, stream)
-                       : launch_eager_t<2, false>(P, W, params, hill_factor, gen, stream);
+            return inc ? launch_eager_t<2, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<2, false>(P, W, params, hill_factor, stream);
         case 3:
-            return inc ? launch_eager_t<3, true>(P, W, params, hill_factor, gen, stream)
-                       : launch_eager_t<3, false>(P, W, params, hill_factor, gen, stream);
+            return inc ? launch_eager_t<3, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<3, false>(P, W, params, hill_factor, stream);
         case 4:
-            return inc ? launch_eager_t<4, true>(P, W, params, hill_factor, gen, stream)
-                       : launch_eager_t<4, false>(P, W, params, hill_factor, gen, stream);
+            return inc ? launch_eager_t<4, true>(P, W, params, hill_factor, stream)
+                       : launch_eager_t<4, false>(P, W, params, hill_factor, stream);
         default:
             return hipErrorInvalidValue;
     }
 }
 
+// Dynamic-LDS budget of the refinement kernel on the current device (the CU's 160 KB less its static
+// LDS), with the attribute admitting it set once per device and instantiation.  rvm_plan_create
+// calls it (prepare_refine) so a launch never changes function attributes -- launches stay
+// capturable -- and a plan whose schedule would not fit is refused there, not at launch.
 template <int NPV, bool D3V>
-static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                                  int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen,
-                                  int eager, hipStream_t stream) {
-    constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
-    const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
-    const size_t smem = (size_t)emax * 8 * sizeof(double);
+static size_t refine_budget() {
     static size_t budget[64] = {};
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+        (void)hipGetLastError();
+        return 32 * 1024;
+    }
     if (budget[dev] == 0) {
         const void* f = reinterpret_cast<const void*>(&refine_kernel<NPV, D3V>);
         hipFuncAttributes fa{};
@@ -915,7 +995,18 @@ static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params,
         (void)hipGetLastError();
         budget[dev] = b;
     }
-    if (smem > budget[dev]) return hipErrorInvalidConfiguration;
+    return budget[dev];
+}
+
+template <int NPV, bool D3V>
+static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
+                                  int32_t* status, double* rv_out, const StretchArgs& sa, int eager,
+                                  hipStream_t stream) {
+    constexpr int wpb = 64 / LanesPerWalker<NPV>::value;
+    const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
+    const size_t smem = (size_t)emax * 8 * sizeof(double);
+    // (checked by rvm_plan_create: a launch that cannot run would leave the work lists' counts set)
+    if (smem > refine_budget<NPV, D3V>()) return hipErrorInvalidConfiguration;
     // every block reads the list sizes (the last one resets them): a grid of at most one block
     // per CU, and no more than the lists could fill
     // (an even count: a split group's two workgroups are 2j, 2j + 1)
@@ -923,31 +1014,44 @@ static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params,
     int nb = std::max(2, std::min(P.n_cu > 0 ? P.n_cu : 256, 2 * groups));
     nb &= ~1;
     refine_kernel<NPV, D3V><<<dim3(nb), dim3(512), smem, stream>>>(P, W, params, hill_factor, rv_out, logl, status, sa,
-                                                                   gen, eager);
+                                                                   eager);
     return hipGetLastError();
 }
 
+#define RVM_DISPATCH_NP(EXPR_T)                  \
+    switch (P.n_planets) {                       \
+        case 1:                                  \
+            return inc ? EXPR_T(1, true) : EXPR_T(1, false); \
+        case 2:                                  \
+            return inc ? EXPR_T(2, true) : EXPR_T(2, false); \
+        case 3:                                  \
+            return inc ? EXPR_T(3, true) : EXPR_T(3, false); \
+        case 4:                                  \
+            return inc ? EXPR_T(4, true) : EXPR_T(4, false); \
+        default:                                 \
+            return hipErrorInvalidValue;         \
+    }
+
 hipError_t launch_refine(const DevPlan& P, int W, const double* params, double hill_factor, double* logl,
-                         int32_t* status, double* rv_out, const StretchArgs& sa, unsigned long long gen, int eager,
-                         hipStream_t stream) {
+                         int32_t* status, double* rv_out, const StretchArgs& sa, int eager, hipStream_t stream) {
     if (P.rmax <= 0 || P.rq_n == nullptr) return hipSuccess;
     const bool inc = P.inclined != 0;
-#define RVM_LAUNCH_R(NPV)                                                                             \
-    (inc ? launch_refine_t<NPV, true>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, eager, stream) \
-         : launch_refine_t<NPV, false>(P, W, params, hill_factor, logl, status, rv_out, sa, gen, eager, stream))
-    switch (P.n_planets) {
-        case 1:
-            return RVM_LAUNCH_R(1);
-        case 2:
-            return RVM_LAUNCH_R(2);
-        case 3:
-            return RVM_LAUNCH_R(3);
-        case 4:
-            return RVM_LAUNCH_R(4);
-        default:
-            return hipErrorInvalidValue;
-    }
+#define RVM_LAUNCH_R(NPV, D3V) launch_refine_t<NPV, D3V>(P, W, params, hill_factor, logl, status, rv_out, sa, eager, stream)
+    RVM_DISPATCH_NP(RVM_LAUNCH_R)
 #undef RVM_LAUNCH_R
 }
+
+// rvm_plan_create: set the refinement kernel's LDS attribute for the plan's instantiation and check
+// that the plan's schedule fits it (hipErrorInvalidConfiguration otherwise)
+hipError_t prepare_refine(const DevPlan& P) {
+    if (P.rmax <= 0 || P.rq_n == nullptr) return hipSuccess;
+    const bool inc = P.inclined != 0;
+    const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
+    const size_t smem = (size_t)emax * 8 * sizeof(double);
+#define RVM_PREP_R(NPV, D3V) (smem <= refine_budget<NPV, D3V>() ? hipSuccess : hipErrorInvalidConfiguration)
+    RVM_DISPATCH_NP(RVM_PREP_R)
+#undef RVM_PREP_R
+}
+#undef RVM_DISPATCH_NP
 
 }  // namespace rvm

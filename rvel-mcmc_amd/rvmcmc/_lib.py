@@ -19,7 +19,7 @@ RVM_STATUS_UNRESOLVED = 4
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
 RVM_N_COUNTERS = 6  # rvm_plan_counters
-ABI_VERSION = 11  # include/rvmcmc.h RVM_ABI_VERSION
+ABI_VERSION = 12  # include/rvmcmc.h RVM_ABI_VERSION
 
 
 class RvmConfig(C.Structure):

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     lib = _lib.load()
     for f in header_functions():
         assert hasattr(lib, f), f"librvmcmc.so lacks {f}"
-    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 11
+    assert lib.rvm_abi_version() == _lib.ABI_VERSION == 12
 
 
 def test_python_binding_matches_header():
