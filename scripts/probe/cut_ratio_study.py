@@ -1,0 +1,134 @@
+"""Study (CPU, oracle): how far the main pass's extrapolation-error estimate can under-read its
+actual error against the reference physics, per direction, on stretch proposals formed from a
+chain's steady-state ensemble -- the quantity the certain-reject cut's lower bound rests on (an open
+direction's chi2 less min(d, RVM_CUT_EST_FACTOR = 100 x est); VERDICT r4
+"what's weak" 1).
+
+Per proposal and direction d (the observations with t >= 0, or t < 0, scored alone, npoints as the
+walker's): the main pass's logL term (plan step, levels 4..7, oracle.logl_whx_seq_batch), its
+estimate est_d (oracle.logl_whx_adapt_batch with resolve_max 0: the main pass's), IAS15's term;
+ratio = |logL_main - logL_ias15| / est_d over the directions whose error matters for the bound
+(> 1e-7, a tenth of T2).  Systems: S2 (scripts/probe/ens_it2000.npy), HD155358 and 3 planets
+(ens_hd155358_it1000.npy, ens_3planet_it1000.npy from scripts/dump_steady_ensembles.py).
+usage: cut_ratio_study.py [system ...] [--n N]  -> one JSON line per system."""
+import json
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [os.path.join(ROOT, d) for d in ("oracle", "rvel-mcmc_amd", "tests")]
+import oracle as O  # noqa: E402
+from conftest import S2_PLANETS, s2_obs_oracle  # noqa: E402
+
+THIRD = {"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}  # scripts/configs_bench.py config 5
+HD_SOL = [6.57730330e-01, -9.72263877e-02, -7.82798396e-02, 8.84031737e-04, 4.42804990e+00,
+          1.04404207e+00, -2.05622789e-02, -1.08797961e-01, 8.30379710e-04, 1.49919861e+00]
+
+
+def system(name):
+    """(planets, oracle observations, steady-state ensemble [W][5 np] in kernel row order m,a,h,k,l)."""
+    from rvmcmc.state import State
+
+    if name == "S2":
+        planets, obs, f = [dict(p) for p in S2_PLANETS], s2_obs_oracle(), "ens_it2000.npy"
+    elif name == "HD155358":
+        planets = [{"m": HD_SOL[3], "a": HD_SOL[0], "h": HD_SOL[1], "k": HD_SOL[2], "l": HD_SOL[4]},
+                   {"m": HD_SOL[8], "a": HD_SOL[5], "h": HD_SOL[6], "k": HD_SOL[7], "l": HD_SOL[9]}]
+        obs = O.obs_from_file(os.path.join(ROOT, "tests", "golden", "HD155358.vels"), Npoints=100)
+        f = "ens_hd155358_it1000.npy"
+    else:
+        np.random.seed(2017)
+        planets = [dict(p) for p in S2_PLANETS] + [dict(THIRD)]
+        obs = O.fake_obs(planets, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
+        f = "ens_3planet_it1000.npy"
+    E = np.load(os.path.join(ROOT, "scripts", "probe", f))
+    s = State(planets=[dict(p) for p in planets])
+    pm = s.param_map()
+    import torch
+
+    K = pm.to_kernel(torch.as_tensor(np.ascontiguousarray(E.T))).numpy().T  # [W][5 np]
+    return planets, obs, K
+
+
+def direction_obs(obs, d):
+    """The observations of one integration direction alone (d = 0: t >= 0, 1: t < 0), same Npoints."""
+    z = np.zeros(0)
+    if d == 0:
+        return O.OracleObs(tf=obs.tf, tb=z, rvf=obs.rvf, rvb=z, errorf=obs.errorf, errorb=z, Npoints=obs.Npoints,
+                           t=obs.tf, rv=obs.rvf, error=obs.errorf)
+    return O.OracleObs(tf=z, tb=obs.tb, rvf=z, rvb=obs.rvb, errorf=z, errorb=obs.errorb, Npoints=obs.Npoints,
+                       t=obs.tb, rv=obs.rvb, error=obs.errorb)
+
+
+def stretch_proposals(K, n, seed=7):
+    W = len(K)
+    rng = np.random.default_rng(seed)
+    X, C = K[:n], K[W // 2:W // 2 + n]
+    z = (rng.random(n) + 1.0) ** 2 / 2.0
+    j = rng.integers(0, n, n)
+    return C[j] - z[:, None] * (C[j] - X)
+
+
+def study(name, n=512, nt=None):
+    from rvmcmc import engine
+
+    planets, obs, K = system(name)
+    npl = len(planets)
+    cfg = engine.IntegratorConfig()
+    dt, mult, _ = cfg.plan_args(planets)
+    tol = cfg.resolve(planets)[0]
+    Q = stretch_proposals(K, min(n, len(K) // 2))
+    P = np.zeros((len(Q), npl, 7))
+    P[:, :, :5] = Q.reshape(-1, npl, 5)
+    nt = nt or os.cpu_count() or 8
+    idx = [ix for ix in np.array_split(np.arange(len(P)), nt) if len(ix)]
+
+    def par(fn):
+        with ThreadPoolExecutor(nt) as ex:
+            parts = list(ex.map(lambda ix: fn(P[ix]), idx))
+        return [np.concatenate([p[k] for p in parts]) for k in range(len(parts[0]))]
+
+    ratios, errs, ests = [], [], []
+    for d in (0, 1):
+        od = direction_obs(obs, d)
+        li, si = par(lambda p: O.logl_ias15_batch(p, npl, od, 1.0))
+        lm, sm = par(lambda p: O.logl_whx_seq_batch(p, npl, od, dt, mult, 1.0))
+        _, sa, _, est, _ = par(lambda p: O.logl_whx_adapt_batch(p, npl, od, dt, mult, tol, 0, 1.0))
+        ok = (si == 0) & (sm == 0) & np.isfinite(li) & np.isfinite(lm)
+        err = np.abs(lm - li)[ok]
+        e = est[ok, d]
+        errs.append(err)
+        ests.append(e)
+        m = err > 1e-7
+        ratios.append(err[m] / np.maximum(e[m], 1e-300))
+    r = np.concatenate(ratios)
+    err = np.concatenate(errs)
+    e = np.concatenate(ests)
+    out = {"system": name, "proposals": len(Q), "directions_ok": int(len(err)),
+           "directions_error_above_1e-7": int(len(r)),
+           "max_error_over_estimate": float(r.max()) if len(r) else None,
+           "p999_error_over_estimate": float(np.quantile(r, 0.999)) if len(r) else None,
+           "p99_error_over_estimate": float(np.quantile(r, 0.99)) if len(r) else None,
+           "directions_error_over_estimate_above_57": int((r > 57).sum()),
+           "directions_error_over_estimate_above_100": int((r > 100).sum()),
+           "max_abs_error": float(err.max()), "cut_est_factor": 100.0}
+    # where the estimate is the binding term of the bound: the error beyond 100 est (0 = the bound holds)
+    out["max_error_beyond_100_est"] = float(np.max(np.maximum(err - 100.0 * e, 0.0)))
+    return out
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    n = 512
+    if "--n" in sys.argv:
+        n = int(sys.argv[sys.argv.index("--n") + 1])
+        args = [a for a in args if a != str(n)]
+    for name in args or ["S2", "HD155358", "3-planet"]:
+        print(json.dumps(study(name, n)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
