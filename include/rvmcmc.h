@@ -67,6 +67,10 @@ extern "C" {
                                   that blows up ends the walker), or a hand-off that gave up -> -inf */
 #define RVM_STATUS_UNRESOLVED 4 /* adaptive resolution: the extrapolation-error estimate still above
                                    rvm_config.resolve_tol after resolve_max refinements -> -inf      */
+#define RVM_STATUS_SKIPPED 5    /* rvm_stretch_iteration_begin's status_spec only: a half-1 variant
+                                   slot whose partner's first-half decision (already final) rules it
+                                   out, not refined by the adaptive resolution; rvm_stretch_iteration_end
+                                   never reads it.  logl -inf                                          */
 
 #define RVM_MAX_PLANETS 4
 #define RVM_MAX_LEVELS 6
@@ -160,8 +164,9 @@ int rvm_plan_faults(rvm_plan* plan, int32_t reset, int64_t* handoff_timeouts, in
 /* All of a plan's counters as an array (the same reset): out[0..4] as rvm_plan_faults, out[5]
  * walker-directions the adaptive resolution settled at their roundoff floor (a halving pass whose
  * estimate no longer fell: the direction keeps its best pass, whose estimate was within
- * RVM_FLOOR_BOUND = 4 x the bound); entries past RVM_N_COUNTERS read 0. */
-#define RVM_N_COUNTERS 6
+ * RVM_FLOOR_BOUND = 4 x the bound), out[6] speculative variant slots skipped
+ * (RVM_STATUS_SKIPPED); entries past RVM_N_COUNTERS read 0. */
+#define RVM_N_COUNTERS 7
 int rvm_plan_counters(rvm_plan* plan, int32_t reset, int64_t* out, int32_t n, void* stream);
 /* Kernel timing (benchmarks): the plan's next max_launches likelihood evaluations (any entry point)
  * record HIP events on their stream around the likelihood kernel and around the refinement kernel

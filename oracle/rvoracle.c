@@ -1083,17 +1083,27 @@ static double lb_of(double chi2, double d, double est_raw) {
 
 /* stage 0: the plan's step */
 static void dir_main(const rvo_plan_ctx* X, rvo_dir* D) {
-    int st = RVO_OK;
+    int st = RVO_OK, coarse = 0;
+    int kf = 0; /* the finest level (largest multiplier) */
+    for (int k = 1; k < X->nl; k++)
+        if (X->mult[k] > X->mult[kf]) kf = k;
     for (int k = 0; k < X->nl; k++) {
         const int s = wh_direction(X->np, X->pl, X->hill_factor, D->at, D->cnt, D->sign, X->dt, X->mult[k],
                                    D->lv0 + (size_t)k * D->cnt);
+        /* (round 5) adaptive: an encounter only a coarser level sees does not end the walker -- the
+         * coarse levels' positions near a close approach are the least accurate -- the direction is
+         * refined instead, its main pass treated like a non-finite one (rvm_logl.hip `cenc`) */
+        if (s == RVO_ENCOUNTER && X->adaptive && k != kf) {
+            coarse = 1;
+            continue;
+        }
         if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
     }
     if (st == RVO_ENCOUNTER || (st != RVO_OK && !X->adaptive)) {
         D->st = st;
         return;
     }
-    D->bad = st != RVO_OK;
+    D->bad = st != RVO_OK || coarse;
     if (D->bad) {
         D->chi2 = D->est = D->est_raw = NAN;
         D->lb = 0.0;

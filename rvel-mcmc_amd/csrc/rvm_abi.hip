@@ -336,6 +336,9 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.lw3[k] = wk;
     }
     P.rtol_dir = cfg->resolve_tol > 0.0 && cfg->n_levels >= 2 ? 0.5 * cfg->resolve_tol : INFINITY;
+    P.fin_level = 0;
+    for (int k = 1; k < cfg->n_levels; k++)
+        if (mult[k] > mult[P.fin_level]) P.fin_level = k;
     P.rmax = P.rtol_dir < INFINITY ? rmax : 0;
     P.cut = 1;
     P.spin_ticks = 200000000ull;  // 2 s of the 100 MHz real-time counter without progress
@@ -482,6 +485,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.rq_t = nullptr;
     P.rq_tf = nullptr;
     P.gen_dev = nullptr;
+    P.rq_mark = nullptr;
     if (P.rmax > 0) {
         // (+ the split exchange: flags and double-buffered values per both-direction group of up to 64
         // walkers and team; groups of 16 walkers at 3-4 planets; + team A's published state and flag)
@@ -492,7 +496,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const size_t b_tf = (size_t)xg * sizeof(unsigned long long);
         const size_t b_c = 2 * (size_t)max_walkers * sizeof(double);
         const size_t b_w = 3 * (size_t)max_walkers * sizeof(int32_t);
-        const size_t b_all = b_x + b_xf + b_t + b_tf + b_c + b_w + 64;  // (+ rq_n [4] and the launch generation)
+        const size_t b_m = ((size_t)max_walkers * sizeof(int32_t) + 63) & ~(size_t)63;  // rq_mark
+        const size_t b_all = b_x + b_xf + b_t + b_tf + b_c + b_w + 64 + b_m;  // (+ rq_n [4], the launch generation)
         if (hipMalloc(&plan->rqmem, b_all) != hipSuccess || hipMemset(plan->rqmem, 0, b_all) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
@@ -508,6 +513,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.rq_w = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c);
         P.rq_n = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w);
         P.gen_dev = reinterpret_cast<unsigned long long*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w + 32);
+        P.rq_mark = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w + 64);  // (zeroed)
         const unsigned long long gen1 = 1;  // (every flag word starts at generation 0)
         if (hipMemcpy(P.gen_dev, &gen1, sizeof(gen1), hipMemcpyHostToDevice) != hipSuccess) {
             (void)hipGetLastError();

@@ -71,6 +71,12 @@ struct DevPlan {
     double lw3[RVM_MAX_LEVELS];
     double rtol_dir;   // +inf: no estimate check
     int32_t rmax;
+    // the finest level (largest multiplier) of the main pass: with the adaptive resolution on, an
+    // encounter the main pass sees only on coarser levels does not end the walker -- those levels'
+    // positions near a close approach are the least accurate (round 5: 21 of HD155358's 23
+    // device-only encounters at its steady state never came within the exit distance on a densely
+    // sampled trajectory) -- the direction is refined instead (oracle/rvoracle.c dir_main)
+    int32_t fin_level;
     // 1: the certain-reject test runs on fused sampler launches (rvm_plan_set_certain_reject; an
     // empirical lower bound on chi2), 0: every open walker refines to the bound
     int32_t cut;
@@ -97,6 +103,11 @@ struct DevPlan {
     int32_t* rq_w;
     double* rq_c;
     int32_t rq_cap;
+    // rq_mark [rq_cap]: the low 32 bits of the launch generation at each walker slot the likelihood
+    // kernel listed -- a speculative iteration's half-1 variant whose partner was NOT listed has its
+    // partner's decision final in StretchArgs::dec, so the variant the decision rules out is skipped
+    // (rvm_refine.hip; RVM_STATUS_SKIPPED)
+    int32_t* rq_mark;
     // a both-direction group split over two workgroups exchanges its walkers' per-direction state
     // after every halving pass (rvm_refine.hip): rq_x [groups][2 directions][2 pass parities][64]
     // values in the meeting slot's encoding, rq_xf [groups][2] the flag (launch generation << 8 | pass)

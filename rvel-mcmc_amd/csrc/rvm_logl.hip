@@ -629,6 +629,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 const int ix = __hip_atomic_fetch_add(P.rq_n + li, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (ix < P.rq_cap) {
                     P.rq_w[(size_t)li * P.rq_cap + ix] = wo;
+                    P.rq_mark[wo] = (int32_t)__hip_atomic_load(P.gen_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     P.rq_c[wo] = of ? 0.0 : cf;
                     P.rq_c[(size_t)P.rq_cap + wo] = ob ? 0.0 : cb;
                     return;
@@ -803,18 +804,37 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const bool cmb = lvl == 0 && lane < WPB;  // lane `lane` of wave 0 owns walker slot `lane`
         const int wo = w0 + lane;
         int enc = 0;
-        if (cmb)
-            for (int k = 0; k < nl; k++) enc |= s_enc[k][lane];
+        // (adaptive plans: an encounter only the coarser levels see refines the direction instead
+        // of ending the walker, DevPlan::fin_level; `cenc`)
+        bool cenc = false;
+        if (cmb) {
+            int encc = 0;
+            for (int k = 0; k < nl; k++) {
+                const int f = s_enc[k][lane];
+                if (k == P.fin_level || !(P.rtol_dir < INFINITY)) {
+                    enc |= f;
+                } else {
+                    enc |= f & ~1;
+                    encc |= f & 1;
+                }
+            }
+            cenc = encc != 0 && (enc & 1) == 0;
+        }
         double chi2w = chi2;
         bool need = false;
         double lbw = 0.0;
         if (P.rtol_dir < INFINITY) {  // (kernel argument: uniform)
             // (a non-finite chi2 -- the fixed step blowing up on an extreme orbit -- refines too, and
-            // so does a walker past the eccentricity guard: its e^2 from the walker's first lane)
+            // so does a walker past the eccentricity guard: its e^2 from the walker's first lane,
+            // and one whose coarser levels alone came within the exit distance -- its main pass,
+            // like a non-finite one, neither settles nor bounds it: the stored RV of a refinement's
+            // first step-doubling change is invalidated, oracle/rvoracle.c dir_main `bad`)
             const double e2c = __shfl(e2w, (lane & (WPB - 1)) * L);
             need = cmb && wo < W && enc == 0 &&
                    (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est) ||
-                    (P.ext_mult > 0 && e2c > P.e2_guard));
+                    (P.ext_mult > 0 && e2c > P.e2_guard) || cenc);
+            if (cenc && need && P.ext_mult > 0)
+                for (int e = 0; e < E; e++) P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + wo] = __builtin_nan("");
             if (P.rmax == 0) {
                 if (need) enc |= RVM_ENC_UNRESOLVED;
                 need = false;
@@ -832,7 +852,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                                 enc |= 1;
                                 chi2w = c5x;
                                 need = false;
-                            } else if (ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
+                            } else if (!cenc && ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
                                 chi2w = c5x;
                                 need = false;
                             }
@@ -847,7 +867,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                     if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
                         extend_stage(lvl, grp, d, need, chi2w, enc, c5x, ddx);
                 }
-                lbw = direction_lb(need, chi2, est, need0 && P.ext_mult > 0, c5x, ddx);
+                lbw = cenc ? 0.0 : direction_lb(need, chi2, est, need0 && P.ext_mult > 0, c5x, ddx);
             }
         }
         if (cmb && wo < W) {
@@ -1068,7 +1088,13 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 __builtin_amdgcn_s_sleep(2);
                 hung = clk.expired(P.spin_ticks);
             }
-            int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];  // (lsx: [3] the extension)
+            // (slot 0 is level 3, the finest; lsx: [3] the extension; the HBM-handed level's in f1)
+            int enc = s_encl[ul][0][slot] | s_encl[ul][1][slot] | s_encl[ul][2][slot];
+            int encc = 0;  // (adaptive: the coarser levels' encounter bits, DevPlan::fin_level)
+            if (P.rtol_dir < INFINITY) {
+                encc = (s_encl[ul][1][slot] | s_encl[ul][2][slot]) & 1;
+                enc = s_encl[ul][0][slot] | ((s_encl[ul][1][slot] | s_encl[ul][2][slot]) & ~1);
+            }
             {
                 f1 = valid ? f1 : 0;
                 if (ballot(f1 < 0) != 0 && !hung) {
@@ -1079,8 +1105,15 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                     } while (ballot(f1 < 0) != 0 && !hung);
                 }
                 if (valid && pl_idx == 0) __hip_atomic_store(e1p, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                enc |= f1 > 0 ? f1 : 0;
+                const int f1p = f1 > 0 ? f1 : 0;
+                if (P.rtol_dir < INFINITY) {
+                    enc |= f1p & ~1;
+                    encc |= f1p & 1;
+                } else {
+                    enc |= f1p;
+                }
             }
+            const bool cenc = encc != 0 && (enc & 1) == 0;
             if (hung) {  // never completed (or a dirty workspace): NONFINITE, and the give-up counted
                 chi2w = __builtin_nan("");
                 enc |= RVM_ENC_FAULT;
@@ -1093,7 +1126,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
             // adaptive resolution: settled, or open (with its lower bound) for the refinement kernel
             bool need = P.rtol_dir < INFINITY && valid && pl_idx == 0 && enc == 0 &&
                         (est / P.npoints > P.rtol_dir || !isfinite(chi2w) || !isfinite(est) ||
-                         (P.ext_mult > 0 && e2w > P.e2_guard));
+                         (P.ext_mult > 0 && e2w > P.e2_guard) || cenc);
+            // (a coarse-only encounter's main pass neither settles nor bounds the direction: its
+            // stored RV for a refinement's first step-doubling change is invalidated)
+            if (cenc && need && !lsx && P.ext_mult > 0)
+                for (int e = 0; e < E; e++) P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = __builtin_nan("");
             if (need && P.rmax == 0) {
                 enc |= RVM_ENC_UNRESOLVED;
                 need = false;
@@ -1110,7 +1147,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                         enc |= 1;
                         chi2w = c5x;
                         need = false;
-                    } else if (ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
+                    } else if (!cenc && ddx <= RVM_EXT_ACCEPT * P.rtol_dir * P.npoints) {
                         chi2w = c5x;
                         need = false;
                     }
@@ -1121,7 +1158,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 // (lane = slot, extend_pass's convention) through LDS
                 if (valid && pl_idx == 0) {
                     s_fchi[ul][slot] = chi2w;
-                    s_fenc[ul][slot] = enc | (need ? 16 : 0);
+                    s_fenc[ul][slot] = enc | (need ? 16 : 0) | (cenc ? 32 : 0);
                     s_fx[0][ul][slot] = est;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1133,21 +1170,23 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 const double cm = c2;
                 int en = f & 15;
                 bool nd = (f & 16) != 0;
+                const bool cn = (f & 32) != 0;  // (a coarse-only encounter: the extension cannot settle it)
                 const uint64_t nm = ballot(nd);
                 if (lane == 0)
                     __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(nm),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 double xc5 = 0.0, xdd = 0.0;
                 extend_pass(ul, d, nm, nd, c2, en, xc5, xdd);
-                const double lb = direction_lb(nd, cm, es, (f & 16) != 0, xc5, xdd);
+                const double lb = cn ? 0.0 : direction_lb(nd, cm, es, (f & 16) != 0, xc5, xdd);
                 if (cl) finish_recompute(w0 + lane, c2, en, nd, lb);
             } else if (valid && pl_idx == 0) {
                 if (lsx && need) {  // the main pass's RV of an open direction (the ring, consume above)
                     const double* rg = ring + (size_t)(ul * 4 + 2) * RING * WPB + slot;
                     for (int e = 0; e < E; e++)
-                        P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = rg[(size_t)e * WPB];
+                        P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = cenc ? __builtin_nan("") : rg[(size_t)e * WPB];
                 }
-                finish_recompute(w, chi2w, enc, need, direction_lb(need, chi2m, est, lsx && need0, c5x, ddx));
+                finish_recompute(w, chi2w, enc, need,
+                                 cenc ? 0.0 : direction_lb(need, chi2m, est, lsx && need0, c5x, ddx));
             }
 #ifdef RVM_PROFILE
             prof_dec(rt_arr, nl - 1);

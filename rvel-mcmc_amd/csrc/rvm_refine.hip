@@ -161,6 +161,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     // kernel finished it), and whether any slot is listed
     __shared__ int s_eitems[64], s_eli[64], s_eany;
     __shared__ int s_emask;  // (eager) directions of the current pass an eager block runs
+    __shared__ int s_skip[64];  // the slot is a speculative variant its partner's decision rules out
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     for (int dd = 0; dd < 2; dd++) {
         const DirSched& SD = dd ? P.bwd : P.fwd;
@@ -256,7 +257,21 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             s_init[7][lane] = s.ir;
             if (lane < WPB) {
                 const int lli = eager ? s_eli[lane] : li;  // (eager: this slot's list, -1 none)
-                const bool v = lane < cnt && lli >= 0;
+                // a speculative iteration's half-1 slot against the outcome of its partner j (kind 1:
+                // j rejects, 2: j accepts): when j was not handed on (its mark is not this launch's)
+                // the likelihood kernel has stored j's final decision, and the variant it rules out is
+                // never read (rvm_stretch_iteration_end) -- skipped instead of refined
+                int skip = 0;
+                if (stretch && sa.n_spec > 0 && sa.dec != nullptr && lane < cnt && lli >= 0) {
+                    int k2 = 0, wk2 = 0, j2 = 0, jp2 = 0;
+                    double z2 = 0.0, zp2 = 0.0;
+                    stretch_slot(sa, items[lane], k2, wk2, z2, j2, zp2, jp2);
+                    const long long jl = (long long)j2 - sa.s0_begin;
+                    if (k2 != 0 && jl >= 0 && jl < sa.n_spec && P.rq_mark[jl] != (int32_t)gen)
+                        skip = (k2 == 2) != (sa.dec[jl] == 1);
+                }
+                s_skip[lane] = skip;
+                const bool v = lane < cnt && lli >= 0 && !skip;
                 const int wl = items[lane < cnt ? lane : 0];
                 const bool of = v && lli != 2, ob = v && lli != 1;
                 s_open[0][lane] = of ? 1 : 0;
@@ -275,8 +290,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 s_lpw[lane] = -INFINITY;
             }
             const int lli = lane < WPB ? (eager ? s_eli[lane] : li) : -1;
-            const uint64_t m0 = ballot(lane < WPB && lane < cnt && lli >= 0 && lli != 2);
-            const uint64_t m1 = ballot(lane < WPB && lane < cnt && lli >= 0 && lli != 1);
+            const bool live0 = lane < WPB && lane < cnt && lli >= 0 && !s_skip[lane < WPB ? lane : 0];
+            const uint64_t m0 = ballot(live0 && lli != 2);
+            const uint64_t m1 = ballot(live0 && lli != 1);
             if (lane == 0) {
                 s_mask[0] = m0;
                 s_mask[1] = m1;
@@ -802,7 +818,11 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         if (team && tm == 1) finisher = own <= 0 && !cancelled;
         // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h;
         // a split group's by its forward-direction workgroup, of team A or B)
-        if (finisher && wv == 0 && lane < WPB && lane < cnt && (!eager || s_eli[lane] >= 0)) {
+        if (finisher && wv == 0 && lane < WPB && lane < cnt && s_skip[lane]) {
+            logl_out[wme] = -INFINITY;
+            status_out[wme] = RVM_STATUS_SKIPPED;
+            __hip_atomic_fetch_add(P.counters + 6, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (finisher && wv == 0 && lane < WPB && lane < cnt && (!eager || s_eli[lane] >= 0)) {
             int k2 = 0, wk2 = wme, j2 = 0, jp2 = 0;
             double z2 = 0.0, zp2 = 0.0;
             if (stretch) stretch_slot(sa, wme, k2, wk2, z2, j2, zp2, jp2);

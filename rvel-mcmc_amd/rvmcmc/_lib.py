@@ -16,9 +16,10 @@ RVM_STATUS_PRIOR = 1
 RVM_STATUS_ENCOUNTER = 2
 RVM_STATUS_NONFINITE = 3
 RVM_STATUS_UNRESOLVED = 4
+RVM_STATUS_SKIPPED = 5  # rvm_stretch_iteration_begin status_spec only
 RVM_MAX_PLANETS = 4
 RVM_MAX_LEVELS = 6
-RVM_N_COUNTERS = 6  # rvm_plan_counters
+RVM_N_COUNTERS = 7  # rvm_plan_counters
 ABI_VERSION = 12  # include/rvmcmc.h RVM_ABI_VERSION
 
 

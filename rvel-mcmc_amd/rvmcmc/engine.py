@@ -215,7 +215,7 @@ class LoglPlan:
         _lib.check(self.lib.rvm_plan_counters(self._h, int(bool(reset)), vals, _lib.RVM_N_COUNTERS,
                                               _lib.stream_handle(stream)), "rvm_plan_counters")
         f = dict(handoff_timeouts=vals[0], nonfinite=vals[1], unresolved=vals[2], refined=vals[3],
-                 truncated=vals[4], floor_settled=vals[5])
+                 truncated=vals[4], floor_settled=vals[5], skipped=vals[6])
         if reset:  # (running totals over every reset: the samplers' periodic checks reset the counters)
             tot = self.__dict__.setdefault("totals", dict.fromkeys(f, 0))
             for k, v in f.items():

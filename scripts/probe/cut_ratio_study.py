@@ -98,7 +98,7 @@ def study(name, n=512, nt=None):
         lm, sm = par(lambda p: O.logl_whx_seq_batch(p, npl, od, dt, mult, 1.0))
         _, sa, _, est, _ = par(lambda p: O.logl_whx_adapt_batch(p, npl, od, dt, mult, tol, 0, 1.0))
         ok = (si == 0) & (sm == 0) & np.isfinite(li) & np.isfinite(lm)
-        err = np.abs(lm - li)[ok]
+        err = np.abs(lm[ok] - li[ok])
         e = est[ok, d]
         errs.append(err)
         ests.append(e)

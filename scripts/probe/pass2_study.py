@@ -31,7 +31,8 @@ def curves(P, obs, dt, d):
     t, o, e = (obs.tf, obs.rvf, obs.errorf) if d == 0 else (obs.tb, obs.rvb, obs.errorb)
     out = {}
     for key, mult in (("r0", (4, 5, 6, 7)), ("r1", (8, 10, 12, 14)), ("r1_3", (10, 12, 14)),
-                      ("r2", (16, 20, 24, 28))):
+                      ("r2", (16, 20, 24, 28)), ("x5", (8, 10, 12, 14, 15)), ("x7", (8, 9, 10, 11, 12, 13, 14)),
+                      ("x6", (9, 10, 11, 12, 13, 14)), ("x6b", (8, 10, 12, 14, 9, 11))):
         out[key] = O.whx_rv(planets, t, dt, mult, 1.0)[0]
     out["ias"] = O.get_rv_ias15(planets, t, 1.0)[0]
     return out, o, e * e
@@ -92,7 +93,15 @@ def main():
             chi = {k: float(np.sum((c[k] - o) ** 2 / s2)) / N for k in ("r0", "r1", "r2", "ias")}
             e1 = float(np.sum(np.abs((c["r1"] - c["r1_3"]) * (c["r1"] + c["r1_3"] - 2 * o)) / s2)) / N
             d1 = float(np.sum(np.abs((c["r1"] - c["r0"]) * (c["r1"] + c["r0"] - 2 * o)) / s2)) / N
+            def chg(a, b):
+                return float(np.sum(np.abs((c[a] - c[b]) * (c[a] + c[b] - 2 * o)) / s2)) / N / (0.5 * tol)
+
+            for k in ("x5", "x7", "x6b"):
+                chi[k] = float(np.sum((c[k] - o) ** 2 / s2)) / N
             rows.append({"it": it, "slot": int(slot), "dir": int(d), "stage": int(rf[slot, d]),
+                         "x5_d_over_tol": chg("x5", "r1"), "x5_err": abs(chi["x5"] - chi["ias"]),
+                         "x7_est_over_tol": chg("x7", "x6"), "x7_err": abs(chi["x7"] - chi["ias"]),
+                         "x6b_d_over_tol": chg("x6b", "r1"), "x6b_err": abs(chi["x6b"] - chi["ias"]),
                          "est1_over_tol": e1 / (0.5 * tol), "d1_over_tol": d1 / (0.5 * tol),
                          "err1": abs(chi["r1"] - chi["ias"]), "err2": abs(chi["r2"] - chi["ias"]),
                          "err0": abs(chi["r0"] - chi["ias"])})
@@ -110,6 +119,15 @@ def main():
     for r in rows:
         if r["stage"] >= 3:
             print(json.dumps(r))
+    for cand, key in (("x5", "x5_d_over_tol"), ("x7", "x7_est_over_tol"), ("x6b", "x6b_d_over_tol")):
+        for st in (2, 3):
+            R = [r for r in rows if r["stage"] == st]
+            if not R:
+                continue
+            ok = [r for r in R if r[key] <= 1.0]
+            print(json.dumps({"candidate": cand, "stage": st, "dirs": len(R), "settled": len(ok),
+                              "max_err_settled": max([r[cand + "_err"] for r in ok], default=0.0),
+                              "max_err_all": max(r[cand + "_err"] for r in R)}))
     R = [r for r in rows if r["stage"] == 2]
     if R:
         ratio = np.array([r["err1"] / max(r["d1_over_tol"] * 0.5 * tol, 1e-300) for r in R])

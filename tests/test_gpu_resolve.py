@@ -177,7 +177,7 @@ def test_tight_ball_never_refines_and_keeps_the_bits():
     f = plan.faults()
     np.testing.assert_array_equal(st, st0)
     np.testing.assert_array_equal(got, got0)
-    assert f == dict(handoff_timeouts=0, nonfinite=0, unresolved=0, refined=0, truncated=0, floor_settled=0), f
+    assert f == dict(handoff_timeouts=0, nonfinite=0, unresolved=0, refined=0, truncated=0, floor_settled=0, skipped=0), f
 
 
 def test_flag_only_matches_oracle():
