@@ -599,7 +599,13 @@ __device__ __forceinline__ bool lane_encountered(const Lane<NP>& s) {
     return ((s.encm >> base) & bits) != 0;
 }
 
-template <int NT, bool GATED, bool D3 = false, int NP>
+// G5: one more term of the guess's series, X = u (1 - us/2 + u^2 T3 + u^3 T4 + u^4 T5),
+//   T5 = (9 beta^2 - 19 beta g + 90 beta s^2 + 10 g^2 - 105 g s^2 + 105 s^4) / 120
+// (series reversion of u = G1 + s G2 + g G3 to fifth order; scripts/kepler_guess_series.py): ~9 VALU
+// more per drift, and the first Halley step is accepted far more often on eccentric orbits near
+// pericentre, where the wave otherwise takes the second step (~250 cycles on a lone wave:
+// scripts/probe/seg_bench.hip, profiles/r05f_seg_bench.txt) -- the refinement passes' regime.
+template <int NT, bool GATED, bool D3 = false, int NP, bool G5 = false>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const VConsts& vk) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;
     double v2 = fma(s.vx, s.vx, s.vy * s.vy);
@@ -614,7 +620,15 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
     const double hs = 0.5 * sg;
     const double T3 = fma(hs, sg, (beta - g) * (1.0 / 6.0));
     const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
-    const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
+    double x;
+    if constexpr (G5) {
+        const double s2 = sg * sg;
+        const double T5 = fma(beta, fma(9.0 / 120.0, beta, fma(-19.0 / 120.0, g, 0.75 * s2)),
+                              fma(g, fma(1.0 / 12.0, g, -0.875 * s2), 0.875 * (s2 * s2)));
+        x = u * fma(u, fma(u, fma(u, fma(u, T5, T4), T3), -hs), 1.0);
+    } else {
+        x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
+    }
     double G0, G1, G2, G3, fp, fpp, Q, z, x3;
     halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2, vk.k3);
     constexpr double B = stumpff_bound<NT>();

@@ -32,6 +32,13 @@
 
 #include "rvm_walker.h"
 
+// the main pass's drifts with the fifth-order Kepler guess (rvm_device.h drift G5; A/B knob, off:
+// the main pass's waves share SIMDs, where the extra VALU cost more than the second Halley steps save
+// at the bench window -- DESIGN.md §10)
+#ifndef RVM_MAIN_G5
+#define RVM_MAIN_G5 0
+#endif
+
 namespace rvm {
 
 #ifdef RVM_PROFILE
@@ -474,22 +481,22 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 // orbits keep needing the general solver (short periods, high eccentricity in a
                 // wide ensemble) then run gated for a while instead of paying for redos
                 if (spec_off == 0) {
-                    if (segment<6, true, D3, NP, L>(s, kp, h, ns, redo)) {
+                    if (segment<6, true, D3, NP, L, RVM_MAIN_G5 != 0>(s, kp, h, ns, redo)) {
                         spec_off = spec_bo;
                         spec_bo = spec_bo < 64 ? 2 * spec_bo : 64;
                     } else {
                         spec_bo = 4;
                     }
                 } else {
-                    segment<6, false, D3, NP, L>(s, kp, h, ns, redo);
+                    segment<6, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kp, h, ns, redo);
                     spec_off--;
                 }
             } else if (nt <= 6)
-                segment<6, false, D3, NP, L>(s, kp, h, ns, redo);
+                segment<6, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kp, h, ns, redo);
             else if (nt == 7)
-                segment<7, false, D3, NP, L>(s, kp, h, ns, redo);
+                segment<7, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kp, h, ns, redo);
             else
-                segment<8, false, D3, NP, L>(s, kp, h, ns, redo);
+                segment<8, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kp, h, ns, redo);
         }
         PROF_T(tb);
         const double v0 = star_vx<NP, L>(s);
@@ -722,22 +729,22 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 const double h = r_len[e] * ix;
                 if (P.ext_spec && ntx <= 6) {  // (the main pass's speculation policy: same bits)
                     if (x_off == 0) {
-                        if (segment<6, true, D3, NP, L>(s, kq, h, ns, dummy_redo)) {
+                        if (segment<6, true, D3, NP, L, RVM_MAIN_G5 != 0>(s, kq, h, ns, dummy_redo)) {
                             x_off = x_bo;
                             x_bo = x_bo < 64 ? 2 * x_bo : 64;
                         } else {
                             x_bo = 4;
                         }
                     } else {
-                        segment<6, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                        segment<6, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kq, h, ns, dummy_redo);
                         x_off--;
                     }
                 } else if (ntx <= 6)
-                    segment<6, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                    segment<6, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kq, h, ns, dummy_redo);
                 else if (ntx == 7)
-                    segment<7, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                    segment<7, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kq, h, ns, dummy_redo);
                 else
-                    segment<8, false, D3, NP, L>(s, kq, h, ns, dummy_redo);
+                    segment<8, false, D3, NP, L, RVM_MAIN_G5 != 0>(s, kq, h, ns, dummy_redo);
             }
             const double v = star_vx<NP, L>(s);
             const double vx = __shfl(v, cs * L);

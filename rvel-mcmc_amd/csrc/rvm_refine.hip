@@ -54,6 +54,13 @@
 
 #include "rvm_walker.h"
 
+// the halving passes' drifts take the fifth-order Kepler guess (rvm_device.h drift G5): they run on
+// lone waves, mostly for the eccentric walkers the main pass could not settle, where the fourth-order
+// guess sends the wave into the second Halley step at most steps (scripts/probe/seg_bench.hip)
+#ifndef RVM_REFINE_G5
+#define RVM_REFINE_G5 1
+#endif
+
 namespace rvm {
 
 // Claim word of one eager (pass, direction) item (DevPlan::eflag): set it to gen << 8 | code unless
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     const bool here = e < Er;
                     const double pv = cmb && here && hasp && !bfirst ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued early)
                     const int ns = __builtin_amdgcn_readfirstlane(work && here ? r_n[e] * m_r : 0);
-                    if (ns > 0) segment_gated<D3, NP, L>(s, kq, r_len[e] * sc, ns, nt_r);
+                    if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_G5 != 0>(s, kq, r_len[e] * sc, ns, nt_r);
                     if (work && here) {  // (star_vx gathers over the walker's lanes by DPP: outside the lane branch)
                         const double v0 = star_vx<NP, L>(s);
                         if (pl_idx == 0) s_rv[dd_u][e & 1][k_u][slot] = v0;
@@ -911,7 +918,7 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     bool cancelled = false;
     for (int e = 0; e < Er; e++) {
         const int ns = __builtin_amdgcn_readfirstlane(work ? SR.seg_n[e] * m_r : 0);
-        if (ns > 0) segment_gated<D3, NP, L>(s, kq, SR.seg_h1[e] * sc, ns, nt_r);
+        if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_G5 != 0>(s, kq, SR.seg_h1[e] * sc, ns, nt_r);
         if (work) {
             const double v0 = star_vx<NP, L>(s);
             if (pl_idx == 0) s_rv[e & 1][k_u][slot] = v0;

@@ -16,26 +16,26 @@ namespace rvm {
 // segment's opening half kick, and leaves holding the one at the next epoch.  (The step loop is
 // unrolled by hand: the compiler will not unroll a runtime trip count around the convergent DPP /
 // ballot operations.)
-template <int NT, bool GATED, bool D3, int NP, int L>
+template <int NT, bool GATED, bool D3, int NP, int L, bool G5 = false>
 __device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, bool& bad) {
     lane_set_step(s, h);
     const VConsts vk = vconsts_for<NT>();  // loop-invariant VGPR constants
     kick_apply<NP, true, D3>(s, kp);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
-        drift<NT, GATED, D3>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
-        drift<NT, GATED, D3>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
     }
     if (j < ns - 1) {
-        drift<NT, GATED, D3>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
     }
-    drift<NT, GATED, D3>(s, h, bad, vk);
+    drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
     kp = kick_prep<NP, L, D3>(s, vk.c1875);
     kick_apply<NP, true, D3>(s, kp);
 }
@@ -44,7 +44,7 @@ __device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, dou
 // of the wave had a step that needs the general solver, restore the segment's initial state and
 // redo it gated.  Used on the fine levels, where such steps are rare.  Returns whether the
 // segment was redone (wave-uniform).  Either way every lane ends bit-identical to a gated run.
-template <int NT, bool SPEC, bool D3, int NP, int L>
+template <int NT, bool SPEC, bool D3, int NP, int L, bool G5 = false>
 __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int& redo) {
     bool bad = false;
     if constexpr (SPEC) {
@@ -52,7 +52,7 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h,
         const double rz = s.rz, vz = s.vz;
         const uint64_t encm = s.encm;
         const KickPrep<NP> kp0 = kp;
-        segment_steps<NT, false, D3, NP, L>(s, kp, h, ns, bad);
+        segment_steps<NT, false, D3, NP, L, G5>(s, kp, h, ns, bad);
         if (__builtin_expect(ballot(bad) != 0, 0)) {
 #ifdef RVM_PROFILE
             redo++;
@@ -67,26 +67,27 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h,
             s.ir = ir;
             s.encm = encm;
             kp = kp0;
-            segment_steps<NT, true, D3, NP, L>(s, kp, h, ns, bad);
+            segment_steps<NT, true, D3, NP, L, G5>(s, kp, h, ns, bad);
             return true;
         }
     } else {
-        segment_steps<NT, true, D3, NP, L>(s, kp, h, ns, bad);
+        segment_steps<NT, true, D3, NP, L, G5>(s, kp, h, ns, bad);
     }
     (void)redo;
     return false;
 }
 
-// a gated segment with the Stumpff series length of the level (nt: 6, 7 or 8)
-template <bool D3, int NP, int L>
+// a gated segment with the Stumpff series length of the level (nt: 6, 7 or 8); G5: the fifth-order
+// Kepler guess (rvm_device.h drift)
+template <bool D3, int NP, int L, bool G5 = false>
 __device__ __forceinline__ void segment_gated(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int nt) {
     int unused = 0;
     if (nt <= 6)
-        segment<6, false, D3, NP, L>(s, kp, h, ns, unused);
+        segment<6, false, D3, NP, L, G5>(s, kp, h, ns, unused);
     else if (nt == 7)
-        segment<7, false, D3, NP, L>(s, kp, h, ns, unused);
+        segment<7, false, D3, NP, L, G5>(s, kp, h, ns, unused);
     else
-        segment<8, false, D3, NP, L>(s, kp, h, ns, unused);
+        segment<8, false, D3, NP, L, G5>(s, kp, h, ns, unused);
 }
 
 // kernel parameter row r of walker w: from the SoA input, or (fused sampler step) the row's fixed

@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librvmcmc.so")
+# (RVM_LIB_PATH: another build of the same ABI, for A/B runs of compile-time variants -- scripts/probe)
+LIB_PATH = os.environ.get("RVM_LIB_PATH") or os.path.join(_HERE, "librvmcmc.so")
 
 RVM_STATUS_OK = 0
 RVM_STATUS_PRIOR = 1

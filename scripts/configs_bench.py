@@ -87,17 +87,25 @@ def config4(chains=256, steps=100, fused=True):
     sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=chains, seed=0)
     sm.step(fused=fused)
     torch.cuda.synchronize()
+    # (an event on the launch stream after each step: the steps' own durations, for their spread --
+    # a step whose centres need a second halving pass takes about twice as long)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(steps):
+    evs[0].record()
+    for i in range(steps):
         sm.step(fused=fused)
+        evs[i + 1].record()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    per = np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(steps)])
     P = s.Nvars
     how = ("fused: propose + stencil logL launch + derive/accept kernel" if fused else
            "separate propose / fd / logL / derive / accept launches")
     return {"config": f"4: SMALA, 256 chains, 10-dim, FD (2P+1 = 21 logL per chain-step), {how}",
             "chain_steps_per_s": chains * steps / dt, "walker_logl_evals_per_s": chains * steps * (2 * P + 1) / dt,
-            "ms_per_step": 1e3 * dt / steps, "acceptance": float(sm.accepted.double().mean().item() / sm.iteration)}
+            "ms_per_step": 1e3 * dt / steps, "acceptance": float(sm.accepted.double().mean().item() / sm.iteration),
+            "step_ms_quantiles": [float(v) for v in np.quantile(per, [0, 0.25, 0.5, 0.75, 0.9, 1.0])],
+            "step_ms_quantile_levels": [0, 0.25, 0.5, 0.75, 0.9, 1.0]}
 
 
 def config4x(chains=256, steps=5):

@@ -9,10 +9,39 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
 export TMPDIR=/tmp
 T=${T:-r05}
-STEPS=${STEPS:-"bench prof pmc"}
+STEPS=${STEPS:-"bench prof pmc"}   # also: tests segbench configs
 mkdir -p gpurun_out
 for step in $STEPS; do
   case $step in
+    tests)
+      RVM_PARITY_REPORT=gpurun_out/${T}_parity.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -x -q \
+        --timeout 300 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1 \
+        || { grep -E "FAIL|Error" gpurun_out/${T}_pytest.log | tail -20; tail -3 gpurun_out/${T}_pytest.log; exit 1; }
+      tail -2 gpurun_out/${T}_pytest.log
+      timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 \
+        || { cat gpurun_out/${T}_smoke.log; exit 1; }
+      tail -1 gpurun_out/${T}_smoke.log ;;
+    segbench)
+      timeout -k 10 120 ./scripts/probe/seg_bench ${SEG_ARGS:-0.22 32 0.22 112 0.40 112 0.40 224 0.55 112} \
+        > gpurun_out/${T}_seg_bench.txt 2>&1 || { cat gpurun_out/${T}_seg_bench.txt; exit 1; }
+      cat gpurun_out/${T}_seg_bench.txt ;;
+    steadyab)
+      # A/B at the bench chain's steady state: the default library against the variants in AB_LIBS
+      # (built by make -C rvel-mcmc_amd variant-*), interleaved twice
+      for rep in 1 2; do
+        for lib in default ${AB_LIBS:-scripts/probe/librvmcmc_mg5.so}; do
+          if [ "$lib" = default ]; then
+            ITERS=${AB_ITERS:-300} timeout -k 10 200 python -u scripts/probe/steady_bench.py 4,5,6,7:5e-7 >> gpurun_out/${T}_steady_ab.jsonl 2>> gpurun_out/${T}_steady_ab.err || exit 1
+          else
+            RVM_LIB_PATH=$lib ITERS=${AB_ITERS:-300} timeout -k 10 200 python -u scripts/probe/steady_bench.py 4,5,6,7:5e-7 >> gpurun_out/${T}_steady_ab.jsonl 2>> gpurun_out/${T}_steady_ab.err || exit 1
+          fi
+        done
+      done
+      cut -c1-400 gpurun_out/${T}_steady_ab.jsonl ;;
+    configs)
+      timeout -k 10 600 python -u scripts/configs_bench.py ${CONFIGS:-} > gpurun_out/${T}_configs.jsonl 2> gpurun_out/${T}_configs.err \
+        || { tail -20 gpurun_out/${T}_configs.err; exit 1; }
+      cut -c1-300 gpurun_out/${T}_configs.jsonl ;;
     bench)
       timeout -k 10 500 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err \
         || { tail -30 gpurun_out/${T}_bench.err; exit 1; }

@@ -20,7 +20,7 @@ from rvmcmc.observations import FakeObservation  # noqa: E402
 from rvmcmc.state import State  # noqa: E402
 
 
-def run(resolve_tol, levels=(4, 5, 6, 7), resolve_max=None, iters=30, warm=3):
+def run(resolve_tol, levels=(4, 5, 6, 7), resolve_max=None, iters=int(os.environ.get("ITERS", "30")), warm=3):
     if resolve_max is None:
         resolve_max = engine.IntegratorConfig().resolve_max
     state = State(planets=[dict(p) for p in S2_PLANETS])
@@ -35,15 +35,20 @@ def run(resolve_tol, levels=(4, 5, 6, 7), resolve_max=None, iters=30, warm=3):
         ens.step()
     torch.cuda.synchronize()
     f0 = ens.check_faults()
+    ens.plan.time_kernels(iters)
     t0 = time.perf_counter()
     for _ in range(iters):
         ens.step()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    km, kr = ens.plan.kernel_times()
     f = ens.check_faults()
     return dict(resolve_tol=resolve_tol, resolve_max=resolve_max, levels=list(levels), walkers=len(X), iterations=iters, ms_per_iteration=1e3 * dt / iters,
                 evals_per_s=len(X) * iters / dt, speculative=bool(ens.speculating()), faults=f,
-                faults_warm=f0)
+                faults_warm=f0, logl_kernel_ms=float(np.mean(km)) if len(km) else None,
+                refine_kernel_ms=float(np.mean(kr)) if len(kr) else None,
+                refine_kernel_ms_quantiles=[float(v) for v in np.quantile(kr, [0, .25, .5, .75, 1])] if len(kr) else None,
+                lib=os.environ.get("RVM_LIB_PATH", "default"))
 
 
 if __name__ == "__main__":
