@@ -38,6 +38,15 @@ for step in $STEPS; do
         done
       done
       cut -c1-400 gpurun_out/${T}_steady_ab.jsonl ;;
+    c4ab)
+      # config 4's eager halving passes: pass 1 only, passes 1 and 2, pass 2 hinted (RVM_EAGER_PASSES)
+      for rep in 1 2; do
+        for ep in 1 2 h; do
+          RVM_EAGER_PASSES=$ep timeout -k 10 200 python -u scripts/configs_bench.py 4 \
+            | sed "s/^{/{\"eager_passes\": \"$ep\", /" >> gpurun_out/${T}_c4ab.jsonl 2>> gpurun_out/${T}_c4ab.err || exit 1
+        done
+      done
+      cut -c1-300 gpurun_out/${T}_c4ab.jsonl ;;
     configs)
       timeout -k 10 600 python -u scripts/configs_bench.py ${CONFIGS:-} > gpurun_out/${T}_configs.jsonl 2> gpurun_out/${T}_configs.err \
         || { tail -20 gpurun_out/${T}_configs.err; exit 1; }
