@@ -25,9 +25,6 @@
 #ifndef RVM_EAGER_PASSES_DEFAULT
 #define RVM_EAGER_PASSES_DEFAULT 1
 #endif
-#ifndef RVM_EAGER_HINT_DEFAULT
-#define RVM_EAGER_HINT_DEFAULT 0
-#endif
 
 namespace rvm {
 hipError_t launch_logl(const DevPlan& P, int W, const double* params, double hill_factor, unsigned long long* slots,
@@ -421,7 +418,6 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.eflag = nullptr;
     P.eager_max = 0;
     P.eager_passes = 0;
-    P.eager_hint = 0;
     P.e2_guard = INFINITY;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
@@ -555,10 +551,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
                 P.esum = P.rve + 4 * plane;
                 P.eflag = reinterpret_cast<unsigned long long*>(P.esum + 12 * (size_t)P.lvx_stride);
                 P.eager_max = emw;
-                // (A/B knob: 1, 2, or h -- pass 2 for the groups that needed it lately)
-                const char* ep = getenv("RVM_EAGER_PASSES");
-                P.eager_passes = ep && ep[0] == '1' ? 1 : (ep && (ep[0] == '2' || ep[0] == 'h') ? 2 : RVM_EAGER_PASSES_DEFAULT);
-                P.eager_hint = ep ? (ep[0] == 'h' ? 1 : 0) : RVM_EAGER_HINT_DEFAULT;
+                const char* ep = getenv("RVM_EAGER_PASSES");  // (A/B knob: 1 or 2)
+                P.eager_passes = ep && ep[0] == '1' ? 1 : (ep && ep[0] == '2' ? 2 : RVM_EAGER_PASSES_DEFAULT);
             } else {
                 (void)hipGetLastError();
                 if (plan->ev_fork) (void)hipEventDestroy(plan->ev_fork);

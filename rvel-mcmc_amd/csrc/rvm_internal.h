@@ -40,8 +40,6 @@ constexpr int RVM_EAGER_MAX = 512;
 constexpr int RVM_EAGER_MIN = 32;
 // eflag words per eager group (rvm_refine.hip)
 constexpr int RVM_EFLAG_WORDS = 8;
-// hinted eager pass 2 (DevPlan::eager_hint): a group's hint lasts this many launch generations
-constexpr unsigned long long RVM_EAGER_HINT_GENS = 16;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
@@ -129,16 +127,12 @@ struct DevPlan {
     // their chi2, estimate and encounter flag
     double* rve;
     double* esum;
-    // [groups][8] (rvm_refine.hip): [0] cancel the group, [1] the last generation in which the group
-    // needed a second halving pass, [2 + 2 (rf - 1) + d] the claim word of pass rf in direction d
-    // (generation << 8 | 1 eager block running, 2 its results stored, 3 the refinement kernel
-    // integrates it itself), [6 + d] cancel direction d
+    // [groups][8] (rvm_refine.hip): [0] cancel the group, [2 + 2 (rf - 1) + d] the claim word of
+    // pass rf in direction d (generation << 8 | 1 eager block running, 2 its results stored, 3 the
+    // refinement kernel integrates it itself), [6 + d] cancel direction d
     unsigned long long* eflag;
     int32_t eager_max;
     int32_t eager_passes;  // (1 or 2: how many halving passes eager_kernel runs)
-    // (eager_passes 2) pass 2 only for groups that needed it within the last RVM_EAGER_HINT_GENS
-    // launch generations (eflag[1]); 0: for every group
-    int32_t eager_hint;
     // the launch generation (device word, >= 1): the tag of the refinement kernel's exchange flags and
     // the eager blocks' claim words.  Read on the device by both kernels and advanced on the device
     // after every launch (the refinement kernel's last block, or gen_bump_kernel after an eager

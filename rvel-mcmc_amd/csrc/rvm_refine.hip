@@ -379,8 +379,6 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 // block that may not have been dispatched
                 if (threadIdx.x == 0) {
                     int em = 0;
-                    if (rf == 2)  // (the group's hint for the next launches' eager pass 2)
-                        __hip_atomic_store(ef + 1, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     for (int d3 = 0; d3 < 2; d3++) {
                         if (!((amw >> d3) & 1))
                             __hip_atomic_store(ef + 6 + d3, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -862,8 +860,6 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
 // group, whatever of it still runs (eflag[0]) -- blocks check these before reading their walkers and
 // once per epoch.  run_logl joins the side stream back into the caller's after the refinement
 // kernel (rvm_abi.hip): the launch is complete, eager blocks included, when the caller's stream is.
-// Hinted pass 2 (DevPlan::eager_hint): a group's pass-2 blocks run only when the refinement kernel
-// needed pass 2 for that group within the last RVM_EAGER_HINT_GENS launches (eflag[1]).
 template <int NP, bool D3>
 __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W, const double* __restrict__ params,
                                                     const double hill_factor) {
@@ -894,14 +890,7 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
                __hip_atomic_load(ef + 6 + dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ctag;
     };
     gu64* item = ef + 2 + 2 * (rf - 1) + dd;
-    // (hinted pass 2: only a group that needed it lately; otherwise the item stays unclaimed, and the
-    // refinement kernel integrates it should it be needed after all)
-    auto hinted = [&]() {
-        if (rf < 2 || !P.eager_hint) return true;
-        const unsigned long long h = __hip_atomic_load(ef + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return h != 0 && gen - h <= RVM_EAGER_HINT_GENS;
-    };
-    if (threadIdx.x == 0) s_cancel[0] = !hinted() || cancelled_now() || !claim_item(item, gen, 1ull);
+    if (threadIdx.x == 0) s_cancel[0] = cancelled_now() || !claim_item(item, gen, 1ull);
     __syncthreads();
     if (s_cancel[0]) return;  // (before the walkers are read)
     const int w0 = g * WPB;

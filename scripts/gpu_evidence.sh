@@ -39,14 +39,23 @@ for step in $STEPS; do
       done
       cut -c1-400 gpurun_out/${T}_steady_ab.jsonl ;;
     c4ab)
-      # config 4's eager halving passes: pass 1 only, passes 1 and 2, pass 2 hinted (RVM_EAGER_PASSES)
+      # config 4 (SMALA FD: eager halving passes on the centres): the default library against AB_LIBS
       for rep in 1 2; do
-        for ep in 1 2 h; do
-          RVM_EAGER_PASSES=$ep timeout -k 10 200 python -u scripts/configs_bench.py 4 \
-            | sed "s/^{/{\"eager_passes\": \"$ep\", /" >> gpurun_out/${T}_c4ab.jsonl 2>> gpurun_out/${T}_c4ab.err || exit 1
+        for lib in default ${AB_LIBS:-scripts/probe/librvmcmc_mg5.so}; do
+          if [ "$lib" = default ]; then lp=""; else lp=$lib; fi
+          RVM_LIB_PATH=$lp timeout -k 10 200 python -u scripts/configs_bench.py 4 \
+            | sed "s|^{|{\"lib\": \"${lib}\", |" >> gpurun_out/${T}_c4ab.jsonl 2>> gpurun_out/${T}_c4ab.err || exit 1
         done
       done
       cut -c1-300 gpurun_out/${T}_c4ab.jsonl ;;
+    rehearse2)
+      # world-size-2 rehearsal of the bench on the box's one GPU (gloo: RCCL cannot put two ranks on
+      # one device), timed at the chain's steady state like the N = 1 line
+      RVM_DIST_BACKEND=gloo timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 3 --ess-iters 2000 --no-cpu \
+        > gpurun_out/${T}_bench_n2_gloo.json 2> gpurun_out/${T}_bench_n2_gloo.err \
+        || { tail -30 gpurun_out/${T}_bench_n2_gloo.err; exit 1; }
+      head -c 600 gpurun_out/${T}_bench_n2_gloo.json; echo ;;
     configs)
       timeout -k 10 600 python -u scripts/configs_bench.py ${CONFIGS:-} > gpurun_out/${T}_configs.jsonl 2> gpurun_out/${T}_configs.err \
         || { tail -20 gpurun_out/${T}_configs.err; exit 1; }

@@ -426,15 +426,13 @@ def test_certain_reject_can_be_switched_off():
     assert f["refined"] > 0 and f["truncated"] == 0 and f["unresolved"] == 0, f
 
 
-@pytest.mark.parametrize("W,passes", [(32, "1"), (256, "1"), (512, "1"), (32, "2"), (256, "2"), (256, "h")])
+@pytest.mark.parametrize("W,passes", [(32, "1"), (256, "1"), (512, "1"), (32, "2"), (256, "2")])
 def test_eager_halving_passes_bit_identical(W, passes):
     """Plain launches of few walkers run the first halving pass (RVM_EAGER_PASSES=2: the first two)
     of every walker beside the likelihood kernel (rvm_refine.hip eager_kernel) and the refinement
     kernel replays them: the same logL, status bits and plan counters as the refinement kernel
     integrating them after the likelihood kernel (RVM_EAGER=0), on wide-ball walkers (extensions,
-    one- and two-pass walkers, deeper ones, encounters, prior rejections).  RVM_EAGER_PASSES=h runs
-    pass 2 only for the groups that needed it in a recent launch: the second launch of the same
-    walkers has the hints of the first."""
+    one- and two-pass walkers, deeper ones, encounters, prior rejections)."""
     import os
 
     obs = s2_obs_oracle()
@@ -447,9 +445,6 @@ def test_eager_halving_passes_bit_identical(W, passes):
         try:
             plan, _, _ = _plan(obs, W)
             got, st = _run(plan, X)
-            if passes == "h":
-                plan.faults(reset=True)
-                got, st = _run(plan, X)
             res.append((got, st, plan.faults(reset=True)))
         finally:
             for k, v in old.items():
