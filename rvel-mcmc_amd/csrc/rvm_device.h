@@ -604,7 +604,9 @@ __device__ __forceinline__ bool lane_encountered(const Lane<NP>& s) {
 // (series reversion of u = G1 + s G2 + g G3 to fifth order; scripts/kepler_guess_series.py): ~9 VALU
 // more per drift, and the first Halley step is accepted far more often on eccentric orbits near
 // pericentre, where the wave otherwise takes the second step (~250 cycles on a lone wave:
-// scripts/probe/seg_bench.hip, profiles/r05f_seg_bench.txt) -- the refinement passes' regime.
+// scripts/probe/seg_bench.hip, profiles/r05g_seg_bench_g5.txt).  Off in every shipped kernel: the
+// ~55 cycles it adds to every other step outweigh that at the steps the passes take
+// (rvm_refine.hip RVM_REFINE_G5, rvm_logl.hip RVM_MAIN_G5).
 template <int NT, bool GATED, bool D3 = false, int NP, bool G5 = false>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const VConsts& vk) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;

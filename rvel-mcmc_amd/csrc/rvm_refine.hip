@@ -54,11 +54,14 @@
 
 #include "rvm_walker.h"
 
-// the halving passes' drifts take the fifth-order Kepler guess (rvm_device.h drift G5): they run on
-// lone waves, mostly for the eccentric walkers the main pass could not settle, where the fourth-order
-// guess sends the wave into the second Halley step at most steps (scripts/probe/seg_bench.hip)
+// the halving passes' drifts on the fifth-order Kepler guess (rvm_device.h drift G5): off.  It cuts a
+// lone wave's step on eccentric orbits at coarse resolution (933 -> 693 cycles at 32 steps per inner
+// orbit, e = 0.22) but costs ~55 cycles where the fourth-order guess already takes one Halley step
+// (scripts/probe/seg_bench.hip, profiles/r05g_seg_bench_g5.txt), and at the halving passes' finer
+// steps the latter dominates: steady state 1.422 -> 1.388 ms per iteration and config 4 295k -> 318k
+// chain-steps/s with it off (profiles/r05h_steady_ab_refine_g5.jsonl, r05h_config4_ab_refine_g5.jsonl; "default" there is G5 on)
 #ifndef RVM_REFINE_G5
-#define RVM_REFINE_G5 1
+#define RVM_REFINE_G5 0
 #endif
 
 namespace rvm {

@@ -74,6 +74,16 @@ for step in $STEPS; do
       tr=$(find gpurun_out/${T}_prof_steady -name "*kernel_trace.csv" | head -1)
       python3 scripts/trace_window.py "$tr" 84 > gpurun_out/${T}_rocprof_window.json
       cat gpurun_out/${T}_rocprof_window.json ;;
+    profcfg)
+      # kernel trace of one configuration (PCFG) of scripts/configs_bench.py
+      mkdir -p gpurun_out/${T}_prof_cfg${PCFG:-2}
+      cd /tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${T}_prof_cfg${PCFG:-2}" -o run --output-format csv -- \
+        python3 "$R/scripts/configs_bench.py" ${PCFG:-2} > "$R/gpurun_out/${T}_cfg${PCFG:-2}_under_rocprof.jsonl" \
+        2> "$R/gpurun_out/${T}_cfg${PCFG:-2}_under_rocprof.err"
+      cd "$R"
+      st=$(find gpurun_out/${T}_prof_cfg${PCFG:-2} -name "*kernel_stats.csv" | head -1)
+      cut -c1-200 "$st" | head -12 ;;
     pmc)
       timeout -k 10 900 bash scripts/pmc_profile.sh > gpurun_out/${T}_pmc.log 2>&1 || { tail -20 gpurun_out/${T}_pmc.log; exit 1; }
       cp gpurun_out/pmc/pmc_latest.json gpurun_out/${T}_pmc_latest.json
