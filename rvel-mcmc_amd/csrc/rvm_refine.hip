@@ -66,6 +66,23 @@
 
 namespace rvm {
 
+#ifdef RVM_PROFILE
+// Timing build (make profile -> scripts/probe/librvmcmc_prof.so; scripts/probe/refine_prof.py): per
+// wave of a block's first task, [0..3] the 100 MHz real time at kernel entry, pass-loop start,
+// pass-loop end and task end; [4] shader cycles inside segments, [5] in epoch handling (star vx,
+// barrier, combiner), [6] steps integrated, [7] prologue cycles, [8] pass-loop cycles,
+// [9] task | team << 16 | (own + 1) << 20 | (last level + 1) << 24 | eager << 28, [10] passes
+// integrated, [11] HW_REG_HW_ID, [12] cycles in the eager / team / split waits and replays.
+#define RVM_RPROF_SLOTS 16
+#define RVM_RPROF_MAX_WAVES 4096
+__device__ unsigned long long rvm_rprof[RVM_RPROF_MAX_WAVES * RVM_RPROF_SLOTS];
+#define RPROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
+#define RPROF_RT(v) const unsigned long long v = __builtin_amdgcn_s_memrealtime()
+#else
+#define RPROF_T(v)
+#define RPROF_RT(v)
+#endif
+
 // Claim word of one eager (pass, direction) item (DevPlan::eflag): set it to gen << 8 | code unless
 // this launch generation already holds it.  Returns whether the caller now owns the item.  The eager
 // block claims at its start (code 1), the refinement kernel when it needs the pass (code 3): whoever
@@ -104,6 +121,12 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
     const int slot = lane / L;
     const int pl_idx = lane % L;
     const int nl = P.n_levels;
+    RPROF_T(pt_entry);
+    RPROF_RT(prt_entry);
+#ifdef RVM_PROFILE
+    unsigned long long p_seg = 0, p_epo = 0, p_steps = 0, p_wait = 0, p_pass = 0;
+    int p_lvl = -1;
+#endif
 
     // the list sizes are final (the likelihood kernel has ended); the last block to read them
     // resets them for the plan's next launch and (no eager blocks in this launch: they read the
@@ -368,6 +391,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             }
         };
         bool finisher = !team && own <= 0;  // the workgroup that finishes the walkers
+        RPROF_T(pt_loop0);
+        RPROF_RT(prt_loop0);
         for (int rf = 1 + tm; rf <= P.rmax; rf++) {
             const bool bfirst = tm == 1 && rf == 2;  // team B's pass concurrent with A's
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
@@ -457,7 +482,13 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     const bool here = e < Er;
                     const double pv = cmb && here && hasp && !bfirst ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued early)
                     const int ns = __builtin_amdgcn_readfirstlane(work && here ? r_n[e] * m_r : 0);
+                    RPROF_T(pt_s0);
                     if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_G5 != 0>(s, kq, r_len[e] * sc, ns, nt_r);
+                    RPROF_T(pt_s1);
+#ifdef RVM_PROFILE
+                    p_seg += pt_s1 - pt_s0;
+                    p_steps += (unsigned long long)ns;
+#endif
                     if (work && here) {  // (star_vx gathers over the walker's lanes by DPP: outside the lane branch)
                         const double v0 = star_vx<NP, L>(s);
                         if (pl_idx == 0) s_rv[dd_u][e & 1][k_u][slot] = v0;
@@ -490,7 +521,16 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                         }
                         if (rv_out != nullptr) rv_out[(size_t)r_idx[e] * W + wme] = rvx;
                     }
+#ifdef RVM_PROFILE
+                    p_epo += __builtin_readcyclecounter() - pt_s1;
+#endif
                 }
+#ifdef RVM_PROFILE
+                if (work) {
+                    p_pass++;
+                    p_lvl = k;
+                }
+#endif
                 if (cancelled) break;
                 if (work && pl_idx == 0) s_enc[dd_u][k_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
                 __syncthreads();
@@ -518,6 +558,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 }
             }
             if (cancelled) break;  // (team B: team A finished the group; every wave saw the same flag)
+            RPROF_T(pt_w0);
             __syncthreads();
             if (emask != 0 && wv == 0) {
                 // the eager-run directions: once their blocks have stored pass rf (write-through values,
@@ -746,6 +787,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     }
                 }
             }
+#ifdef RVM_PROFILE
+            p_wait += __builtin_readcyclecounter() - pt_w0;
+#endif
             // the walker's decision (wave 0, lane = walker slot; a split task's two workgroups take the
             // same decisions from the same states)
             if (wv == 0) {
@@ -825,6 +869,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 break;
             }
         }
+        RPROF_T(pt_loop1);
+        RPROF_RT(prt_loop1);
         if (team && tm == 1) finisher = own <= 0 && !cancelled;
         // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h;
         // a split group's by its forward-direction workgroup, of team A or B)
@@ -846,6 +892,25 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         // (the caller's stream joins eager_kernel's after this kernel, rvm_abi.hip run_logl)
         if (eager && threadIdx.x == 0)
             __hip_atomic_store(ef, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef RVM_PROFILE
+        if (t == (int)blockIdx.x && lane == 0 && (size_t)blockIdx.x * 8 + wv < RVM_RPROF_MAX_WAVES) {
+            unsigned long long* o = rvm_rprof + ((size_t)blockIdx.x * 8 + wv) * RVM_RPROF_SLOTS;
+            o[0] = prt_entry;
+            o[1] = prt_loop0;
+            o[2] = prt_loop1;
+            o[3] = __builtin_amdgcn_s_memrealtime();
+            o[4] = p_seg;
+            o[5] = p_epo;
+            o[6] = p_steps;
+            o[7] = pt_loop0 - pt_entry;
+            o[8] = pt_loop1 - pt_loop0;
+            o[9] = (unsigned long long)t | ((unsigned long long)tm << 16) | ((unsigned long long)(own + 1) << 20) |
+                   ((unsigned long long)(p_lvl + 1) << 24) | ((unsigned long long)(eager ? 1 : 0) << 28);
+            o[10] = p_pass;
+            o[11] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
+            o[12] = p_wait;
+        }
+#endif
     }
 }
 
@@ -1085,3 +1150,14 @@ hipError_t prepare_refine(const DevPlan& P) {
 #undef RVM_DISPATCH_NP
 
 }  // namespace rvm
+
+#ifdef RVM_PROFILE
+extern "C" int rvm_rprof_copy(void* host, size_t bytes) {
+    const size_t n = bytes < sizeof(rvm::rvm_rprof) ? bytes : sizeof(rvm::rvm_rprof);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(rvm::rvm_rprof), n, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int rvm_rprof_clear(void) {
+    static unsigned long long zero[RVM_RPROF_MAX_WAVES * RVM_RPROF_SLOTS];
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(rvm::rvm_rprof), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+}
+#endif
