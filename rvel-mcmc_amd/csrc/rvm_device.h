@@ -607,7 +607,10 @@ __device__ __forceinline__ bool lane_encountered(const Lane<NP>& s) {
 // scripts/probe/seg_bench.hip, profiles/r05g_seg_bench_g5.txt).  Off in every shipped kernel: the
 // ~55 cycles it adds to every other step outweigh that at the steps the passes take
 // (rvm_refine.hip RVM_REFINE_G5, rvm_logl.hip RVM_MAIN_G5).
-template <int NT, bool GATED, bool D3 = false, int NP, bool G5 = false>
+// KG, the guess: 0 fourth order, 1 fifth order (G5).  (A per-lane choice -- G5 on a lane's step after
+// one whose first Halley test failed -- cost more than either: 935 against 863 / 697 cycles per step
+// at e = 0.55, 689 against 620 / 680 at e = 0.22; profiles/r05o_seg_bench.txt)
+template <int NT, bool GATED, bool D3 = false, int NP, int KG = 0>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const VConsts& vk) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;
     double v2 = fma(s.vx, s.vx, s.vy * s.vy);
@@ -622,12 +625,15 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
     const double hs = 0.5 * sg;
     const double T3 = fma(hs, sg, (beta - g) * (1.0 / 6.0));
     const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
-    double x;
-    if constexpr (G5) {
+    auto guess5 = [&]() {
         const double s2 = sg * sg;
         const double T5 = fma(beta, fma(9.0 / 120.0, beta, fma(-19.0 / 120.0, g, 0.75 * s2)),
                               fma(g, fma(1.0 / 12.0, g, -0.875 * s2), 0.875 * (s2 * s2)));
-        x = u * fma(u, fma(u, fma(u, fma(u, T5, T4), T3), -hs), 1.0);
+        return u * fma(u, fma(u, fma(u, fma(u, T5, T4), T3), -hs), 1.0);
+    };
+    double x;
+    if constexpr (KG == 1) {
+        x = guess5();
     } else {
         x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
     }

@@ -54,14 +54,22 @@
 
 #include "rvm_walker.h"
 
-// the halving passes' drifts on the fifth-order Kepler guess (rvm_device.h drift G5): off.  It cuts a
-// lone wave's step on eccentric orbits at coarse resolution (933 -> 693 cycles at 32 steps per inner
-// orbit, e = 0.22) but costs ~55 cycles where the fourth-order guess already takes one Halley step
-// (scripts/probe/seg_bench.hip, profiles/r05g_seg_bench_g5.txt), and at the halving passes' finer
-// steps the latter dominates: steady state 1.422 -> 1.388 ms per iteration and config 4 295k -> 318k
-// chain-steps/s with it off (profiles/r05h_steady_ab_refine_g5.jsonl, r05h_config4_ab_refine_g5.jsonl; "default" there is G5 on)
-#ifndef RVM_REFINE_G5
-#define RVM_REFINE_G5 0
+// the halving passes' Kepler guess (rvm_device.h drift KG): 0 the fourth-order guess, 1 the fifth-order
+// one (G5).  G5 on every step
+// cuts a lone wave's step on eccentric orbits at coarse resolution (933 -> 693 cycles at 32 steps per
+// inner orbit, e = 0.22) but costs ~55 cycles where the fourth-order guess already takes one Halley
+// step (scripts/probe/seg_bench.hip, profiles/r05g_seg_bench_g5.txt); at the passes' finer steps the
+// latter dominates: steady state 1.388 ms per iteration and config 4 318k chain-steps/s with the
+// fourth-order guess against 1.422 / 295k with G5 (profiles/r05h_steady_ab_refine_g5.jsonl,
+// r05h_config4_ab_refine_g5.jsonl; "default" there is G5 on).  The refinement and eager kernels share
+// the setting: their bits must agree.
+#ifndef RVM_REFINE_GUESS
+#define RVM_REFINE_GUESS 0
+#endif
+// the blocks' count of list-size readers (the last one resets the lists): relaxed after the reads
+// have returned (1), or acquire-release (0: an agent-scope L2 writeback before, invalidate after)
+#ifndef RVM_REFINE_RELAXED_COUNT
+#define RVM_REFINE_RELAXED_COUNT 0
 #endif
 
 namespace rvm {
@@ -72,7 +80,8 @@ namespace rvm {
 // pass-loop end and task end; [4] shader cycles inside segments, [5] in epoch handling (star vx,
 // barrier, combiner), [6] steps integrated, [7] prologue cycles, [8] pass-loop cycles,
 // [9] task | team << 16 | (own + 1) << 20 | (last level + 1) << 24 | eager << 28, [10] passes
-// integrated, [11] HW_REG_HW_ID, [12] cycles in the eager / team / split waits and replays.
+// integrated, [11] HW_REG_HW_ID, [12] cycles in the eager / team / split waits and replays,
+// [13..15] cycles from entry to: the list sizes read, the schedule staged, the walker state set up.
 #define RVM_RPROF_SLOTS 16
 #define RVM_RPROF_MAX_WAVES 4096
 __device__ unsigned long long rvm_rprof[RVM_RPROF_MAX_WAVES * RVM_RPROF_SLOTS];
@@ -137,13 +146,21 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         for (int i = 0; i < 3; i++) s_n[i] = __hip_atomic_load(P.rq_n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long g0 = __hip_atomic_load(P.gen_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_gen = g0;
+#if RVM_REFINE_RELAXED_COUNT
+        // (the three loads have returned before the count is bumped: the last block's reset
+        // cannot overtake them; no release / acquire -- an L2 writeback and invalidate -- needed)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int done = __hip_atomic_fetch_add(P.rq_n + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
         const int done = __hip_atomic_fetch_add(P.rq_n + 3, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         if (done == (int)gridDim.x - 1) {
             for (int i = 0; i < 4; i++) __hip_atomic_store(P.rq_n + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (!eager) __hip_atomic_store(P.gen_dev, g0 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
+    RPROF_T(pt_lists);
     const unsigned long long gen = s_gen;
     const int nq[3] = {s_n[0], s_n[1], s_n[2]};
     const int gq0 = (nq[0] + WPB - 1) / WPB, gq1 = (nq[1] + WPB - 1) / WPB, gq2 = (nq[2] + WPB - 1) / WPB;
@@ -209,6 +226,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             bn[ED + i] = SD.obs_idx[i];
         }
     }
+    RPROF_T(pt_sched);
     const bool stretch = sa.c != nullptr;
     const bool mh = sa.mh_scale != nullptr;
     const bool mapped = stretch || mh || sa.fd_x != nullptr;
@@ -278,6 +296,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         int status = RVM_STATUS_OK;
         double e2w;
         walker_setup<NP, D3, L>(rowv, pl_idx, hill_factor, s, status, e2w);
+        RPROF_T(pt_setup);
         __syncthreads();  // (the previous group's LDS state is no longer read)
         if (wv == 0) {
             s_init[0][lane] = s.rx;
@@ -483,7 +502,15 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                     const double pv = cmb && here && hasp && !bfirst ? pp[(size_t)e * P.lvx_stride] : 0.0;  // (issued early)
                     const int ns = __builtin_amdgcn_readfirstlane(work && here ? r_n[e] * m_r : 0);
                     RPROF_T(pt_s0);
-                    if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_G5 != 0>(s, kq, r_len[e] * sc, ns, nt_r);
+                    if (ns > 0) {
+                        // (team B's first pass stops part-way once team A has finished the group: the
+                        // barrier below then breaks every wave out at this epoch)
+                        if (bfirst)
+                            (void)segment_gated_c<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r, tflag,
+                                                                                 nullptr, (gen << 8) | 2ull);
+                        else
+                            segment_gated<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r);
+                    }
                     RPROF_T(pt_s1);
 #ifdef RVM_PROFILE
                     p_seg += pt_s1 - pt_s0;
@@ -909,6 +936,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             o[10] = p_pass;
             o[11] = (unsigned long long)(unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID
             o[12] = p_wait;
+            o[13] = pt_lists - pt_entry;
+            o[14] = pt_sched - pt_entry;
+            o[15] = pt_setup - pt_entry;
         }
 #endif
     }
@@ -986,7 +1016,10 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     bool cancelled = false;
     for (int e = 0; e < Er; e++) {
         const int ns = __builtin_amdgcn_readfirstlane(work ? SR.seg_n[e] * m_r : 0);
-        if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_G5 != 0>(s, kq, SR.seg_h1[e] * sc, ns, nt_r);
+        // (cancels are seen at the epochs: the segment-level cancel of team B's passes,
+        // segment_gated_c, measured slower here -- config 4 0.645 -> 0.66 ms median step,
+        // profiles/r05r_config4_ab_cancel.jsonl)
+        if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_GUESS>(s, kq, SR.seg_h1[e] * sc, ns, nt_r);
         if (work) {
             const double v0 = star_vx<NP, L>(s);
             if (pl_idx == 0) s_rv[e & 1][k_u][slot] = v0;

@@ -16,26 +16,26 @@ namespace rvm {
 // segment's opening half kick, and leaves holding the one at the next epoch.  (The step loop is
 // unrolled by hand: the compiler will not unroll a runtime trip count around the convergent DPP /
 // ballot operations.)
-template <int NT, bool GATED, bool D3, int NP, int L, bool G5 = false>
+template <int NT, bool GATED, bool D3, int NP, int L, int KG = 0>
 __device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, bool& bad) {
     lane_set_step(s, h);
     const VConsts vk = vconsts_for<NT>();  // loop-invariant VGPR constants
     kick_apply<NP, true, D3>(s, kp);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
-        drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
-        drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
     }
     if (j < ns - 1) {
-        drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
     }
-    drift<NT, GATED, D3, NP, G5>(s, h, bad, vk);
+    drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
     kp = kick_prep<NP, L, D3>(s, vk.c1875);
     kick_apply<NP, true, D3>(s, kp);
 }
@@ -44,7 +44,7 @@ __device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, dou
 // of the wave had a step that needs the general solver, restore the segment's initial state and
 // redo it gated.  Used on the fine levels, where such steps are rare.  Returns whether the
 // segment was redone (wave-uniform).  Either way every lane ends bit-identical to a gated run.
-template <int NT, bool SPEC, bool D3, int NP, int L, bool G5 = false>
+template <int NT, bool SPEC, bool D3, int NP, int L, int KG = 0>
 __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int& redo) {
     bool bad = false;
     if constexpr (SPEC) {
@@ -52,7 +52,7 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h,
         const double rz = s.rz, vz = s.vz;
         const uint64_t encm = s.encm;
         const KickPrep<NP> kp0 = kp;
-        segment_steps<NT, false, D3, NP, L, G5>(s, kp, h, ns, bad);
+        segment_steps<NT, false, D3, NP, L, KG>(s, kp, h, ns, bad);
         if (__builtin_expect(ballot(bad) != 0, 0)) {
 #ifdef RVM_PROFILE
             redo++;
@@ -67,27 +67,27 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h,
             s.ir = ir;
             s.encm = encm;
             kp = kp0;
-            segment_steps<NT, true, D3, NP, L, G5>(s, kp, h, ns, bad);
+            segment_steps<NT, true, D3, NP, L, KG>(s, kp, h, ns, bad);
             return true;
         }
     } else {
-        segment_steps<NT, true, D3, NP, L, G5>(s, kp, h, ns, bad);
+        segment_steps<NT, true, D3, NP, L, KG>(s, kp, h, ns, bad);
     }
     (void)redo;
     return false;
 }
 
-// a gated segment with the Stumpff series length of the level (nt: 6, 7 or 8); G5: the fifth-order
-// Kepler guess (rvm_device.h drift)
-template <bool D3, int NP, int L, bool G5 = false>
+// a gated segment with the Stumpff series length of the level (nt: 6, 7 or 8); KG: the Kepler guess
+// (rvm_device.h drift: 0 fourth order, 1 fifth)
+template <bool D3, int NP, int L, int KG = 0>
 __device__ __forceinline__ void segment_gated(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int nt) {
     int unused = 0;
     if (nt <= 6)
-        segment<6, false, D3, NP, L, G5>(s, kp, h, ns, unused);
+        segment<6, false, D3, NP, L, KG>(s, kp, h, ns, unused);
     else if (nt == 7)
-        segment<7, false, D3, NP, L, G5>(s, kp, h, ns, unused);
+        segment<7, false, D3, NP, L, KG>(s, kp, h, ns, unused);
     else
-        segment<8, false, D3, NP, L, G5>(s, kp, h, ns, unused);
+        segment<8, false, D3, NP, L, KG>(s, kp, h, ns, unused);
 }
 
 // kernel parameter row r of walker w: from the SoA input, or (fused sampler step) the row's fixed
@@ -257,6 +257,65 @@ struct SpinClock {
         return __builtin_amdgcn_s_memrealtime() - last > ticks;
     }
 };
+
+// A gated segment (segment_gated) that a partner can stop part-way: the work a team B or an eager
+// block does speculatively (rvm_refine.hip) is cancelled through a word that reaches `tag`.  Polled
+// at the epochs alone, a cancel waited for the rest of the segment -- up to ~100 us on the passes'
+// long segments, which kept the refinement launch open after team A had finished every walker
+// (scripts/probe/refine_prof.py).  The words (c1 may be null) are loaded every CH steps, each load
+// tested after the CH steps that follow it (no wait on the step chain).  Returns false when cancelled:
+// the lanes' state is then partial, and the caller discards it.  A segment that runs to its end
+// computes exactly segment_gated's bits.
+template <int NT, bool D3, int NP, int L, int KG, int CH = 64>
+__device__ __forceinline__ bool segment_steps_c(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, const gu64* c0,
+                                                const gu64* c1, unsigned long long tag) {
+    bool bad = false;
+    lane_set_step(s, h);
+    const VConsts vk = vconsts_for<NT>();
+    kick_apply<NP, true, D3>(s, kp);
+    // (unconditional loads: a load under a branch is waited for where the branches join; c1 null
+    // reads c0 twice)
+    const gu64* w1 = c1 ? c1 : c0;
+    auto load = [](const gu64* c) { return __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    // the ns - 1 drift-kick pairs in chunks of CH steps, each chunk's loop the plain segment_steps
+    // loop; the words are loaded before a chunk and compared after it.  A compare before the chunk
+    // made the wave wait for the load there, a test inside the step loop cost ~60 cycles per step, and
+    // chunks of 16 (32) steps still ~17 (~3) -- the agent-scope load outlasting the chunk; 64 steps
+    // cost nothing measurable and bound a cancel's latency at ~17 us (scripts/probe/seg_bench.hip,
+    // profiles/r05q_seg_bench_cancel_chunks.txt)
+    int left = ns - 1;
+    while (left >= 2) {
+        const unsigned long long a = load(c0), b = load(w1);
+        const int c = left < CH ? (left & ~1) : CH;
+        for (int j = 0; j < c; j += 2) {
+            drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+            kp = kick_prep<NP, L, D3>(s, vk.c1875);
+            kick_apply<NP, false, D3>(s, kp);
+            drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+            kp = kick_prep<NP, L, D3>(s, vk.c1875);
+            kick_apply<NP, false, D3>(s, kp);
+        }
+        left -= c;
+        if (__builtin_amdgcn_readfirstlane((int)((a == tag) | (b == tag)))) return false;
+    }
+    if (left == 1) {
+        drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+        kp = kick_prep<NP, L, D3>(s, vk.c1875);
+        kick_apply<NP, false, D3>(s, kp);
+    }
+    drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+    kp = kick_prep<NP, L, D3>(s, vk.c1875);
+    kick_apply<NP, true, D3>(s, kp);
+    return true;
+}
+
+template <bool D3, int NP, int L, int KG = 0>
+__device__ __forceinline__ bool segment_gated_c(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int nt,
+                                                const gu64* c0, const gu64* c1, unsigned long long tag) {
+    if (nt <= 6) return segment_steps_c<6, D3, NP, L, KG>(s, kp, h, ns, c0, c1, tag);
+    if (nt == 7) return segment_steps_c<7, D3, NP, L, KG>(s, kp, h, ns, c0, c1, tag);
+    return segment_steps_c<8, D3, NP, L, KG>(s, kp, h, ns, c0, c1, tag);
+}
 
 // ---- the two directions of a walker meet (rvm_logl.hip finish) -------------------------------
 // One 64-bit slot per walker (plan workspace, RVM_SLOT_EMPTY between launches).  The direction that

@@ -23,7 +23,7 @@ SLOTS, MAXW = 16, 4096
 
 
 def main():
-    _lib.LIB_PATH = os.path.join(ROOT, "scripts", "probe", "librvmcmc_prof.so")
+    _lib.LIB_PATH = os.environ.get("RVM_LIB_PATH") or os.path.join(ROOT, "scripts", "probe", "librvmcmc_prof.so")
     lib = _lib.load()
     lib.rvm_rprof_copy.argtypes = [C.c_void_p, C.c_size_t]
     from rvmcmc.ensemble import EnsembleSampler
@@ -76,6 +76,24 @@ def main():
             out["busy_cyc_per_step_max"] = float(cps.max())
             out["busy_steps_max"] = int(busy[:, 6].max())
             out["busy_prologue_us_median"] = float(np.median(busy[:, 1] - busy[:, 0]) / 100.0)
+            # cycles from entry: list sizes read, schedule staged, walker state set up, pass loop
+            out["busy_prologue_kcyc_median"] = [float(np.median(busy[:, c]) / 1e3) for c in (13, 14, 15, 7)]
+            crit = busy[int(np.argmax(busy[:, 6]))]
+            out["critical"] = {"steps": int(crit[6]), "cyc_per_step": float(crit[4]) / max(1, crit[6]),
+                               "seg_kcyc": crit[4] / 1e3, "epoch_kcyc": crit[5] / 1e3, "wait_kcyc": crit[12] / 1e3,
+                               "prologue_us": float(crit[1] - crit[0]) / 100.0, "loop_us": float(crit[2] - crit[1]) / 100.0,
+                               "level": int((crit[9] >> 24) & 0xF) - 1, "team": int((crit[9] >> 16) & 0xF)}
+        # per team (0 = A: pass 1, 1 = B: pass 2 concurrently, then the rest): when its last wave
+        # ended, and its longest-integrating wave's breakdown
+        for tm in (0, 1):
+            bt = b[((b[:, 9] >> 16) & 0xF) == tm]
+            if not len(bt):
+                continue
+            wt = bt[int(np.argmax(bt[:, 6]))]
+            out[f"team{tm}"] = {"end_us": us(bt[:, 3].max() - t_launch0), "loop_end_us": us(bt[:, 2].max() - t_launch0),
+                                "steps": int(wt[6]), "seg_kcyc": wt[4] / 1e3, "epoch_kcyc": wt[5] / 1e3,
+                                "wait_kcyc": wt[12] / 1e3, "loop_us": us(wt[2] - wt[1]),
+                                "loop_start_us": us(wt[1] - t_launch0), "passes": int(wt[10])}
         rows.append(out)
         print(json.dumps(out), flush=True)
     if rows:
@@ -89,7 +107,8 @@ def main():
                           "slowest_epoch_share_median": float(np.median(
                               [s["epoch_kcyc"] / max(1e-9, s["seg_kcyc"] + s["epoch_kcyc"] + s["wait_kcyc"]) for s in S])),
                           "slowest_wait_kcyc_median": float(np.median([s["wait_kcyc"] for s in S])),
-                          "slowest_ghz_median": float(np.median([s["ghz"] for s in S]))}), flush=True)
+                          "slowest_ghz_median": float(np.median([s["ghz"] for s in S])),
+                          "lib": os.path.basename(_lib.LIB_PATH)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -13,11 +13,12 @@
 #include "../../rvel-mcmc_amd/csrc/rvm_walker.h"
 using namespace rvm;
 
-#define NSEG 64
-#define NS 28
+#define NSEG 16
+#define NS 140
 
-template <int NT, bool GATED, bool G5 = false>
-__global__ __launch_bounds__(64) void seg_bench(double ecc, double h, long long* cyc, double* sink, int* nbad) {
+template <int NT, bool GATED, int G5 = 0, int CAN = 0>
+__global__ __launch_bounds__(64) void seg_bench(double ecc, double h, long long* cyc, double* sink, int* nbad,
+                                                const unsigned long long* flag) {
     const int lane = threadIdx.x & 63;
     const int slot = lane >> 1, p = lane & 1;
     // S2 (mcmc_benchmark_mh.py:32) with planet 1's eccentricity set to ecc (h = ecc sin w, k = ecc cos w)
@@ -34,7 +35,13 @@ __global__ __launch_bounds__(64) void seg_bench(double ecc, double h, long long*
     bool bad = false;
     __syncthreads();
     const long long t0 = clock64();
-    for (int g = 0; g < NSEG; g++) segment_steps<NT, GATED, false, 2, 2, G5>(s, kp, h, NS, bad);
+    if constexpr (CAN) {  // (the cancellable gated segment: a flag that never reaches the tag)
+        for (int g = 0; g < NSEG; g++)
+            (void)segment_steps_c<NT, false, 2, 2, G5, CAN == 1 ? 16 : (CAN == 2 ? 32 : 64)>(s, kp, h, NS,
+                                                                                          (const gu64*)flag, nullptr, 1ull);
+    } else {
+        for (int g = 0; g < NSEG; g++) segment_steps<NT, GATED, false, 2, 2, G5>(s, kp, h, NS, bad);
+    }
     const long long t1 = clock64();
     sink[blockIdx.x * 64 + lane] = s.rx + s.vy;
     const uint64_t b = ballot(bad);
@@ -44,16 +51,21 @@ __global__ __launch_bounds__(64) void seg_bench(double ecc, double h, long long*
     }
 }
 
-template <int NT, bool GATED, bool G5 = false>
+template <int NT, bool GATED, int G5 = 0, int CAN = 0>
 static void run(const char* name, double ecc, double h, long long* cyc, double* sink, int* nbad) {
     const int blocks = 256;
-    seg_bench<NT, GATED, G5><<<blocks, 64>>>(ecc, h, cyc, sink, nbad);
+    static unsigned long long* flag = nullptr;
+    if (!flag) {
+        hipMalloc(&flag, sizeof(unsigned long long));
+        hipMemset(flag, 0, sizeof(unsigned long long));
+    }
+    seg_bench<NT, GATED, G5, CAN><<<blocks, 64>>>(ecc, h, cyc, sink, nbad, flag);
     hipDeviceSynchronize();
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
     hipEventRecord(e0);
-    seg_bench<NT, GATED, G5><<<blocks, 64>>>(ecc, h, cyc, sink, nbad);
+    seg_bench<NT, GATED, G5, CAN><<<blocks, 64>>>(ecc, h, cyc, sink, nbad, flag);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms;
@@ -86,13 +98,15 @@ int main(int argc, char** argv) {
         const double h = P1 / spo;
         printf("-- e %.2f, steps per inner orbit %.0f\n", ecc, spo);
         run<6, true>("gated<6>", ecc, h, cyc, sink, nbad);
-        run<6, true, true>("gated<6> G5", ecc, h, cyc, sink, nbad);
+        run<6, true, 1>("gated<6> G5", ecc, h, cyc, sink, nbad);
+        run<6, true, 0, 1>("gated<6> cancellable", ecc, h, cyc, sink, nbad);
+        run<6, true, 0, 2>("gated<6> cancel 32", ecc, h, cyc, sink, nbad);
+        run<6, true, 0, 3>("gated<6> cancel 64", ecc, h, cyc, sink, nbad);
         run<6, false>("ungated<6>", ecc, h, cyc, sink, nbad);
-        run<6, false, true>("ungated<6> G5", ecc, h, cyc, sink, nbad);
         run<7, true>("gated<7>", ecc, h, cyc, sink, nbad);
-        run<7, true, true>("gated<7> G5", ecc, h, cyc, sink, nbad);
+        run<7, true, 0, 1>("gated<7> cancellable", ecc, h, cyc, sink, nbad);
         run<8, true>("gated<8>", ecc, h, cyc, sink, nbad);
-        run<8, true, true>("gated<8> G5", ecc, h, cyc, sink, nbad);
+        run<8, true, 0, 1>("gated<8> cancellable", ecc, h, cyc, sink, nbad);
     }
     return 0;
 }
