@@ -81,8 +81,10 @@ namespace rvm {
 // barrier, combiner), [6] steps integrated, [7] prologue cycles, [8] pass-loop cycles,
 // [9] task | team << 16 | (own + 1) << 20 | (last level + 1) << 24 | eager << 28, [10] passes
 // integrated, [11] HW_REG_HW_ID, [12] cycles in the eager / team / split waits and replays,
-// [13..15] cycles from entry to: the list sizes read, the schedule staged, the walker state set up.
-#define RVM_RPROF_SLOTS 16
+// [13..15] cycles from entry to: the list sizes read, the schedule staged, the walker state set up;
+// [16], [17] to the slot's walker index and stretch draws, and its parameter rows, loaded (this build
+// waits for each there).
+#define RVM_RPROF_SLOTS 20
 #define RVM_RPROF_MAX_WAVES 4096
 __device__ unsigned long long rvm_rprof[RVM_RPROF_MAX_WAVES * RVM_RPROF_SLOTS];
 #define RPROF_T(v) const unsigned long long v = __builtin_readcyclecounter()
@@ -289,9 +291,17 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
         int kind = 0, wk = wo, jst = 0, jp = 0;
         double zst = 0.0, zp = 0.0;
         if (stretch) stretch_slot(sa, wo, kind, wk, zst, jst, zp, jp);
+#ifdef RVM_PROFILE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (timing build: the slot's index in)
+#endif
+        RPROF_T(pt_slot);
         double rowv[R];
 #pragma unroll
         for (int r = 0; r < R; r++) rowv[r] = walker_param(mapped, params, W, wk, sa, r, zst, jst, kind, zp, jp);
+#ifdef RVM_PROFILE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // (timing build: the rows in)
+#endif
+        RPROF_T(pt_rows);
         Lane<NP> s;
         int status = RVM_STATUS_OK;
         double e2w;
@@ -939,6 +949,8 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
             o[13] = pt_lists - pt_entry;
             o[14] = pt_sched - pt_entry;
             o[15] = pt_setup - pt_entry;
+            o[16] = pt_slot - pt_entry;
+            o[17] = pt_rows - pt_entry;
         }
 #endif
     }

@@ -19,7 +19,7 @@ import torch  # noqa: E402
 from conftest import S2_PLANETS  # noqa: E402
 from rvmcmc import _lib, engine  # noqa: E402
 
-SLOTS, MAXW = 16, 4096
+SLOTS, MAXW = 20, 4096
 
 
 def main():
@@ -76,8 +76,9 @@ def main():
             out["busy_cyc_per_step_max"] = float(cps.max())
             out["busy_steps_max"] = int(busy[:, 6].max())
             out["busy_prologue_us_median"] = float(np.median(busy[:, 1] - busy[:, 0]) / 100.0)
-            # cycles from entry: list sizes read, schedule staged, walker state set up, pass loop
-            out["busy_prologue_kcyc_median"] = [float(np.median(busy[:, c]) / 1e3) for c in (13, 14, 15, 7)]
+            # cycles from entry: list sizes read, schedule staged, slot index + draws, rows loaded,
+            # walker state set up, pass loop
+            out["busy_prologue_kcyc_median"] = [float(np.median(busy[:, c]) / 1e3) for c in (13, 14, 16, 17, 15, 7)]
             crit = busy[int(np.argmax(busy[:, 6]))]
             out["critical"] = {"steps": int(crit[6]), "cyc_per_step": float(crit[4]) / max(1, crit[6]),
                                "seg_kcyc": crit[4] / 1e3, "epoch_kcyc": crit[5] / 1e3, "wait_kcyc": crit[12] / 1e3,
