@@ -43,7 +43,7 @@ for step in $STEPS; do
       for rep in 1 2; do
         for lib in default ${AB_LIBS:-scripts/probe/librvmcmc_mg5.so}; do
           if [ "$lib" = default ]; then lp=""; else lp=$lib; fi
-          RVM_LIB_PATH=$lp timeout -k 10 200 python -u scripts/configs_bench.py 4 \
+          RVM_LIB_PATH=$lp timeout -k 10 200 python -u scripts/configs_bench.py ${ABCFG:-4} \
             | sed "s|^{|{\"lib\": \"${lib}\", |" >> gpurun_out/${T}_c4ab.jsonl 2>> gpurun_out/${T}_c4ab.err || exit 1
         done
       done
