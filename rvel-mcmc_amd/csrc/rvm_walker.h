@@ -118,15 +118,21 @@ __device__ __forceinline__ void stretch_slot(const StretchArgs& sa, int wl, int&
     const int nsp = sa.n_spec;
     kind = nsp > 0 ? (wl < nsp ? 0 : (wl < 2 * nsp ? 1 : 2)) : 0;
     wk = wl - kind * nsp;
-    zp = 0.0;
-    jp = 0;
-    if (kind == 0) {
-        stretch_draw(sa.seed, (uint64_t)(sa.s0_begin + wk), sa.iteration, sa.half, sa.a, sa.n1, z, j);
-    } else {
-        stretch_draw(sa.seed, (uint64_t)(sa.s1_begin + wk), sa.iteration, 1u, sa.a, sa.n1, z, j);
-        // the partner's own draws (half 0's keys are its global indices 0 .. n1-1)
-        if (kind == 2) stretch_draw(sa.seed, (uint64_t)j, sa.iteration, 0u, sa.a, sa.n1, zp, jp);
-    }
+    // (one call for the slot's own draw, each result in a local of its own: two calls writing z, j
+    // from both branches were merged into one through a select of their addresses, which put z, j
+    // in scratch -- 56 B per lane in the likelihood kernel)
+    const uint64_t key = kind == 0 ? (uint64_t)(sa.s0_begin + wk) : (uint64_t)(sa.s1_begin + wk);
+    double z0;
+    int j0;
+    stretch_draw(sa.seed, key, sa.iteration, kind == 0 ? sa.half : 1u, sa.a, sa.n1, z0, j0);
+    z = z0;
+    j = j0;
+    double z1 = 0.0;
+    int j1 = 0;
+    // the partner's own draws (half 0's keys are its global indices 0 .. n1-1)
+    if (kind == 2) stretch_draw(sa.seed, (uint64_t)j0, sa.iteration, 0u, sa.a, sa.n1, z1, j1);
+    zp = z1;
+    jp = j1;
 }
 
 // ---- setup_sim (state.py:36-47): prior, Pal -> heliocentric (own planet) -> Jacobi, Hill exit ----
