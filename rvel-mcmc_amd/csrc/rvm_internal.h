@@ -10,6 +10,9 @@ namespace rvm {
 // (levels wait for the combiner beyond it); the dynamic LDS request plus the kernel's static LDS
 // (read with hipFuncGetAttributes at launch) must stay within the CU's 160 KB
 constexpr int RVM_LS_RING = 64;
+// LDS-coupled layouts (one or two groups per block): epochs of the levels' star vx a group's ring
+// holds (rvm_logl.hip; the levels wait for the combiner beyond it)
+constexpr int RVM_LC_RING = 16;
 constexpr int RVM_LDS_PER_CU = 160 * 1024;
 // adaptive resolution: lane state at t = 0 kept in LDS for the refinement passes, per walker group
 // (rx, ry, vx, vy, rz, vz, r, ir of each of the 64 lanes)

@@ -185,12 +185,17 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     const bool valid = w < W;
     const int wl = valid ? w : (W - 1);
 
-    __shared__ double s_rv_all[2][2][RVM_MAX_LEVELS][64];
     // level-split hand-off inside a type-A block (unit ul = wv & 1; local level slot ks = 0, 1, 2
     // for levels 3, 2, 0): epochs published per level, epochs consumed by the combiner, the levels'
     // encounter / prior flags; the RVs themselves sit in the ring after the schedule (s_sched)
     __shared__ int s_lvp[2][4];
     __shared__ int s_cprog[2];
+    // LDS-coupled layouts (round 5): each group's levels publish their star vx per epoch in a ring of
+    // RVM_LC_RING epochs after the stretch staging and the lanes' t = 0 state (dynamic LDS,
+    // [group][epoch % ring][level (nl + 1: the extension)][WPB]) and their progress here; the group's combiner (level 0's
+    // wave) combines epoch e once every level has published it and publishes its own progress
+    __shared__ int s_lcp[2][RVM_MAX_LEVELS + 1];
+    __shared__ int s_lcc[2];
     __shared__ int s_encl[2][4][64];
     // head -> tail hand-off of a split level (slot hs): the lanes' dynamic state, the wave's
     // encounter mask and speculation state, and the ready flag
@@ -207,7 +212,6 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // (the early certain-reject test of the refinement team: the main pass's estimate and the
     // concurrent extension's chi2 and change, per unit and walker slot)
     __shared__ double s_fx[1][2][64];
-    double(*s_rv)[RVM_MAX_LEVELS][64] = s_rv_all[grp];
     int(*s_enc)[64] = s_enc_all[grp];
     // this direction's epoch schedule, staged once into LDS (wave-uniform broadcast reads later)
     extern __shared__ double s_sched[];  // [E] seg_h1 | [E] obs_rv | [E] obs_s2 | [E] (seg_n, obs_idx)
@@ -336,6 +340,8 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
 
     PROF_T(t_p3);  // lane constants, encounter check at t = 0
     if (!dec) {
+        if (threadIdx.x < 2 * (RVM_MAX_LEVELS + 1)) (&s_lcp[0][0])[threadIdx.x] = 0;
+        if (threadIdx.x < 2) s_lcc[threadIdx.x] = 0;
         if (i0 < E) {
             l_len[i0] = st_h;
             l_rv[i0] = st_rv;
@@ -391,7 +397,11 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     // a head runs first (its tail, on another SIMD, cannot start before it ends): it publishes more
     // remaining work than any whole level has
     int done = 0;
-    if (dec && lane == 0) {
+    // (LDS-coupled layouts, round 5: waves wv and wv ^ 4 share a SIMD -- the cx layout's levels 1 and
+    // 0, the two-group layout's mirrored pairs -- and without the per-epoch barrier run free, so they
+    // balance their issue priority by remaining work as the level-split waves do)
+    const bool lc_pair = !dec && (wv ^ 4) < (int)(blockDim.x >> 6);
+    if ((dec || lc_pair) && lane == 0) {
         s_rem[wv] = rem;
         s_done[wv] = 0;
     }
@@ -460,6 +470,68 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         // encounter test repeats on positions the head already tested)
         kp = kick_prep<NP, L, D3>(s, 1.875);
     }
+    // (LDS-coupled) this group's ring of the levels' star vx, after the lanes' t = 0 state
+    const int NLC = nl + (cx ? 1 : 0);  // levels that publish (the extension wave too)
+    const int RC = emax2 < RVM_LC_RING ? emax2 : RVM_LC_RING;
+    double* lring = dec ? nullptr
+                        : l_init + (P.rmax > 0 ? (size_t)G * RVM_INIT_DOUBLES : 0) +
+                              (size_t)grp * RC * (nl + 1) * WPB;
+    // (LDS-coupled) the combiner's side: the epochs every other level has published (wave-uniform),
+    // a bounded wait for epoch ec, and the combine of epoch ec -- Richardson RV, chi2, estimate, the
+    // extension's sums, the RV for a refinement -- in epoch order (the bits of the barrier-coupled
+    // loop), then its progress for the writers
+    int next_c = 0;  // (combiner) the next epoch to combine
+    auto lc_min = [&]() {
+        int mn = 1 << 30;
+        for (int k = 1; k < NLC; k++)
+            mn = min(mn, __hip_atomic_load(&s_lcp[grp][k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        return __builtin_amdgcn_readfirstlane(mn);
+    };
+    auto lc_wait = [&](const int ec) {
+        int seen = -1;
+        clk.restart();
+        for (;;) {
+            const int mn = lc_min();
+            if (mn > ec) return;
+            if (mn != seen) {
+                seen = mn;
+                clk.restart();
+            } else if (clk.expired(P.spin_ticks)) {
+                wfault = true;
+                return;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    };
+    auto lc_combine = [&](const int ec) {
+        const double* rv_e = lring + (size_t)(ec % RC) * (nl + 1) * WPB;
+        if (lane < WPB) {  // lane `lane` of level 0's wave owns walker slot `lane`
+            double rvx = 0.0, rv3 = 0.0;
+            for (int k = 0; k < nl; k++) rvx += P.lw[k] * rv_e[(size_t)k * WPB + lane];
+            for (int k = 1; k < nl; k++) rv3 += P.lw3[k] * rv_e[(size_t)k * WPB + lane];
+            const double r = rvx - l_rv[ec];
+            chi2 += (r * r) / l_s2[ec];
+            est += fabs((rvx - rv3) * (r + (rv3 - l_rv[ec]))) / l_s2[ec];
+            const int wo = w0 + lane;
+            if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[ec] * W + wo] = rvx;
+            if (P.ext_mult > 0 && wo < W) {  // the RV and the extension's partial sum, for a refinement
+                double s5 = 0.0;
+                for (int k = 0; k < nl; k++) s5 += P.lw5[k] * rv_e[(size_t)k * WPB + lane];
+                const size_t xi = (size_t)(d * P.lvx_emax + ec) * P.lvx_stride + wo;
+                if (cx) {  // (extend_pass's sums, from the extension wave's value of this epoch)
+                    const double r5 = s5 + P.lw5[nl] * rv_e[(size_t)nl * WPB + lane];
+                    const double q = r5 - l_rv[ec];
+                    c5x += (q * q) / l_s2[ec];
+                    ddx += fabs((r5 - rvx) * (q + (rvx - l_rv[ec]))) / l_s2[ec];
+                } else {
+                    P.lvx[xi] = s5;
+                }
+                P.rvp[xi] = rvx;
+            }
+        }
+        // (the combiner has read epoch ec: its ring slot may be rewritten)
+        if (lane == 0) __hip_atomic_store(&s_lcc[grp], ec + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     int n1 = e_lo < E ? l_n[e_lo] : 0;
     double len = e_lo < E ? l_len[e_lo] : 0.0;
     for (int e = e_lo; e < E_int; e++) {
@@ -469,7 +541,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         const int ns = n1 * mult;
         // the partner's remaining work, read now and used after the segment (latency hidden)
         int rem_oth = 0, done_oth = 0;
-        if (dec) {
+        if (dec || lc_pair) {
             rem_oth = __hip_atomic_load(s_rem + (wv ^ 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             done_oth = __hip_atomic_load(s_done + (wv ^ 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -546,31 +618,46 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
                 rslot = rslot + 1 == RING ? 0 : rslot + 1;
             }
         } else {
-            if (pl_idx == 0) s_rv[e & 1][lvl][slot] = v0;
-            __syncthreads();
-        }
-        if (!dec && lvl == 0 && lane < WPB) {  // lane `lane` of wave 0 owns walker slot `lane`
-            double rvx = 0.0, rv3 = 0.0;
-            for (int k = 0; k < nl; k++) rvx += P.lw[k] * s_rv[e & 1][k][lane];
-            for (int k = 1; k < nl; k++) rv3 += P.lw3[k] * s_rv[e & 1][k][lane];
-            const double r = rvx - l_rv[e];
-            chi2 += (r * r) / l_s2[e];
-            est += fabs((rvx - rv3) * (r + (rv3 - l_rv[e]))) / l_s2[e];
-            const int wo = w0 + lane;
-            if (rv_out != nullptr && wo < W) rv_out[(size_t)l_idx[e] * W + wo] = rvx;
-            if (P.ext_mult > 0 && wo < W) {  // the RV and the extension's partial sum, for a refinement
-                double s5 = 0.0;
-                for (int k = 0; k < nl; k++) s5 += P.lw5[k] * s_rv[e & 1][k][lane];
-                const size_t xi = (size_t)(d * P.lvx_emax + e) * P.lvx_stride + wo;
-                if (cx) {  // (extend_pass's sums, from the extension wave's value of this epoch)
-                    const double r5 = s5 + P.lw5[nl] * s_rv[e & 1][nl][lane];
-                    const double q = r5 - l_rv[e];
-                    c5x += (q * q) / l_s2[e];
-                    ddx += fabs((r5 - rvx) * (q + (rvx - l_rv[e]))) / l_s2[e];
-                } else {
-                    P.lvx[xi] = s5;
+            if (lc_pair) {
+                rem -= ns * wcost;
+                if (lane == 0) __hip_atomic_store(s_rem + wv, rem, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                const int ro = __builtin_amdgcn_readfirstlane(rem_oth), rm = __builtin_amdgcn_readfirstlane(rem);
+                if (__builtin_amdgcn_readfirstlane((int)(ro < rm)))
+                    __builtin_amdgcn_s_setprio(2);
+                else
+                    __builtin_amdgcn_s_setprio(1);
+            }
+            // publish this epoch in the group's ring.  A whole ring ahead of the combiner: a level
+            // waits (only when E > RC; a wait without progress for spin_ticks gives up:
+            // RVM_ENC_FAULT), the combiner itself combines the oldest epochs first
+            if (lvl == 0) {
+                while (!wfault && e - next_c >= RC) {
+                    lc_wait(next_c);
+                    if (!wfault) lc_combine(next_c++);
                 }
-                P.rvp[xi] = rvx;
+            } else if (E > RC && !wfault && e >= RC) {
+                int seen = -1;
+                for (;;) {
+                    const int cp = __builtin_amdgcn_readfirstlane(
+                        __hip_atomic_load(&s_lcc[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+                    if (e - cp < RC) break;
+                    if (cp != seen) {
+                        seen = cp;
+                        clk.restart();
+                    } else if (clk.expired(P.spin_ticks)) {
+                        wfault = true;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(4);
+                }
+            }
+            if (pl_idx == 0) lring[((size_t)(e % RC) * (nl + 1) + lvl) * WPB + slot] = v0;
+            if (lane == 0) __hip_atomic_store(&s_lcp[grp][lvl], e + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lvl == 0 && !wfault) {
+                // the combiner integrates on and combines, without waiting, the epochs every level
+                // has published (the rest after its last segment)
+                const int mn = min(lc_min(), e + 1);
+                while (next_c < mn) lc_combine(next_c++);
             }
         }
         n1 = n1_next;
@@ -580,6 +667,12 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
         t_seg += tb - ta;
         t_epo += tc - tb;
 #endif
+    }
+    if (!dec && lvl == 0) {  // (LDS-coupled) the combiner: the epochs the others published later
+        while (!wfault && next_c < E_int) {
+            lc_wait(next_c);
+            if (!wfault) lc_combine(next_c++);
+        }
     }
     const int encflag = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0) |
                         (status == RVM_STATUS_PRIOR ? 2 : 0) | (wfault ? RVM_ENC_FAULT : 0);
@@ -1278,7 +1371,10 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     const size_t rows = (size_t)(D3V ? 7 : 5) * NPV;
     const bool fused = sa.c != nullptr || sa.mh_scale != nullptr;
     const size_t init = P.rmax > 0 ? (size_t)RVM_INIT_DOUBLES * sizeof(double) : 0;  // per group / unit
-    size_t smem = (size_t)emax * 4 * sizeof(double) + (fused ? (rows + 3) * G * wpb * sizeof(double) : 0) + G * init;
+    // (+ the LDS-coupled layout's ring of the levels' star vx per group, logl_kernel lring)
+    const size_t lc_ring = (size_t)(emax < RVM_LC_RING ? emax : RVM_LC_RING) * (P.n_levels + 1) * wpb * sizeof(double);
+    size_t smem = (size_t)emax * 4 * sizeof(double) + (fused ? (rows + 3) * G * wpb * sizeof(double) : 0) + G * init +
+                  G * lc_ring;
     // level-split layout (logl_kernel) when it lowers the heaviest SIMD's load: in steps per base
     // step, max(m3, m2 + m0, 2 m1) for one round of <= n_cu blocks, against m3 per round of
     // single-group blocks or max_i(m_i + m_{n-1-i}) per round of two-group blocks
