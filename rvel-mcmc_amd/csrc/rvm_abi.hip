@@ -363,6 +363,15 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             P.spec[k] = zn <= 0.04 ? 1 : 0;
         }
     }
+    // the halving passes' late vote (DevPlan::late_mult): levels of at least RVM_LATE_SPO (default 96)
+    // steps per period_hint; RVM_LATE_SPO=0 turns it off (A/B)
+    P.late_mult = 0;
+    {
+        const char* ls = getenv("RVM_LATE_SPO");
+        const double spo = ls ? atof(ls) : 96.0;
+        if (spo > 0.0 && cfg->period_hint > 0.0) P.late_mult = (int32_t)std::ceil(spo * cfg->dt / cfg->period_hint - 1e-9);
+        if (P.late_mult < 1 && spo > 0.0 && cfg->period_hint > 0.0) P.late_mult = 1;
+    }
     // level-split layout (rvm_logl.hip launch_logl): four strictly increasing levels and batches
     // big enough that the plan's largest launch would need two-group blocks
     P.lv_rv = nullptr;

@@ -430,7 +430,8 @@ __device__ __forceinline__ void kepler_safe(double r0, double eta, double zeta, 
 template <int NT>
 __device__ __forceinline__ void halley(double x, double beta, double r0, double eta, double zeta, double GM,
                                        double dt, double& G0, double& G1, double& G2, double& G3, double& fp,
-                                       double& fpp, double& q, double& z, double& x3, double k2v, double k3v) {
+                                       double& fpp, double& q, double& z, double& x3, double k2v, double k3v,
+                                       double& f) {
     const double x2 = x * x;
     z = beta * x2;
     x3 = x2 * x;
@@ -440,7 +441,7 @@ __device__ __forceinline__ void halley(double x, double beta, double r0, double 
     G2 = x2 * c2;
     G1 = fma(-beta, G3, x);  // x c1 = x (1 - z c3)
     G0 = fma(-z, c2, 1.0);
-    const double f = fma(GM, G3, fma(eta, G2, fma(r0, G1, -dt)));
+    f = fma(GM, G3, fma(eta, G2, fma(r0, G1, -dt)));
     fp = fma(zeta, G2, fma(eta, G1, r0));  // r0 G0 + eta G1 + GM G2 with G0 = 1 - beta G2
     fpp = fma(zeta, G1, eta * G0);
     const double den = fma(-0.5 * f, fpp, fp * fp);
@@ -610,7 +611,22 @@ __device__ __forceinline__ bool lane_encountered(const Lane<NP>& s) {
 // KG, the guess: 0 fourth order, 1 fifth order (G5).  (A per-lane choice -- G5 on a lane's step after
 // one whose first Halley test failed -- cost more than either: 935 against 863 / 697 cycles per step
 // at e = 0.55, 689 against 620 / 680 at e = 0.22; profiles/r05o_seg_bench.txt)
-template <int NT, bool GATED, bool D3 = false, int NP, int KG = 0>
+//
+// ACC (gated drift only): what a lane whose first Halley step fails the cheap test gets.
+//   0: a second Halley step with the 8-term series, then kepler_rare (rounds 1-5).
+//   1: first the z-aware form of the acceptance the cheap test's constant derives from,
+//      |q|^3 |z| <= 7.3e-17 |x|^3 (at the passes' fine steps z is far below the series bound, and
+//      the constant tolerance rejects corrections the error bound accepts); then as 0.
+//      Then a lane still failing with |q| <= 1e-4 |x| takes a Newton step at X1 = x - q from the
+//      Taylor expansion of the Kepler function about x (f^(4) = -beta f'', so no new series), and
+//      the third-order terms of the Taylor update fold into drift_apply's inputs; else as 0.
+//   2: the same as 1.
+//   3: ACC 0's solve with the vote after the update (the late vote): the same bits as 0.
+//   4: ACC 1's solve with the late vote.
+//   (steady-state walkers at a pass's finest step, P/112: 12 % of wave-steps fail the cheap test,
+//   6.8 % the z-aware one, and 80 % of the lanes failing that pass the 1e-4 bound --
+//   scripts/probe/kepler_accept_probe.hip, profiles/r06a_kepler_accept_probe.jsonl)
+template <int NT, bool GATED, bool D3 = false, int NP, int KG = 0, int ACC = 0>
 __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const VConsts& vk) {
     const double GM = s.GM, r0 = s.r, ir0 = s.ir;
     double v2 = fma(s.vx, s.vx, s.vy * s.vy);
@@ -637,51 +653,99 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
     } else {
         x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
     }
-    double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2, vk.k3);
+    double G0, G1, G2, G3, fp, fpp, Q, z, x3, f0;
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2, vk.k3, f0);
     constexpr double B = stumpff_bound<NT>();
 #ifdef RVM_PROFILE_FAILS
     drift_fail_count(NT, fabs(z) <= B, halley_ok<NT>(Q, x));
 #endif
     // A step spanning a large part of an orbit (|beta| (dt/r0)^2 > 0.5) that passes these tests has
     // converged all the same; only kepler_rare treats such steps separately (bracketed solver).
-    if constexpr (GATED) {
-        constexpr double B8 = stumpff_bound<8>();
-        const bool ok1 = (fabs(z) <= B && halley_ok<NT>(Q, x)) || lane_encountered(s);
-        if (ballot(!ok1) != 0) {
-#ifdef RVM_PROFILE_FAILS
-            rare_count(0, 0);
-#endif
-            // a second Halley step with the 8-term series (|z| <= 0.3) for the lanes that need it:
-            // pericentre passages on the coarse levels, and walkers whose periods are much shorter
-            // than the plan's period hint on any level
-            bool ok = ok1;
-            double xe = x;
-            if (!ok1) {
-                const double X1 = x - Q;
-                if (fabs(beta * X1 * X1) <= B8) {
-                    xe = X1;
-                    halley<8>(xe, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2_8, vk.k3_8);
-                    ok = fabs(z) <= B8 && halley_ok<8>(Q, xe);
-                }
-            }
-            if (__builtin_expect(ballot(!ok) != 0, 0)) {
-#ifdef RVM_PROFILE_FAILS
-                rare_count(1, 0);
-                rare_count(2, ballot(!ok));
-#endif
-                if (!ok) {
-                    const bool hard = fabs(beta) * (u * u) > 0.5;
-                    const double start = xe - Q;
-                    kepler_rare(r0, eta, zeta, beta, GM, dt, isfinite(start) && xe != x ? start : x, hard, G0, G1,
-                                G2, G3, fp, fpp, Q);
+    // The lanes whose first Halley step failed (ok1 false) get a better solve here; every lane of the
+    // wave calls it (it votes).  ZT: first the z-aware acceptance and the Taylor second step (ACC 2).
+    auto second_chance = [&](bool ok1, const bool ZT) __attribute__((always_inline)) {
+        bool ok = ok1;
+        if (ZT) {
+            const bool zok = fabs(z) <= B;
+            ok = ok || (zok && fabs((Q * Q) * (Q * z)) <= 7.3e-17 * fabs(x3));
+            if (!ok && zok && fabs(Q) <= 1e-4 * fabs(x)) {
+                // derivatives of f at x: f3 = zeta G0 - beta eta G1, f4 = -beta f'' (d/dX G0 = -beta G1)
+                const double f3 = fma(zeta, G0, -(beta * eta) * G1);
+                const double f4 = -beta * fpp;
+                const double d = -Q;
+                const double F = fma(d, fma(d, fma(d, fma(d, f4 * (1.0 / 24.0), f3 * (1.0 / 6.0)), 0.5 * fpp), fp), f0);
+                const double F1 = fma(d, fma(d, fma(d, f4 * (1.0 / 6.0), 0.5 * f3), fpp), fp);
+                const double q2 = F * rcp_nr(F1);
+                if (fabs(q2) <= 1e-8 * fabs(x)) {
+                    // X = x - Qt: the update's third-order terms folded into drift_apply's inputs
+                    const double Qt = Q + q2;
+                    const double c = ((Qt * Qt) * Qt) * (1.0 / 6.0) * beta;
+                    const double g0 = G0, g1 = G1;
+                    G1 = fma(c, g0, G1);
+                    G2 = fma(c, g1, G2);
+                    fp = fma(c, fpp, fp);
+                    Q = Qt;
+                    ok = true;
                 }
             }
         }
+        // a second Halley step with the 8-term series (|z| <= 0.3) for the lanes that need it:
+        // pericentre passages on the coarse levels, and walkers whose periods are much shorter
+        // than the plan's period hint on any level
+        constexpr double B8 = stumpff_bound<8>();
+        double xe = x;
+        if (!ok) {
+            const double X1 = x - Q;
+            if (fabs(beta * X1 * X1) <= B8) {
+                xe = X1;
+                double fu;
+                halley<8>(xe, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vk.k2_8, vk.k3_8, fu);
+                ok = fabs(z) <= B8 && halley_ok<8>(Q, xe);
+            }
+        }
+        if (__builtin_expect(ballot(!ok) != 0, 0)) {
+#ifdef RVM_PROFILE_FAILS
+            rare_count(1, 0);
+            rare_count(2, ballot(!ok));
+#endif
+            if (!ok) {
+                const bool hard = fabs(beta) * (u * u) > 0.5;
+                const double start = xe - Q;
+                kepler_rare(r0, eta, zeta, beta, GM, dt, isfinite(start) && xe != x ? start : x, hard, G0, G1, G2,
+                            G3, fp, fpp, Q);
+            }
+        }
+    };
+    DriftOut o;
+    if constexpr (GATED && ACC >= 3) {
+        // late vote: the update from the first Halley step for every lane, and the wave's vote only
+        // after it -- the vote's compare then waits on nothing, and the branch is not taken on a
+        // clean step (the early vote drained the lone wave's pipeline at the end of the Halley chain:
+        // ~125 cycles per step).  A failing lane's update is recomputed.  ACC 3 gives exactly
+        // ACC 0's bits.
+        const bool ok1 = (fabs(z) <= B && halley_ok<NT>(Q, x)) || lane_encountered(s);
+        o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
+        if (__builtin_expect(ballot(!ok1) != 0, 0)) {
+#ifdef RVM_PROFILE_FAILS
+            rare_count(0, 0);
+#endif
+            second_chance(ok1, ACC == 4);
+            if (!ok1) o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
+        }
     } else {
-        bad = bad || ((!(fabs(z) <= B) || !halley_ok<NT>(Q, x)) && !lane_encountered(s));
+        if constexpr (GATED) {
+            const bool ok1 = (fabs(z) <= B && halley_ok<NT>(Q, x)) || lane_encountered(s);
+            if (ballot(!ok1) != 0) {
+#ifdef RVM_PROFILE_FAILS
+                rare_count(0, 0);
+#endif
+                second_chance(ok1, ACC == 1 || ACC == 2);
+            }
+        } else {
+            bad = bad || ((!(fabs(z) <= B) || !halley_ok<NT>(Q, x)) && !lane_encountered(s));
+        }
+        o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     }
-    const DriftOut o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     s.rx = o.rx;
     s.ry = o.ry;
     s.vx = o.vx;

@@ -65,6 +65,11 @@ struct DevPlan {
     int32_t mult[RVM_MAX_LEVELS];  // level step multipliers (steps per base step)
     int32_t nt[RVM_MAX_LEVELS];    // Stumpff series terms per level (6, 7 or 8)
     int32_t spec[RVM_MAX_LEVELS];  // 1: speculative segments on this level (rvm_logl.hip)
+    // halving passes (rvm_refine.hip refinement and eager kernels): a level whose steps per base step
+    // (mult << rf) reach late_mult runs the gated drift with the late vote (rvm_device.h drift ACC 3:
+    // the same bits; ~3-6 % faster per step where few first Halley steps fail, slower where many do:
+    // scripts/probe/kepler_accept_probe.hip, profiles/r06a_kepler_accept_probe.jsonl); 0: never
+    int32_t late_mult;
     double inv_mult[RVM_MAX_LEVELS];  // 1 / mult: level step = seg_h1 * inv_mult
     double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
     // adaptive resolution (rvm_logl.hip): lw3 = the Lagrange weights of levels

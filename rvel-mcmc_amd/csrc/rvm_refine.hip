@@ -499,6 +499,7 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                 }
                 const int m_r = P.mult[k_u] << rf;
                 const int nt_r = P.nt[k_u];
+                const bool late = P.late_mult > 0 && m_r >= P.late_mult;  // (the late vote: the same bits)
                 const double sc = ldexp(P.inv_mult[k_u], -rf);  // (exact: a power-of-two scaling)
                 const bool cmb = work && k == 0 && lane < WPB && ((need >> lane) & 1);
                 const bool hasp = P.rvp != nullptr;
@@ -517,9 +518,9 @@ __global__ __launch_bounds__(512) void refine_kernel(const DevPlan P, const int 
                         // barrier below then breaks every wave out at this epoch)
                         if (bfirst)
                             (void)segment_gated_c<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r, tflag,
-                                                                                 nullptr, (gen << 8) | 2ull);
+                                                                                 nullptr, (gen << 8) | 2ull, late);
                         else
-                            segment_gated<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r);
+                            segment_gated<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r, late);
                     }
                     RPROF_T(pt_s1);
 #ifdef RVM_PROFILE
@@ -1020,6 +1021,7 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
     if (work && Er > 0) kq = kick_prep<NP, L, D3>(s, 1.875);
     const int m_r = P.mult[k_u] << rf;
     const int nt_r = P.nt[k_u];
+    const bool late = P.late_mult > 0 && m_r >= P.late_mult;  // (the late vote: the same bits)
     const double sc = ldexp(P.inv_mult[k_u], -rf);
     const bool cmb = work && k == 0 && lane < WPB && w0 + lane < W;
     const size_t plane = (size_t)P.lvx_emax * P.lvx_stride;
@@ -1031,7 +1033,7 @@ __global__ __launch_bounds__(256) void eager_kernel(const DevPlan P, const int W
         // (cancels are seen at the epochs: the segment-level cancel of team B's passes,
         // segment_gated_c, measured slower here -- config 4 0.645 -> 0.66 ms median step,
         // profiles/r05r_config4_ab_cancel.jsonl)
-        if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_GUESS>(s, kq, SR.seg_h1[e] * sc, ns, nt_r);
+        if (ns > 0) segment_gated<D3, NP, L, RVM_REFINE_GUESS>(s, kq, SR.seg_h1[e] * sc, ns, nt_r, late);
         if (work) {
             const double v0 = star_vx<NP, L>(s);
             if (pl_idx == 0) s_rv[e & 1][k_u][slot] = v0;

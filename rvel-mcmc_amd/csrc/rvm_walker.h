@@ -8,6 +8,11 @@
 #include "rvm_internal.h"
 #include "rvm_stretch.h"
 
+// the gated drift's second chance for a lane whose first Halley step fails (rvm_device.h drift ACC)
+#ifndef RVM_DRIFT_ACC
+#define RVM_DRIFT_ACC 0
+#endif
+
 namespace rvm {
 
 // One epoch-to-epoch segment of ns Wisdom-Holman kick-drift-kick steps of size h (ns >= 1,
@@ -16,26 +21,26 @@ namespace rvm {
 // segment's opening half kick, and leaves holding the one at the next epoch.  (The step loop is
 // unrolled by hand: the compiler will not unroll a runtime trip count around the convergent DPP /
 // ballot operations.)
-template <int NT, bool GATED, bool D3, int NP, int L, int KG = 0>
+template <int NT, bool GATED, bool D3, int NP, int L, int KG = 0, int ACC = RVM_DRIFT_ACC>
 __device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, bool& bad) {
     lane_set_step(s, h);
     const VConsts vk = vconsts_for<NT>();  // loop-invariant VGPR constants
     kick_apply<NP, true, D3>(s, kp);
     int j = 0;
     for (; j + 2 <= ns - 1; j += 2) {
-        drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, KG, ACC>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
-        drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, KG, ACC>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
     }
     if (j < ns - 1) {
-        drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
+        drift<NT, GATED, D3, NP, KG, ACC>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
     }
-    drift<NT, GATED, D3, NP, KG>(s, h, bad, vk);
+    drift<NT, GATED, D3, NP, KG, ACC>(s, h, bad, vk);
     kp = kick_prep<NP, L, D3>(s, vk.c1875);
     kick_apply<NP, true, D3>(s, kp);
 }
@@ -44,7 +49,7 @@ __device__ __forceinline__ void segment_steps(Lane<NP>& s, KickPrep<NP>& kp, dou
 // of the wave had a step that needs the general solver, restore the segment's initial state and
 // redo it gated.  Used on the fine levels, where such steps are rare.  Returns whether the
 // segment was redone (wave-uniform).  Either way every lane ends bit-identical to a gated run.
-template <int NT, bool SPEC, bool D3, int NP, int L, int KG = 0>
+template <int NT, bool SPEC, bool D3, int NP, int L, int KG = 0, int ACC = RVM_DRIFT_ACC>
 __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int& redo) {
     bool bad = false;
     if constexpr (SPEC) {
@@ -52,7 +57,7 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h,
         const double rz = s.rz, vz = s.vz;
         const uint64_t encm = s.encm;
         const KickPrep<NP> kp0 = kp;
-        segment_steps<NT, false, D3, NP, L, KG>(s, kp, h, ns, bad);
+        segment_steps<NT, false, D3, NP, L, KG, ACC>(s, kp, h, ns, bad);
         if (__builtin_expect(ballot(bad) != 0, 0)) {
 #ifdef RVM_PROFILE
             redo++;
@@ -67,11 +72,11 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h,
             s.ir = ir;
             s.encm = encm;
             kp = kp0;
-            segment_steps<NT, true, D3, NP, L, KG>(s, kp, h, ns, bad);
+            segment_steps<NT, true, D3, NP, L, KG, ACC>(s, kp, h, ns, bad);
             return true;
         }
     } else {
-        segment_steps<NT, true, D3, NP, L, KG>(s, kp, h, ns, bad);
+        segment_steps<NT, true, D3, NP, L, KG, ACC>(s, kp, h, ns, bad);
     }
     (void)redo;
     return false;
@@ -79,15 +84,27 @@ __device__ __forceinline__ bool segment(Lane<NP>& s, KickPrep<NP>& kp, double h,
 
 // a gated segment with the Stumpff series length of the level (nt: 6, 7 or 8); KG: the Kepler guess
 // (rvm_device.h drift: 0 fourth order, 1 fifth)
-template <bool D3, int NP, int L, int KG = 0>
-__device__ __forceinline__ void segment_gated(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int nt) {
+// (late: the gated drift's late vote, rvm_device.h drift ACC 3 -- the same bits, faster where few
+// lanes fail their first Halley step: the refinement passes' fine levels)
+template <bool D3, int NP, int L, int KG = 0, int ACC = RVM_DRIFT_ACC>
+__device__ __forceinline__ void segment_gated(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int nt,
+                                              bool late = false) {
     int unused = 0;
+    if (late) {
+        if (nt <= 6)
+            segment<6, false, D3, NP, L, KG, 3>(s, kp, h, ns, unused);
+        else if (nt == 7)
+            segment<7, false, D3, NP, L, KG, 3>(s, kp, h, ns, unused);
+        else
+            segment<8, false, D3, NP, L, KG, 3>(s, kp, h, ns, unused);
+        return;
+    }
     if (nt <= 6)
-        segment<6, false, D3, NP, L, KG>(s, kp, h, ns, unused);
+        segment<6, false, D3, NP, L, KG, ACC>(s, kp, h, ns, unused);
     else if (nt == 7)
-        segment<7, false, D3, NP, L, KG>(s, kp, h, ns, unused);
+        segment<7, false, D3, NP, L, KG, ACC>(s, kp, h, ns, unused);
     else
-        segment<8, false, D3, NP, L, KG>(s, kp, h, ns, unused);
+        segment<8, false, D3, NP, L, KG, ACC>(s, kp, h, ns, unused);
 }
 
 // kernel parameter row r of walker w: from the SoA input, or (fused sampler step) the row's fixed
@@ -272,7 +289,7 @@ struct SpinClock {
 // tested after the CH steps that follow it (no wait on the step chain).  Returns false when cancelled:
 // the lanes' state is then partial, and the caller discards it.  A segment that runs to its end
 // computes exactly segment_gated's bits.
-template <int NT, bool D3, int NP, int L, int KG, int CH = 64>
+template <int NT, bool D3, int NP, int L, int KG, int CH = 64, int ACC = RVM_DRIFT_ACC>
 __device__ __forceinline__ bool segment_steps_c(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, const gu64* c0,
                                                 const gu64* c1, unsigned long long tag) {
     bool bad = false;
@@ -294,10 +311,10 @@ __device__ __forceinline__ bool segment_steps_c(Lane<NP>& s, KickPrep<NP>& kp, d
         const unsigned long long a = load(c0), b = load(w1);
         const int c = left < CH ? (left & ~1) : CH;
         for (int j = 0; j < c; j += 2) {
-            drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+            drift<NT, true, D3, NP, KG, ACC>(s, h, bad, vk);
             kp = kick_prep<NP, L, D3>(s, vk.c1875);
             kick_apply<NP, false, D3>(s, kp);
-            drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+            drift<NT, true, D3, NP, KG, ACC>(s, h, bad, vk);
             kp = kick_prep<NP, L, D3>(s, vk.c1875);
             kick_apply<NP, false, D3>(s, kp);
         }
@@ -305,22 +322,28 @@ __device__ __forceinline__ bool segment_steps_c(Lane<NP>& s, KickPrep<NP>& kp, d
         if (__builtin_amdgcn_readfirstlane((int)((a == tag) | (b == tag)))) return false;
     }
     if (left == 1) {
-        drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+        drift<NT, true, D3, NP, KG, ACC>(s, h, bad, vk);
         kp = kick_prep<NP, L, D3>(s, vk.c1875);
         kick_apply<NP, false, D3>(s, kp);
     }
-    drift<NT, true, D3, NP, KG>(s, h, bad, vk);
+    drift<NT, true, D3, NP, KG, ACC>(s, h, bad, vk);
     kp = kick_prep<NP, L, D3>(s, vk.c1875);
     kick_apply<NP, true, D3>(s, kp);
     return true;
 }
 
-template <bool D3, int NP, int L, int KG = 0>
+template <bool D3, int NP, int L, int KG = 0, int ACC = RVM_DRIFT_ACC>
 __device__ __forceinline__ bool segment_gated_c(Lane<NP>& s, KickPrep<NP>& kp, double h, int ns, int nt,
-                                                const gu64* c0, const gu64* c1, unsigned long long tag) {
-    if (nt <= 6) return segment_steps_c<6, D3, NP, L, KG>(s, kp, h, ns, c0, c1, tag);
-    if (nt == 7) return segment_steps_c<7, D3, NP, L, KG>(s, kp, h, ns, c0, c1, tag);
-    return segment_steps_c<8, D3, NP, L, KG>(s, kp, h, ns, c0, c1, tag);
+                                                const gu64* c0, const gu64* c1, unsigned long long tag,
+                                                bool late = false) {
+    if (late) {
+        if (nt <= 6) return segment_steps_c<6, D3, NP, L, KG, 64, 3>(s, kp, h, ns, c0, c1, tag);
+        if (nt == 7) return segment_steps_c<7, D3, NP, L, KG, 64, 3>(s, kp, h, ns, c0, c1, tag);
+        return segment_steps_c<8, D3, NP, L, KG, 64, 3>(s, kp, h, ns, c0, c1, tag);
+    }
+    if (nt <= 6) return segment_steps_c<6, D3, NP, L, KG, 64, ACC>(s, kp, h, ns, c0, c1, tag);
+    if (nt == 7) return segment_steps_c<7, D3, NP, L, KG, 64, ACC>(s, kp, h, ns, c0, c1, tag);
+    return segment_steps_c<8, D3, NP, L, KG, 64, ACC>(s, kp, h, ns, c0, c1, tag);
 }
 
 // ---- the two directions of a walker meet (rvm_logl.hip finish) -------------------------------

@@ -28,8 +28,8 @@ __device__ __forceinline__ void drift_v1(Lane<NP>& s, double dt) {
     } else {
         x = u * fma(u, fma(u, T3, -hs), 1.0);
     }
-    double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>().k2, vconsts_for<NT>().k3);
+    double G0, G1, G2, G3, fp, fpp, Q, z, x3, f0;
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>().k2, vconsts_for<NT>().k3, f0);
     constexpr double B = stumpff_bound<NT>();
     const double X = x - Q;
     const bool hard = fabs(beta) * (u * u) > 0.5;
@@ -60,8 +60,8 @@ __device__ __forceinline__ void drift_v2(Lane<NP>& s, double dt) {
     const double T3 = fma(hs, sg, (beta - g) * (1.0 / 6.0));
     const double T4 = sg * fma(-0.625 * sg, sg, fma(5.0 / 12.0, g, -0.375 * beta));
     const double x = u * fma(u, fma(u, fma(u, T4, T3), -hs), 1.0);
-    double G0, G1, G2, G3, fp, fpp, Q, z, x3;
-    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>().k2, vconsts_for<NT>().k3);
+    double G0, G1, G2, G3, fp, fpp, Q, z, x3, f0;
+    halley<NT>(x, beta, r0, eta, zeta, GM, dt, G0, G1, G2, G3, fp, fpp, Q, z, x3, vconsts_for<NT>().k2, vconsts_for<NT>().k3, f0);
     const DriftOut o = drift_apply<false>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     s.rx = o.rx;
     s.ry = o.ry;
