@@ -1124,7 +1124,12 @@ static hipError_t launch_refine_t(const DevPlan& P, int W, const double* params,
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t smem = (size_t)emax * 8 * sizeof(double);
     // (checked by rvm_plan_create: a launch that cannot run would leave the work lists' counts set)
-    const bool w4 = P.n_levels <= 4;  // (refine_kernel NW: four waves per workgroup for up to four levels)
+    // (refine_kernel NW: four waves per workgroup for up to four levels; RVM_REFINE_W4=0 forces eight, A/B)
+    static const bool w4_env = [] {
+        const char* e = getenv("RVM_REFINE_W4");
+        return !(e && e[0] == '0');
+    }();
+    const bool w4 = P.n_levels <= 4 && w4_env;
     if (smem > (w4 ? refine_budget<NPV, D3V, 4>() : refine_budget<NPV, D3V, 8>())) return hipErrorInvalidConfiguration;
     // every block reads the list sizes (the last one resets them): a grid of at most one block
     // per CU, and no more than the lists could fill
@@ -1146,7 +1151,7 @@ template <int NPV, bool D3V>
 static hipError_t prepare_refine_t(const DevPlan& P) {
     const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
     const size_t smem = (size_t)emax * 8 * sizeof(double);
-    const size_t b = P.n_levels <= 4 ? refine_budget<NPV, D3V, 4>() : refine_budget<NPV, D3V, 8>();
+    const size_t b = std::min(refine_budget<NPV, D3V, 4>(), refine_budget<NPV, D3V, 8>());
     return smem <= b ? hipSuccess : hipErrorInvalidConfiguration;
 }
 

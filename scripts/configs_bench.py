@@ -10,6 +10,11 @@
   config 1b: batched MH chains (MhChains, fused rvm_mh_step), 4096 chains; 1bu / 4u: the same
             with the separate propose / logL / accept launches (before the fusion)
 
+The affine configs (2, 2w, 3, 5) and SMALA (4) are timed at their chain's steady state, after a
+burn-in of BURN_IN iterations (RVM_CONFIGS_BURN_IN, default 3000; SMALA a third of it), as the
+headline bench.py is; the window from the tight ball of rounds 1-5 stays as `ball_window`
+(`first_steps` for SMALA).
+
 Prints one JSON line per config.  Usage: python scripts/configs_bench.py [config ...]
 """
 import json
@@ -33,14 +38,11 @@ S2 = [{"m": 1.2e-3, "a": 0.88, "h": 0.218, "k": 0.015, "l": 0.3},
       {"m": 2.1e-3, "a": 1.55, "h": 0.16, "k": 0.02, "l": 2.2}]
 THIRD = {"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}
 SCALES = {"m": 1.5e-3, "a": 0.3, "h": 0.1, "k": 0.1, "l": np.pi / 2.}
+# iterations before the steady-state window (bench.py burns in 4000; RVM_CONFIGS_BURN_IN overrides)
+BURN_IN = int(os.environ.get("RVM_CONFIGS_BURN_IN", "3000"))
 
 
-def _affine(state, obs, W, steps=20, warmup=3, ball=1e-3):
-    sc = np.array([SCALES[k] for k in state.get_rawkeys()])
-    X0 = state.get_params()[None] + ball * sc * np.random.normal(size=(W, state.Nvars))
-    ens = EnsembleSampler(W, state, obs, seed=1)
-    ens.set_positions(X0)
-    ens.compute_lnprob()
+def _window(ens, steps, warmup):
     for _ in range(warmup):
         ens.step()
     torch.cuda.synchronize()
@@ -48,9 +50,43 @@ def _affine(state, obs, W, steps=20, warmup=3, ball=1e-3):
     for _ in range(steps):
         ens.step()
     torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    return {"walker_logl_evals_per_s": W * steps / dt, "ms_per_iteration": 1e3 * dt / steps,
-            "acceptance": float(ens.acceptance_fraction().mean().item()), "plan_steps": ens.plan.info()}
+    return time.perf_counter() - t0
+
+
+def _affine(state, obs, W, steps=20, warmup=3, ball=1e-3, burn_in=BURN_IN, steady_steps=100):
+    """The ball window (iterations warmup .. warmup + steps from the tight ball: rounds 1-5's figure,
+    now a side figure) and, after a burn-in, the chain's steady state (the
+    headline bench times its steady state too, bench.py); the top-level rate is the steady state's."""
+    sc = np.array([SCALES[k] for k in state.get_rawkeys()])
+    X0 = state.get_params()[None] + ball * sc * np.random.normal(size=(W, state.Nvars))
+    ens = EnsembleSampler(W, state, obs, seed=1)
+    ens.set_positions(X0)
+    ens.compute_lnprob()
+    dt = _window(ens, steps, warmup)
+    ball_win = {"walker_logl_evals_per_s": W * steps / dt, "ms_per_iteration": 1e3 * dt / steps,
+                "iterations": [warmup, warmup + steps]}
+    out = {"ball_window": ball_win}
+    if burn_in > 0:
+        done = warmup + steps
+        for _ in range(max(0, burn_in - done)):
+            ens.step()
+        torch.cuda.synchronize()
+        ens.check_faults()
+        ens.plan.faults(reset=True)
+        t0 = dict(ens.plan.totals)  # (running totals: the sampler's periodic checks reset the counters)
+        dt = _window(ens, steady_steps, 3)
+        ens.plan.faults(reset=True)
+        f = {k: ens.plan.totals[k] - t0[k] for k in t0}
+        first = max(burn_in, done) + 3
+        out.update({"walker_logl_evals_per_s": W * steady_steps / dt, "ms_per_iteration": 1e3 * dt / steady_steps,
+                    "timed_window": [first, first + steady_steps], "window": "steady state (after the burn-in)",
+                    "refined_per_iteration": f["refined"] / (steady_steps + 3),
+                    "faults_in_window": {k: v for k, v in f.items() if v and k not in ("refined", "truncated", "skipped")}})
+    else:
+        out.update(ball_win)
+        out["window"] = "ball"
+    out.update({"acceptance": float(ens.acceptance_fraction().mean().item()), "plan_steps": ens.plan.info()})
+    return out
 
 
 def config2():
@@ -80,30 +116,43 @@ def config3():
     return {"config": "3: affine, 4096 walkers, HD155358.vels", **_affine(s, obs, 4096)}
 
 
-def config4(chains=256, steps=100, fused=True):
+def config4(chains=256, steps=100, fused=True, burn_in=None):
+    """SMALA config 4; timed after a burn-in of the chains (the steady state; the first `steps` steps
+    from the start are reported as a side figure)."""
+    burn_in = max(0, BURN_IN // 3) if burn_in is None else burn_in
     np.random.seed(2017)
     s = State(planets=[dict(p) for p in S2])
     obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)
     sm = SmalaChains(s, obs, eps=0.5, alpha=1e3, n_chains=chains, seed=0)
     sm.step(fused=fused)
     torch.cuda.synchronize()
-    # (an event on the launch stream after each step: the steps' own durations, for their spread --
-    # a step whose centres need a second halving pass takes about twice as long)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
-    t0 = time.perf_counter()
-    evs[0].record()
-    for i in range(steps):
+
+    def window(n):
+        # (an event on the launch stream after each step: the steps' own durations, for their spread --
+        # a step whose centres need a second halving pass takes about twice as long)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        t0 = time.perf_counter()
+        evs[0].record()
+        for i in range(n):
+            sm.step(fused=fused)
+            evs[i + 1].record()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(n)])
+
+    dt0, _ = window(steps)
+    first = {"chain_steps_per_s": chains * steps / dt0, "ms_per_step": 1e3 * dt0 / steps, "steps": [1, 1 + steps]}
+    for _ in range(max(0, burn_in - steps - 1)):
         sm.step(fused=fused)
-        evs[i + 1].record()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    per = np.array([evs[i].elapsed_time(evs[i + 1]) for i in range(steps)])
+    dt, per = window(steps)
+    start = max(burn_in, steps + 1)
     P = s.Nvars
     how = ("fused: propose + stencil logL launch + derive/accept kernel" if fused else
            "separate propose / fd / logL / derive / accept launches")
     return {"config": f"4: SMALA, 256 chains, 10-dim, FD (2P+1 = 21 logL per chain-step), {how}",
             "chain_steps_per_s": chains * steps / dt, "walker_logl_evals_per_s": chains * steps * (2 * P + 1) / dt,
             "ms_per_step": 1e3 * dt / steps, "acceptance": float(sm.accepted.double().mean().item() / sm.iteration),
+            "window": "steady state (after the burn-in)", "timed_window": [start, start + steps],
+            "first_steps": first,
             "step_ms_quantiles": [float(v) for v in np.quantile(per, [0, 0.25, 0.5, 0.75, 0.9, 1.0])],
             "step_ms_quantile_levels": [0, 0.25, 0.5, 0.75, 0.9, 1.0]}
 
