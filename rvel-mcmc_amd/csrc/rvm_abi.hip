@@ -363,6 +363,18 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             P.spec[k] = zn <= 0.04 ? 1 : 0;
         }
     }
+    // the LDS-coupled layouts' ring (DevPlan::lc_ring): up to RVM_LC_RING epochs, within
+    // RVM_LC_RING_BYTES per group, at least 2 (a level runs at most a ring ahead of its combiner)
+    {
+        const int wpb = cfg->n_planets == 1 ? 64 : (cfg->n_planets == 2 ? 32 : 16);
+        const int emax = (int)std::max<size_t>(std::max(nf, nb), 1);
+        const int fit = (int)(rvm::RVM_LC_RING_BYTES / ((size_t)(cfg->n_levels + 1) * wpb * sizeof(double)));
+        P.lc_ring = std::max(2, std::min(std::min(rvm::RVM_LC_RING, emax), fit));
+    }
+    {
+        const char* sv = getenv("RVM_SKIP_VARIANTS");
+        P.skip_variants = sv && sv[0] == '0' ? 0 : 1;
+    }
     // the halving passes' late vote (DevPlan::late_mult): levels of at least RVM_LATE_SPO (default 96)
     // steps per period_hint; RVM_LATE_SPO=0 turns it off (A/B)
     P.late_mult = 0;
@@ -575,9 +587,15 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     }
     // kernel attributes (dynamic LDS) set once here, so launches stay capturable; a schedule the
     // refinement kernel cannot stage is refused now rather than failing every launch
-    if (rvm::prepare_logl(P) != hipSuccess) {
-        rvm_plan_destroy(plan);
-        return fail(-1, "rvm_plan_create: n_planets has no kernel instantiation");
+    {
+        const hipError_t pe = rvm::prepare_logl(P);
+        if (pe != hipSuccess) {
+            rvm_plan_destroy(plan);
+            return fail(-1, pe == hipErrorInvalidConfiguration
+                                ? "rvm_plan_create: the epoch schedule does not fit the likelihood kernel's LDS "
+                                  "(too many epochs in one direction)"
+                                : "rvm_plan_create: n_planets has no kernel instantiation");
+        }
     }
     if (rvm::prepare_refine(P) != hipSuccess) {
         rvm_plan_destroy(plan);

@@ -13,6 +13,10 @@ constexpr int RVM_LS_RING = 64;
 // LDS-coupled layouts (one or two groups per block): epochs of the levels' star vx a group's ring
 // holds (rvm_logl.hip; the levels wait for the combiner beyond it)
 constexpr int RVM_LC_RING = 16;
+// ... within this many bytes per group (the one-planet layouts, 64 walkers per group, took
+// 40 KB per group at 16 epochs -- 80 KB for a two-group block -- which cut a one-planet fused launch to
+// ~1150 epochs per direction and one block per CU); DevPlan::lc_ring holds the plan's ring length
+constexpr int RVM_LC_RING_BYTES = 24 * 1024;
 constexpr int RVM_LDS_PER_CU = 160 * 1024;
 // adaptive resolution: lane state at t = 0 kept in LDS for the refinement passes, per walker group
 // (rx, ry, vx, vy, rz, vz, r, ir of each of the 64 lanes)
@@ -70,6 +74,9 @@ struct DevPlan {
     // the same bits; ~3-6 % faster per step where few first Halley steps fail, slower where many do:
     // scripts/probe/kepler_accept_probe.hip, profiles/r06a_kepler_accept_probe.jsonl); 0: never
     int32_t late_mult;
+    // LDS-coupled layouts: epochs in each group's ring of the levels' star vx (rvm_logl.hip lring; 2 ..
+    // RVM_LC_RING, within RVM_LC_RING_BYTES per group; set by rvm_plan_create)
+    int32_t lc_ring;
     double inv_mult[RVM_MAX_LEVELS];  // 1 / mult: level step = seg_h1 * inv_mult
     double lw[RVM_MAX_LEVELS];     // Richardson (Lagrange-at-zero in h^2) weights
     // adaptive resolution (rvm_logl.hip): lw3 = the Lagrange weights of levels
@@ -116,6 +123,7 @@ struct DevPlan {
     // partner's decision final in StretchArgs::dec, so the variant the decision rules out is skipped
     // (rvm_refine.hip; RVM_STATUS_SKIPPED)
     int32_t* rq_mark;
+    int32_t skip_variants;  // 1: skip the ruled-out variants (RVM_SKIP_VARIANTS=0 at plan creation: refine them, A/B)
     // a both-direction group split over two workgroups exchanges its walkers' per-direction state
     // after every halving pass (rvm_refine.hip): rq_x [groups][2 directions][2 pass parities][64]
     // values in the meeting slot's encoding, rq_xf [groups][2] the flag (launch generation << 8 | pass)

@@ -472,7 +472,7 @@ __global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
     }
     // (LDS-coupled) this group's ring of the levels' star vx, after the lanes' t = 0 state
     const int NLC = nl + (cx ? 1 : 0);  // levels that publish (the extension wave too)
-    const int RC = emax2 < RVM_LC_RING ? emax2 : RVM_LC_RING;
+    const int RC = P.lc_ring;  // (rvm_plan_create: min(RVM_LC_RING, epochs), within RVM_LC_RING_BYTES)
     double* lring = dec ? nullptr
                         : l_init + (P.rmax > 0 ? (size_t)G * RVM_INIT_DOUBLES : 0) +
                               (size_t)grp * RC * (nl + 1) * WPB;
@@ -1372,7 +1372,7 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     const bool fused = sa.c != nullptr || sa.mh_scale != nullptr;
     const size_t init = P.rmax > 0 ? (size_t)RVM_INIT_DOUBLES * sizeof(double) : 0;  // per group / unit
     // (+ the LDS-coupled layout's ring of the levels' star vx per group, logl_kernel lring)
-    const size_t lc_ring = (size_t)(emax < RVM_LC_RING ? emax : RVM_LC_RING) * (P.n_levels + 1) * wpb * sizeof(double);
+    const size_t lc_ring = (size_t)P.lc_ring * (P.n_levels + 1) * wpb * sizeof(double);
     size_t smem = (size_t)emax * 4 * sizeof(double) + (fused ? (rows + 3) * G * wpb * sizeof(double) : 0) + G * init +
                   G * lc_ring;
     // level-split layout (logl_kernel) when it lowers the heaviest SIMD's load: in steps per base
@@ -1433,11 +1433,24 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
 
 // rvm_plan_create: set the likelihood kernel's LDS attribute for the plan's instantiations once, so
 // that launches never change function attributes (they stay capturable into a hipGraph)
+// The LDS-coupled layouts' largest request for this plan (two groups per block, a fused sampler step's
+// staging, the adaptive resolution's t = 0 state): the fallback every launch may take, so a plan whose
+// schedule it cannot stage is refused at creation rather than failing its launches
+static size_t logl_smem_worst(const DevPlan& P, int npv, bool d3) {
+    const int wpb = 64 / (npv == 1 ? 1 : (npv == 2 ? 2 : 4));
+    const int emax = P.fwd.n_epochs > P.bwd.n_epochs ? P.fwd.n_epochs : P.bwd.n_epochs;
+    const size_t rows = (size_t)(d3 ? 7 : 5) * npv;
+    const size_t init = P.rmax > 0 ? (size_t)RVM_INIT_DOUBLES * sizeof(double) : 0;
+    const size_t ring = (size_t)P.lc_ring * (P.n_levels + 1) * wpb * sizeof(double);
+    return (size_t)emax * 4 * sizeof(double) + (rows + 3) * 2 * wpb * sizeof(double) + 2 * init + 2 * ring;
+}
+
 hipError_t prepare_logl(const DevPlan& P) {
     const bool inc = P.inclined != 0;
-#define RVM_PREP(NPV)                                                                      \
-    (inc ? (lds_budget<NPV, true, true>(), lds_budget<NPV, true, false>())                 \
-         : (lds_budget<NPV, false, true>(), lds_budget<NPV, false, false>()))
+    size_t budget = 0;
+#define RVM_PREP(NPV)                                                                          \
+    (inc ? ((void)lds_budget<NPV, true, true>(), budget = lds_budget<NPV, true, false>())      \
+         : ((void)lds_budget<NPV, false, true>(), budget = lds_budget<NPV, false, false>()))
     switch (P.n_planets) {
         case 1:
             (void)RVM_PREP(1);
@@ -1455,7 +1468,7 @@ hipError_t prepare_logl(const DevPlan& P) {
             return hipErrorInvalidValue;
     }
 #undef RVM_PREP
-    return hipSuccess;
+    return logl_smem_worst(P, P.n_planets, inc) <= budget ? hipSuccess : hipErrorInvalidConfiguration;
 }
 
 // the likelihood kernel (main pass + extension); an adaptive plan's walkers it hands on are

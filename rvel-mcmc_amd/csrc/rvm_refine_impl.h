@@ -115,8 +115,12 @@ __device__ __forceinline__ bool claim_item(gu64* w, unsigned long long gen, unsi
 // Bounded wait of a refinement pass's hand-off (split exchange, team B for team A): the partner
 // integrates a pass of 2^rf x the base steps without publishing progress, so the allowance scales
 // with the pass (a deep pass is no timeout; the timeout stays a last-resort fault)
+// (capped at 60 s: a partner that is really lost -- a fault, a workgroup never co-resident -- still
+// ends in a counted fault within a minute, not hours at a deep pass)
 __device__ __forceinline__ unsigned long long pass_ticks(const DevPlan& P, int rf) {
-    return P.spin_ticks << (rf < RVM_RESOLVE_MAX_LIMIT ? rf : RVM_RESOLVE_MAX_LIMIT);
+    const unsigned long long t = P.spin_ticks << (rf < RVM_RESOLVE_MAX_LIMIT ? rf : RVM_RESOLVE_MAX_LIMIT);
+    constexpr unsigned long long cap = 6000000000ull;  // 60 s of the 100 MHz real-time counter
+    return t < cap ? t : (P.spin_ticks > cap ? P.spin_ticks : cap);
 }
 
 // NW: waves per workgroup.  8 (512 threads) runs a both-direction group's two directions side by side
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
         const int base = (li == 0 ? g : (li == 1 ? g - gq0 : g - gq0 - gq1)) * WPB;
         int cnt = nq[li] - base < WPB ? nq[li] - base : WPB;
         const int* items = P.rq_w + (size_t)li * P.rq_cap + base;
-        gu64* ef = eager ? (gu64*)(P.eflag + (size_t)g * 8) : nullptr;  // (the eager group's flags)
+        gu64* ef = eager ? (gu64*)(P.eflag + (size_t)g * RVM_EFLAG_WORDS) : nullptr;  // (the eager group's flags)
         if (eager) {
             // the launch's walkers g * WPB ..: which of them the lists hold, and in which
             const int w0 = g * WPB;
@@ -331,7 +335,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 // the likelihood kernel has stored j's final decision, and the variant it rules out is
                 // never read (rvm_stretch_iteration_end) -- skipped instead of refined
                 int skip = 0;
-                if (stretch && sa.n_spec > 0 && sa.dec != nullptr && lane < cnt && lli >= 0) {
+                if (P.skip_variants && stretch && sa.n_spec > 0 && sa.dec != nullptr && lane < cnt && lli >= 0) {
                     int k2 = 0, wk2 = 0, j2 = 0, jp2 = 0;
                     double z2 = 0.0, zp2 = 0.0;
                     stretch_slot(sa, items[lane], k2, wk2, z2, j2, zp2, jp2);

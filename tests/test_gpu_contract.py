@@ -157,3 +157,109 @@ def test_nonfinite_halving_pass_ends_the_walker(W):
         err = np.abs(got[ok] - ref[ok]) / np.maximum(1.0, np.abs(ref[ok]))
         assert err.max() <= 1e-11 * 35.0, err.max()
     assert RMAX <= rmax
+
+
+def test_one_planet_long_schedule_fits_the_lds_coupled_layout():
+    """the LDS-coupled layouts' ring of the levels' star velocities took 16 epochs x
+    (levels + 1) x 64 walkers x 8 B = 40 KB per one-planet group (80 KB per two-group block), so a
+    one-planet fused launch fit only ~1150 epochs per direction -- and a plan between that and the
+    refinement kernel's limit was created but failed every launch.  The ring is now sized per plan
+    within 24 KB per group (DevPlan::lc_ring; 9 epochs here), rvm_plan_create refuses a schedule the
+    worst-case launch cannot stage, and a 1500-epoch-per-direction one-planet plan runs its two-group
+    launch: every copy of a walker gets the same bits, and the values are the oracle's (T1)."""
+    torch = _torch()
+    from rvmcmc import _lib, engine
+
+    one = [{"m": 1.2e-3, "a": 0.88, "h": 0.05, "k": 0.02, "l": 0.3}]
+    np.random.seed(7)
+    obs = O.fake_obs(one, Npoints=3000, error=1.5e-4, errorVar=2.5e-5, tmax=400.)  # 1501 + 1500 epochs
+    dt, mult, hint = engine.IntegratorConfig().plan_args(one)
+    t, rv, er = engine.obs_arrays(obs)
+    W = 12288  # 192 groups of 64 walkers: two groups per block
+    plan = engine.LoglPlan(t, rv, er, obs.Npoints, 1, dt, mult, W, period_hint=hint, resolve=(TOL, RMAX))
+    rng = np.random.default_rng(1)
+    base = np.array([one[0][k] for k in "mahkl"])
+    X16 = base * (1 + 1e-4 * rng.standard_normal((16, 5)))
+    X = np.tile(X16, (W // 16, 1))
+    lp, st, _ = plan.logl(_rows(X))
+    torch.cuda.synchronize()
+    lp, st = lp.cpu().numpy().reshape(-1, 16), st.cpu().numpy().reshape(-1, 16)
+    assert (st == 0).all()
+    assert (lp == lp[0]).all()  # (every copy the same bits)
+    P = np.zeros((16, 1, 7))
+    P[:, 0, :5] = X16
+    ref, sref = O.logl_whx_adapt_batch(P, 1, obs, dt, mult, TOL, RMAX)[:2]
+    assert (sref == 0).all()
+    err = np.max(np.abs(lp[0] - ref) / np.maximum(1.0, np.abs(ref)))
+    assert err < 1e-11 * float(np.abs(O.richardson_weights_seq(mult)).sum()), err
+    # a schedule no launch could stage is refused when the plan is created, not at launch
+    np.random.seed(7)
+    big = O.fake_obs(one, Npoints=12000, error=1.5e-4, errorVar=2.5e-5, tmax=400.)
+    t2, rv2, er2 = engine.obs_arrays(big)
+    with pytest.raises(_lib.RvmError, match="LDS"):
+        engine.LoglPlan(t2, rv2, er2, big.Npoints, 1, dt, mult, W, period_hint=hint, resolve=(TOL, RMAX))
+
+
+def test_skipped_variants_are_exactly_the_ruled_out_ones():
+    """a speculative iteration's half-1 slot is one of two variants of its partner j's
+    outcome; when j was not handed to the refinement kernel its decision is final, and the
+    refinement kernel skips (RVM_STATUS_SKIPPED) the variant that decision rules out instead of
+    refining it.  At the bench chain's steady state, over three iterations: SKIPPED appears only on
+    ruled-out variants ((kind 2) != (dec[j] == 1)), never on half 0 or on a chosen variant, and the
+    chosen variants' logL and status, the positions and the lnprob are bit-identical to a plan with
+    skipping disabled (RVM_SKIP_VARIANTS=0), which skips nothing."""
+    torch = _torch()
+    from philox_ref import stretch_uniforms
+    from rvmcmc import _lib
+    from rvmcmc.ensemble import EnsembleSampler
+    from rvmcmc.observations import FakeObservation
+    from rvmcmc.state import State
+
+    X0 = np.load(os.path.join(HERE, "..", "scripts", "probe", "ens_it2000.npy"))
+
+    def run(skip):
+        old = os.environ.get("RVM_SKIP_VARIANTS")
+        os.environ["RVM_SKIP_VARIANTS"] = "1" if skip else "0"
+        try:
+            s = State(planets=[dict(p) for p in S2_PLANETS])
+            np.random.seed(2017)
+            obs = FakeObservation(s, Npoints=100, error=1.5e-4, errorVar=2.5e-5, tmax=120.)  # (its own plan)
+            ens = EnsembleSampler(len(X0), s, obs, seed=2017)
+            ens.set_positions(X0)
+            ens.compute_lnprob()
+            assert ens.speculating()
+            out = []
+            for _ in range(3):
+                it = ens.iteration
+                ens.step()
+                torch.cuda.synchronize()
+                out.append((it, ens._st_spec.cpu().numpy().copy(), ens._lnp_spec.cpu().numpy().copy(),
+                            ens._dec.cpu().numpy().copy()))
+            return ens, out
+        finally:
+            if old is None:
+                os.environ.pop("RVM_SKIP_VARIANTS", None)
+            else:
+                os.environ["RVM_SKIP_VARIANTS"] = old
+
+    ea, oa = run(True)
+    eb, ob = run(False)
+    n = ea.nloc
+    skipped = 0
+    for (it, sa_, la, da), (_, sb, lb, db) in zip(oa, ob):
+        np.testing.assert_array_equal(da, db)
+        _, u2, _ = stretch_uniforms(ea.seed, ea.global_begin(1), n, it, 1)
+        j = np.clip(np.floor(u2 * ea.halfk).astype(int), 0, ea.halfk - 1)
+        accepted = da[j] == 1
+        chosen = np.concatenate([np.arange(n), n + np.arange(n) + np.where(accepted, n, 0)])
+        ruled_out = n + np.arange(n) + np.where(accepted, 0, n)
+        sk = np.nonzero(sa_ == _lib.RVM_STATUS_SKIPPED)[0]
+        assert set(sk.tolist()) <= set(ruled_out.tolist())
+        assert not (sb == _lib.RVM_STATUS_SKIPPED).any()
+        np.testing.assert_array_equal(sa_[chosen], sb[chosen])
+        np.testing.assert_array_equal(la[chosen], lb[chosen])
+        skipped += len(sk)
+    assert skipped > 0  # (~16 per steady-state iteration)
+    for h in (0, 1):
+        np.testing.assert_array_equal(ea.pos[h].cpu().numpy(), eb.pos[h].cpu().numpy())
+        np.testing.assert_array_equal(ea.lnp[h].cpu().numpy(), eb.lnp[h].cpu().numpy())
