@@ -79,7 +79,7 @@ __global__ __launch_bounds__(64) void probe(const double* rows, int n, double h,
 
 // timing: the plain segment loop (segments of NS steps, the refinement passes' rf = 1 finest level at
 // ~2.3 base steps per segment) with the gated drift's second chance ACC, or ungated (ACC = -1)
-template <int ACC>
+template <int ACC, int KG = 0>
 __global__ __launch_bounds__(64) void timing(const double* rows, int n, double h, int nseg, int ns, long long* cyc,
                                              double* sink) {
     const int lane = threadIdx.x & 63;
@@ -98,20 +98,20 @@ __global__ __launch_bounds__(64) void timing(const double* rows, int n, double h
     const long long t0 = clock64();
     for (int g = 0; g < nseg; g++) {
         if constexpr (ACC < 0)
-            segment_steps<6, false, false, 2, 2, 0, 0>(s, kp, h, ns, bad);
+            segment_steps<6, false, false, 2, 2, KG, 0>(s, kp, h, ns, bad);
         else
-            segment_steps<6, true, false, 2, 2, 0, ACC>(s, kp, h, ns, bad);
+            segment_steps<6, true, false, 2, 2, KG, ACC>(s, kp, h, ns, bad);
     }
     const long long t1 = clock64();
     sink[blockIdx.x * 64 + lane] = s.rx + s.vy + s.ry + s.vx;
     if (lane == 0) cyc[blockIdx.x] = t1 - t0;
 }
 
-template <int ACC>
+template <int ACC, int KG = 0>
 static double run_timing(const double* rows, int n, double h, int nseg, int ns, long long* cyc, double* sink,
                          double* out_sink) {
     const int blocks = (n + 31) / 32;
-    timing<ACC><<<blocks, 64>>>(rows, n, h, nseg, ns, cyc, sink);
+    timing<ACC, KG><<<blocks, 64>>>(rows, n, h, nseg, ns, cyc, sink);
     hipDeviceSynchronize();
     long long* hc = (long long*)malloc(blocks * sizeof(long long));
     hipMemcpy(hc, cyc, blocks * sizeof(long long), hipMemcpyDeviceToHost);
@@ -182,6 +182,10 @@ int main(int argc, char** argv) {
     int n3 = 0;
     for (int i = 0; i < ((nt_walk + 31) / 32) * 64; i++) n3 += !(s1[i] == s0[i]) && (s1[i] == s1[i] || s0[i] == s0[i]);
     const double t4c = run_timing<4>(rows, nt_walk, h, nseg, ns, cyc, sink, s1);
+    const double g5u = run_timing<-1, 1>(rows, nt_walk, h, nseg, ns, cyc, sink, s1);
+    const double g5g = run_timing<0, 1>(rows, nt_walk, h, nseg, ns, cyc, sink, s1);
+    const double g5l = run_timing<3, 1>(rows, nt_walk, h, nseg, ns, cyc, sink, s1);
+    printf("{\"spo\": %.1f, \"g5_cyc_per_step\": {\"ungated\": %.1f, \"acc0\": %.1f, \"late3\": %.1f}}\n", spo, g5u, g5g, g5l);
     printf("{\"spo\": %.1f, \"cyc_per_step\": {\"ungated\": %.1f, \"acc0\": %.1f, \"acc1\": %.1f, \"late3\": %.1f, "
            "\"late4\": %.1f}, \"lanes_acc3_differing_from_acc0\": %d}\n", spo, tu, t0c, t1c, t3c, t4c, n3);
     return 0;
