@@ -40,6 +40,14 @@ THIRD = {"m": 1e-3, "a": 2.6, "h": 0.05, "k": 0.0, "l": 1.0}
 SCALES = {"m": 1.5e-3, "a": 0.3, "h": 0.1, "k": 0.1, "l": np.pi / 2.}
 # iterations before the steady-state window (bench.py burns in 4000; RVM_CONFIGS_BURN_IN overrides)
 BURN_IN = int(os.environ.get("RVM_CONFIGS_BURN_IN", "3000"))
+# (studies) base steps per shortest period for every config's plan (IntegratorConfig.steps_per_orbit)
+if os.environ.get("RVM_CONFIGS_SPO"):
+    import dataclasses
+
+    from rvmcmc import engine
+
+    engine.DEFAULT_CONFIG = dataclasses.replace(engine.DEFAULT_CONFIG,
+                                                steps_per_orbit=float(os.environ["RVM_CONFIGS_SPO"]))
 
 
 def _window(ens, steps, warmup):
