@@ -434,6 +434,11 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.lvx = nullptr;
     P.rvp = nullptr;
     P.rvp2 = nullptr;
+    // refinement teams (A/B knob RVM_REFINE_TEAMS: 0 or 1 runs the passes one after the other, 2 ..
+    // RVM_TEAMS_MAX that many passes at once)
+    int n_teams = rvm::RVM_TEAMS_DEFAULT;
+    if (const char* tp = getenv("RVM_REFINE_TEAMS")) n_teams = std::max(1, std::min(atoi(tp), rvm::RVM_TEAMS_MAX));
+    P.n_teams = n_teams;
     P.rve = nullptr;
     P.esum = nullptr;
     P.eflag = nullptr;
@@ -450,7 +455,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         const int nl = cfg->n_levels;
         const size_t emax = std::max<size_t>(std::max(nf, nb), 1);
         const size_t bl = 2 * emax * (size_t)max_walkers * sizeof(double);  // partial sums
-        const size_t bx = 3 * bl;                                           // + last RV (x2 teams)
+        const size_t bx = (1 + (size_t)n_teams) * bl;                       // + last RV (per team)
         // (a failed allocation is not an error: the plan refines by halving passes alone, ext_mult 0)
         if (bx <= RVM_EXT_MAX_BYTES && hipMalloc(&plan->xmem, bx) != hipSuccess) {
             plan->xmem = nullptr;
@@ -489,7 +494,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
             P.inv_mult[nl] = P.inv_ext;
             P.lvx = reinterpret_cast<double*>(plan->xmem);
             P.rvp = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(plan->xmem) + bl);
-            P.rvp2 = reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(plan->xmem) + 2 * bl);
+            P.rvp2 = n_teams >= 2 ? reinterpret_cast<double*>(reinterpret_cast<unsigned char*>(plan->xmem) + 2 * bl)
+                                  : nullptr;
             P.lvx_emax = (int32_t)emax;
             P.lvx_stride = max_walkers;
         }
@@ -506,19 +512,22 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.rq_t = nullptr;
     P.rq_tf = nullptr;
     P.gen_dev = nullptr;
+    P.depth_w = nullptr;
     P.rq_mark = nullptr;
     if (P.rmax > 0) {
         // (+ the split exchange: flags and double-buffered values per both-direction group of up to 64
         // walkers and team; groups of 16 walkers at 3-4 planets; + team A's published state and flag)
         const int64_t xg = ((int64_t)max_walkers + 15) / 16 + 1;
-        const size_t b_x = (size_t)xg * 2 * 2 * 2 * 64 * sizeof(unsigned long long);
-        const size_t b_xf = (size_t)xg * 2 * 2 * sizeof(unsigned long long);
-        const size_t b_t = (size_t)xg * 16 * 64 * sizeof(unsigned long long);
-        const size_t b_tf = (size_t)xg * sizeof(unsigned long long);
+        const size_t nt = (size_t)std::max(n_teams, 2);
+        const size_t b_x = (size_t)xg * nt * 2 * 2 * 64 * sizeof(unsigned long long);
+        const size_t b_xf = (size_t)xg * nt * 2 * sizeof(unsigned long long);
+        const size_t b_t = (size_t)xg * (nt - 1) * 16 * 64 * sizeof(unsigned long long);
+        const size_t b_tf = (size_t)xg * nt * sizeof(unsigned long long);  // (+ the group's done word)
         const size_t b_c = 2 * (size_t)max_walkers * sizeof(double);
         const size_t b_w = 3 * (size_t)max_walkers * sizeof(int32_t);
         const size_t b_m = ((size_t)max_walkers * sizeof(int32_t) + 63) & ~(size_t)63;  // rq_mark
-        const size_t b_all = b_x + b_xf + b_t + b_tf + b_c + b_w + 64 + b_m;  // (+ rq_n [4], the launch generation)
+        const size_t b_d = (rvm::RVM_DEPTH_WINDOW + 1) * sizeof(unsigned long long);    // depth_w
+        const size_t b_all = b_x + b_xf + b_t + b_tf + b_c + b_w + 64 + b_m + b_d;  // (+ rq_n [4], the launch generation)
         if (hipMalloc(&plan->rqmem, b_all) != hipSuccess || hipMemset(plan->rqmem, 0, b_all) != hipSuccess ||
             hipDeviceSynchronize() != hipSuccess) {
             (void)hipGetLastError();
@@ -534,6 +543,8 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.rq_w = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c);
         P.rq_n = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w);
         P.gen_dev = reinterpret_cast<unsigned long long*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w + 32);
+        // (zeroed: generation 0, older than any launch)
+        P.depth_w = reinterpret_cast<unsigned long long*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w + 64 + b_m);
         P.rq_mark = reinterpret_cast<int32_t*>(base + b_x + b_xf + b_t + b_tf + b_c + b_w + 64);  // (zeroed)
         const unsigned long long gen1 = 1;  // (every flag word starts at generation 0)
         if (hipMemcpy(P.gen_dev, &gen1, sizeof(gen1), hipMemcpyHostToDevice) != hipSuccess) {
@@ -545,8 +556,10 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.rq_xgroups = (int32_t)xg;
         if (const char* sp = getenv("RVM_REFINE_SPLIT"))  // (A/B knob: 0 keeps both directions in one block)
             if (sp[0] == '0') P.rq_x = nullptr;
-        if (const char* tp = getenv("RVM_REFINE_TEAMS"))  // (A/B knob: 0 runs the passes one after the other)
-            if (tp[0] == '0') P.rq_t = nullptr;
+        if (n_teams < 2) P.rq_t = nullptr;
+        if (const char* th = getenv("RVM_TEAMS_HINT"))  // (A/B knob: 0 always runs the plan's team count)
+            if (th[0] == '0') P.depth_w = nullptr;
+        P.n_teams = (int32_t)nt;
     }
     // eager halving passes for the plan's plain launches of RVM_EAGER_MIN..RVM_EAGER_MAX walkers
     // (SMALA's centres, batched State evaluations): results of passes 1 and 2, a side stream and two

@@ -47,6 +47,12 @@ constexpr int RVM_EAGER_MAX = 512;
 constexpr int RVM_EAGER_MIN = 32;
 // eflag words per eager group (rvm_refine.hip)
 constexpr int RVM_EFLAG_WORDS = 8;
+// refinement kernel teams per walker group (rvm_refine_impl.h): team t runs halving pass t + 1 from
+// the launch's start, all at once; at most this many (the plan's count: DevPlan::n_teams)
+constexpr int RVM_TEAMS_MAX = 4;
+constexpr int RVM_TEAMS_DEFAULT = 4;
+// ... and no more than the deepest pass of the plan's last this-many launches needed (at least two)
+constexpr int RVM_DEPTH_WINDOW = 8;
 
 // Epoch schedule of one integration direction (t >= 0 ascending from 0, or t < 0 descending).
 struct DirSched {
@@ -130,13 +136,21 @@ struct DevPlan {
     unsigned long long* rq_x;
     unsigned long long* rq_xf;
     int32_t rq_xgroups;
-    // (both [groups][2 teams] since round 4: team A runs pass 1, team B pass 2 at the same time, then
-    // the rest, rvm_refine.hip) team A's walker state after pass 1 for team B, rq_t [groups][16][64],
-    // and its flag rq_tf [groups] (launch generation << 8 | 1, or 2 when the group is done)
+    // (both [groups][n_teams] since round 4: team t runs pass t + 1 from the launch's start, then hands
+    // its walkers on, rvm_refine_impl.h) team t's walker state after its pass for team t + 1,
+    // rq_t [groups][n_teams - 1][16][64], and its flag rq_tf [groups][n_teams] (launch generation
+    // << 8 | 1, or 2 when the group is done; [n_teams - 1] the group's done word)
     unsigned long long* rq_t;
     unsigned long long* rq_tf;
-    // team B's own RV per pass (as rvp)
+    // teams 1 .. n_teams - 1: their own RV per pass (as rvp), [n_teams - 1][2][lvx_emax][lvx_stride]
     double* rvp2;
+    // the plan's team count (2 .. RVM_TEAMS_MAX; a launch uses fewer when its groups' tasks would not
+    // all fit the grid, or when the deepest pass of the plan's last two launches was shallower; rq_t
+    // null: no teams)
+    int32_t n_teams;
+    // [RVM_DEPTH_WINDOW + 1] by launch generation mod RVM_DEPTH_WINDOW + 1: the deepest pass a group
+    // of that launch finished at, tagged (generation << 8 | pass; atomic max)
+    unsigned long long* depth_w;
     // eager halving passes (rvm_refine.hip eager_kernel; plain launches of at most eager_max
     // walkers, 0: none): passes 1 and 2 of every walker beside the likelihood kernel -- rve [2
     // passes][2 directions][lvx_emax][lvx_stride] their RV per epoch, esum [2][2][3][lvx_stride]

@@ -70,8 +70,12 @@ __device__ unsigned long long rvm_prof[RVM_PROF_MAX_WAVES * RVM_PROF_SLOTS];
 // construction: launch_logl uses the layout only when its grid fits the CUs.
 
 // D3: inclined systems (7 parameter rows per planet, m a h k l ix iy; 3-D positions/velocities)
+// (the 3-planet LDS-coupled instantiation within 168 VGPRs: three waves per SIMD, so that two blocks of
+// the paired layout -- one group and its extension wave, five waves each -- share a CU, launch_logl_t;
+// at 170 the second block waited for the first: two rounds)
 template <int NP, bool D3, bool DEC>
-__global__ __launch_bounds__(512) void logl_kernel(const DevPlan P, const int W,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NP == 3 && !D3 && !DEC ? 3 : 1)))
+void logl_kernel(const DevPlan P, const int W,
                                                                    const double* __restrict__ params,
                                                                    const double hill_factor,
                                                                    unsigned long long* __restrict__ slots,
@@ -1356,7 +1360,18 @@ static hipError_t launch_logl_t(const DevPlan& P, int W, const double* params, d
     // one walker group per block while the blocks fit one per CU (every wave alone on its SIMD:
     // latency-bound); beyond that two groups with mirrored level order per block, which pairs
     // the heaviest level with the lightest on each SIMD (logl_kernel)
-    const int G = (P.n_cu > 0 && 2 * groups > P.n_cu && 2 * P.n_levels * 64 <= 512) ? 2 : 1;
+    // Paired one-group blocks (3 planets, round 6): where two groups would share a block, a launch of
+    // at most one group per CU instead runs one group per block with the extension as its fifth wave
+    // (cx below), two such blocks per CU (the 3-planet instantiation is held to 168 VGPRs for it) --
+    // the extension beside the main pass instead of after it, for config 5's 4096-walker half-steps.
+    // (A/B knob RVM_CX_PAIRS=0: the two-group blocks)
+    static const bool pairs_env = [] {
+        const char* e = getenv("RVM_CX_PAIRS");
+        return !(e && e[0] == '0');
+    }();
+    const bool pairs = NPV == 3 && !D3V && pairs_env && P.ext_mult > 0 && rv_out == nullptr && P.n_cu > 0 &&
+                       2 * groups > P.n_cu && groups <= P.n_cu && W >= RVM_CX_MIN_WALKERS;
+    const int G = (!pairs && P.n_cu > 0 && 2 * groups > P.n_cu && 2 * P.n_levels * 64 <= 512) ? 2 : 1;
     dim3 grid((groups + G - 1) / G, 2);
     // one group per block (the blocks fit one per CU): the extension level as an extra wave
     // (logl_kernel, cx) when the plan has one and no model RVs are asked for.  The fifth wave shares

@@ -35,16 +35,20 @@
 // same bits as the likelihood kernel's prologue) and finishes the walker as it would have
 // (rvm_walker.h walker_out: logl, status, counters, the fused accept).
 //
-// Two teams (round 4).  At the steady state about one walker slot in a launch needs a second
-// halving pass, and that launch then waited pass 1 (14 steps per base step on the longest level)
-// and pass 2 (28) one after the other.  When every task fits the grid, each group has team A,
-// which runs pass 1, and team B on other CUs, which runs pass 2 at the same time, before pass 1's
-// outcome is known.  A decides after pass 1 and publishes its walkers' state (write-through
+// Teams (round 4: two; round 6: a ladder of up to RVM_TEAMS_MAX).  At the bench's steady state about
+// one walker slot in a launch needs a second halving pass, and that launch then waited pass 1 (14
+// steps per base step on the longest level) and pass 2 (28) one after the other; at HD155358's and
+// the 3-planet system's steady states a launch climbs to pass 3 or 4.  When every task fits the grid,
+// each group has team A, which runs pass 1, team B on other CUs, which runs pass 2 at the same time,
+// before pass 1's outcome is known, team C pass 3, and so on (DevPlan::n_teams, fewer when the tasks
+// would not all fit).  A decides after pass 1 and publishes its walkers' state (write-through
 // granules and a flag tagged with the launch generation).  If every walker of the group is done,
-// A finishes them and B, which polls the flag at every epoch, stops.  Otherwise B, at the end of its
-// pass, takes A's state and applies pass 2's results to the walkers still open: their step-doubling
-// change is against pass 1's RV, which A stored write-through.  It then goes on alone, rf = 3, ...,
-// and finishes the group.  Decisions and values are the sequential passes' bit for bit.
+// A finishes them and B, which polls the flag at every epoch, stops (and passes the stop on to C).
+// Otherwise B, at the end of its pass, takes A's state and applies pass 2's results to the walkers
+// still open: their step-doubling change is against pass 1's RV, which A stored write-through; B
+// then publishes for C in turn.  The last team goes on alone, rf = nteam + 1, ..., and finishes the
+// group.  Decisions and values are the sequential passes' bit for bit; a launch whose deepest walker
+// needs pass r <= nteam waits max(pass r) instead of the sum of passes 2 .. r.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -155,10 +159,27 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
     // generation too) advances the launch generation -- every block has read it by then
     __shared__ int s_n[3];
     __shared__ unsigned long long s_gen;
+    __shared__ int s_depth;
     if (threadIdx.x == 0) {
         for (int i = 0; i < 3; i++) s_n[i] = __hip_atomic_load(P.rq_n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long g0 = __hip_atomic_load(P.gen_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_gen = g0;
+        // the deepest pass the plan's previous RVM_DEPTH_WINDOW launches needed (P.depth_w, by generation
+        // mod RVM_DEPTH_WINDOW + 1, tagged with it; this launch writes its own word only, so every block
+        // reads the same)
+        int d = P.depth_w != nullptr ? 0 : RVM_TEAMS_MAX;  // (no words: no limit)
+        if (P.depth_w != nullptr) {
+            unsigned long long v[RVM_DEPTH_WINDOW];
+#pragma unroll
+            for (int i = 0; i < RVM_DEPTH_WINDOW; i++)
+                v[i] = __hip_atomic_load(P.depth_w + (g0 + 1 + i) % (RVM_DEPTH_WINDOW + 1), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int i = 0; i < RVM_DEPTH_WINDOW; i++)
+                if ((v[i] >> 8) < g0 && (v[i] >> 8) + RVM_DEPTH_WINDOW >= g0 && (int)(v[i] & 0xFF) > d)
+                    d = (int)(v[i] & 0xFF);
+        }
+        s_depth = d;
 #if RVM_REFINE_RELAXED_COUNT
         // (the three loads have returned before the count is bumped: the last block's reset
         // cannot overtake them; no release / acquire -- an L2 writeback and invalidate -- needed)
@@ -176,6 +197,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
     RPROF_T(pt_lists);
     const unsigned long long gen = s_gen;
     const int nq[3] = {s_n[0], s_n[1], s_n[2]};
+    const int depth_hint = s_depth;
     const int gq0 = (nq[0] + WPB - 1) / WPB, gq1 = (nq[1] + WPB - 1) / WPB, gq2 = (nq[2] + WPB - 1) / WPB;
     const int ng = gq0 + gq1 + gq2;
     // split: each both-direction group's two directions on two workgroups (2j, 2j + 1) -- every
@@ -187,12 +209,22 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
     // (eager: pass 1 is a replay of eager_kernel's results, both directions in one block)
     const bool split = !eager && P.rq_x != nullptr && gq0 <= P.rq_xgroups && ((int)gridDim.x & 1) == 0 &&
                        ntask_split <= (int)gridDim.x;
-    // teams: A (pass 1) and B (pass 2 concurrently, then the rest) per group -- when the split
-    // layout holds, every team task fits the grid, and no RV curve is wanted (both teams would
-    // write it)
-    const int ntask_team = 4 * gq0 + 2 * (gq1 + gq2);
-    const bool team = split && P.rq_t != nullptr && P.rvp != nullptr && P.rvp2 != nullptr && P.rmax >= 2 &&
-                      rv_out == nullptr && ng <= P.rq_xgroups && ntask_team <= (int)gridDim.x;
+    // teams: team t runs pass t + 1 of the group from the start (A pass 1, B pass 2, C pass 3 ...), the
+    // last one then the rest -- when the split layout holds, no RV curve is wanted (every team would
+    // write it), and as many teams as the plan allows whose tasks all fit the grid (at least two), and
+    // no more than the deepest pass of the plan's recent launches asks for: a team beyond it runs a
+    // pass that is cancelled almost always, and its cancel latency and clock share lengthen the launch
+    // (bench chain: 1.334 / 1.339 / 1.342 ms per iteration at 2 / 3 / 4 teams; HD155358 and the
+    // 3-planet system, whose launches reach passes 3 and 4: 5.61 / 4.42 / 3.78 and 11.4 / 9.52 / 8.61)
+    int nteam = 0;
+    if (split && P.rq_t != nullptr && P.rvp != nullptr && P.rvp2 != nullptr && rv_out == nullptr &&
+        ng <= P.rq_xgroups) {
+        nteam = P.n_teams < P.rmax ? P.n_teams : P.rmax;
+        if (nteam > (depth_hint > 2 ? depth_hint : 2)) nteam = depth_hint > 2 ? depth_hint : 2;
+        while (nteam >= 2 && nteam * ntask_split > (int)gridDim.x) nteam--;
+    }
+    const bool team = nteam >= 2;
+    const int ntask_team = nteam * ntask_split;
     // (eager: one task per group of the launch's walkers, as eager_kernel grouped them)
     const int ngw = (W + WPB - 1) / WPB;
     const int ntask = eager ? ngw : (team ? ntask_team : (split ? ntask_split : ng));
@@ -246,16 +278,17 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
 
     for (int t = blockIdx.x; t < ntask; t += gridDim.x) {
         // the task's group, and (split both-direction group) the direction this workgroup integrates
-        int g = t, own = -1, tm = 0;  // tm: the task's team (0 = A, 1 = B; always A without teams)
+        int g = t, own = -1, tm = 0;  // tm: the task's team (0 = A, 1 = B, ...; always A without teams)
         if (team) {
-            if (t < 4 * gq0) {
-                g = t >> 2;
-                own = t & 1;
-                tm = (t >> 1) & 1;
+            if (t < 2 * nteam * gq0) {
+                g = t / (2 * nteam);
+                const int r = t - g * 2 * nteam;
+                own = r & 1;
+                tm = r >> 1;
             } else {
-                const int u = t - 4 * gq0;
-                g = gq0 + (u >> 1);
-                tm = u & 1;
+                const int u = t - 2 * nteam * gq0;
+                g = gq0 + u / nteam;
+                tm = u - (u / nteam) * nteam;
             }
         } else if (split) {
             if (t < 2 * gq0) {
@@ -387,12 +420,20 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
         }
         __syncthreads();
 
-        // team A publishes after pass 1 at rq_t[g] (16 rows of 64 values: live, status, logl, then per
-        // direction open, chi2, lb, previous / best estimate, best chi2), its flag at rq_tf[g] =
-        // (launch generation << 8) | 1 (walkers left for B) or 2 (all done: B stops)
-        gu64* tpub = team ? (gu64*)(P.rq_t + (size_t)g * 16 * 64) : nullptr;
-        gu64* tflag = team ? (gu64*)(P.rq_tf + g) : nullptr;
-        bool cancelled = false;  // (team B: A finished the group)
+        // team t < nteam - 1 publishes after its pass at rq_t[g][t] (16 rows of 64 values: live, status,
+        // logl, then per direction open, chi2, lb, previous / best estimate, best chi2), its flag at
+        // rq_tf[g][t] = (launch generation << 8) | 1 (walkers left for team t + 1) or 2 (all done);
+        // team t > 0 reads team t - 1's.  rq_tf[g][n_teams - 1], the group's done word, is set with
+        // the flag 2 by whichever team finishes the group: every later team polls it, so all of them
+        // stop within one poll of the finish (not one poll per team down the ladder)
+        const size_t ks = (size_t)(P.n_teams - 1);
+        gu64* tpub = team && tm < nteam - 1 ? (gu64*)(P.rq_t + ((size_t)g * ks + tm) * 16 * 64) : nullptr;
+        gu64* tflag = team && tm < nteam - 1 ? (gu64*)(P.rq_tf + (size_t)g * P.n_teams + tm) : nullptr;
+        gu64* tprev = team && tm > 0 ? (gu64*)(P.rq_t + ((size_t)g * ks + tm - 1) * 16 * 64) : nullptr;
+        gu64* tpflag = team && tm > 0 ? (gu64*)(P.rq_tf + (size_t)g * P.n_teams + tm - 1) : nullptr;
+        gu64* tdone = team ? (gu64*)(P.rq_tf + (size_t)g * P.n_teams + ks) : nullptr;
+        const size_t plane2 = (size_t)2 * P.lvx_emax * P.lvx_stride;  // (one team's RV buffer)
+        bool cancelled = false;  // (team t > 0: an earlier team finished the group)
         // a pass's outcome for direction dd of walker slot `lane` (its combiner lane): encounter,
         // non-finite (the walker ends NONFINITE: a halving pass that blows up is not refined further,
         // oracle/rvoracle.c dir_halve -- the last pass would run 2^rmax x the base steps),
@@ -431,10 +472,11 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
             }
         };
         bool finisher = !team && own <= 0;  // the workgroup that finishes the walkers
+        int rf_last = 0;                    // the last pass the group's decisions took
         RPROF_T(pt_loop0);
         RPROF_RT(prt_loop0);
         for (int rf = 1 + tm; rf <= P.rmax; rf++) {
-            const bool bfirst = tm == 1 && rf == 2;  // team B's pass concurrent with A's
+            const bool bfirst = tm > 0 && rf == 1 + tm;  // a later team's pass concurrent with A's
             const uint64_t mk0 = s_mask[0], mk1 = s_mask[1];
             const int amw = (mk0 ? 1 : 0) | (mk1 ? 2 : 0);  // directions a live walker still needs
             if (amw == 0) break;
@@ -515,9 +557,10 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 const bool cmb = work && k == 0 && lane < WPB && ((need >> lane) & 1);
                 const bool hasp = P.rvp != nullptr;
                 double c2 = 0.0, e2 = 0.0, d2 = hasp ? 0.0 : INFINITY;  // (the combiner lanes)
-                // the previous pass's RV, replaced by this pass's: P.rvp (team B: P.rvp2, its own;
-                // its first pass only writes it -- pass 1's RV is still being written by team A)
-                double* pbuf = tm ? P.rvp2 : P.rvp;
+                // the previous pass's RV, replaced by this pass's: P.rvp (team t > 0: its own plane of
+                // P.rvp2; its first pass only writes it -- the previous pass's RV is still being written
+                // by team t - 1)
+                double* pbuf = tm ? P.rvp2 + (size_t)(tm - 1) * plane2 : P.rvp;
                 double* pp = hasp ? pbuf + (size_t)dd_u * P.lvx_emax * P.lvx_stride + (cmb ? wme : 0) : nullptr;
                 for (int e = 0; e < eb; e++) {
                     const bool here = e < Er;
@@ -525,10 +568,10 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                     const int ns = __builtin_amdgcn_readfirstlane(work && here ? r_n[e] * m_r : 0);
                     RPROF_T(pt_s0);
                     if (ns > 0) {
-                        // (team B's first pass stops part-way once team A has finished the group: the
-                        // barrier below then breaks every wave out at this epoch)
+                        // (a later team's first pass stops part-way once an earlier team has finished the
+                        // group: the barrier below then breaks every wave out at this epoch)
                         if (bfirst)
-                            (void)segment_gated_c<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r, tflag,
+                            (void)segment_gated_c<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r, tdone,
                                                                                  nullptr, (gen << 8) | 2ull, late);
                         else
                             segment_gated<D3, NP, L, RVM_REFINE_GUESS>(s, kq, r_len[e] * sc, ns, nt_r, late);
@@ -542,10 +585,10 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                         const double v0 = star_vx<NP, L>(s);
                         if (pl_idx == 0) s_rv[dd_u][e & 1][k_u][slot] = v0;
                     }
-                    // team B polls A's flag (one load per epoch; the result by epoch parity, read by
-                    // every wave after the barrier and rewritten only two barriers later)
+                    // a later team polls the group's done word (one load per epoch; the result by epoch
+                    // parity, read by every wave after the barrier and rewritten only two barriers later)
                     if (bfirst && wv == 0 && lane == 0)
-                        s_cancel[e & 1] = __hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        s_cancel[e & 1] = __hip_atomic_load(tdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                                           ((gen << 8) | 2ull);
                     __syncthreads();
                     if (bfirst && s_cancel[e & 1]) {
@@ -561,7 +604,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                         e2 += fabs((rvx - rv3) * (r + (rv3 - r_rv[e]))) / r_s2[e];
                         if (hasp) {
                             d2 += fabs((rvx - pv) * (r + (pv - r_rv[e]))) / r_s2[e];
-                            if (team && tm == 0)  // (write-through: team B reads pass 1's RV)
+                            if (team && tm < nteam - 1)  // (write-through: the next team reads it)
                                 __hip_atomic_store((gu64*)(pp + (size_t)e * P.lvx_stride),
                                                    (unsigned long long)__double_as_longlong(rvx), __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -584,7 +627,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 if (work && pl_idx == 0) s_enc[dd_u][k_u][slot] = (int)(((s.encm >> lane) & kick_enc_bits<NP>()) != 0);
                 __syncthreads();
                 if (bfirst) {
-                    // team B: this pass's results aside until team A's state is in
+                    // a later team: this pass's results aside until the previous team's state is in
                     if (work && k == 0 && lane < WPB) {
                         int er = 0;
                         for (int q = 0; q < nl; q++) er |= s_enc[dd_u][q][lane];
@@ -606,7 +649,8 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
-            if (cancelled) break;  // (team B: team A finished the group; every wave saw the same flag)
+            if (cancelled) break;  // (a later team: an earlier one finished the group; every wave saw the same flag)
+            rf_last = rf;
             RPROF_T(pt_w0);
             __syncthreads();
             if (emask != 0 && wv == 0) {
@@ -688,15 +732,19 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 }
             }
             if (bfirst) {
-                // team B: team A's state after pass 1 (wave 0; the flag is in by now unless A is
-                // late), then this pass's results for the walkers still open
+                // a later team: the previous team's state after its pass (wave 0; the flag is in by now
+                // unless that team is late), then this pass's results for the walkers still open
                 if (wv == 0) {
                     SpinClock clk;
                     clk.restart();
                     unsigned long long f = 0;
                     bool ok = true;
-                    while (((f = __hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 8) != gen) {
-                        if (clk.expired(pass_ticks(P, 1))) {
+                    while (((f = __hip_atomic_load(tpflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 8) != gen) {
+                        if (__hip_atomic_load(tdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ((gen << 8) | 2ull)) {
+                            f = (gen << 8) | 2ull;  // (an earlier team finished the group)
+                            break;
+                        }
+                        if (clk.expired(pass_ticks(P, tm))) {
                             ok = false;
                             break;
                         }
@@ -711,13 +759,13 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                             __hip_atomic_fetch_add(P.counters, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         }
                     } else if ((f & 0xFF) == 2) {
-                        if (lane == 0) s_cancel[0] = 1;  // (A finished the group after all)
+                        if (lane == 0) s_cancel[0] = 1;  // (an earlier team finished the group after all)
                     } else if (lane < WPB) {
                         // (every row's load in flight before the first LDS store)
                         unsigned long long row_v[15];
 #pragma unroll
                         for (int rw = 0; rw < 15; rw++)
-                            row_v[rw] = __hip_atomic_load(tpub + rw * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            row_v[rw] = __hip_atomic_load(tprev + rw * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         auto ld = [&](int row) { return row_v[row]; };
                         s_live[lane] = (int)ld(0);
                         s_stw[lane] = (int)ld(1);
@@ -738,8 +786,10 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                     break;
                 }
                 // the directions this workgroup integrated: the walkers still live and open there
-                // take pass 2's chi2 and estimate, and the step-doubling change against pass 1's RV
-                // (team A's, write-through) and this pass's (P.rvp2)
+                // take this pass's chi2 and estimate, and the step-doubling change against the previous
+                // pass's RV (team t - 1's, write-through) and this pass's (team t's plane of P.rvp2)
+                const double* rprev = tm == 1 ? P.rvp : P.rvp2 + (size_t)(tm - 2) * plane2;
+                const double* rown = P.rvp2 + (size_t)(tm - 1) * plane2;
                 for (int d3 = 0; d3 < 2; d3++) {
                     const bool mine = own < 0 ? (((d3 == 0 ? mk0 : mk1) != 0)) : d3 == own;
                     if (!mine || wv != 0 || lane >= WPB) continue;
@@ -760,9 +810,9 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                             for (int j = 0; j < RCH; j++) {
                                 const int e = e0 + j < Eb ? e0 + j : Eb - 1;
                                 pvc[j] = __longlong_as_double((long long)__hip_atomic_load(
-                                    (gu64*)(P.rvp + off + (size_t)e * P.lvx_stride), __ATOMIC_RELAXED,
+                                    (gu64*)(rprev + off + (size_t)e * P.lvx_stride), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT));
-                                rvc[j] = P.rvp2[off + (size_t)e * P.lvx_stride];
+                                rvc[j] = rown[off + (size_t)e * P.lvx_stride];
                             }
 #pragma unroll
                             for (int j = 0; j < RCH; j++) {
@@ -774,7 +824,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                                 }
                             }
                         }
-                        pass_result(d3, 2, s_tc2[d3][lane], s_te2[d3][lane], d2b, s_ter[d3][lane]);
+                        pass_result(d3, 1 + tm, s_tc2[d3][lane], s_te2[d3][lane], d2b, s_ter[d3][lane]);
                     }
                     if (lane == 0 && needb)
                         __hip_atomic_fetch_add(P.counters + 3, (unsigned long long)__builtin_popcountll(needb),
@@ -790,7 +840,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 // Double-buffered by the pass's parity: a partner reads pass rf's values before it
                 // publishes rf + 1, which this workgroup awaits before it writes rf + 2.
                 // (each team of a group its own slots and flags)
-                const size_t xb = ((size_t)(g * 2 + tm) * 2) * 2 * 64;
+                const size_t xb = ((size_t)(g * P.n_teams + tm) * 2) * 2 * 64;
                 gu64* mine = (gu64*)(P.rq_x + xb + ((size_t)own * 2 + (rf & 1)) * 64);
                 gu64* theirs = (gu64*)(P.rq_x + xb + ((size_t)(own ^ 1) * 2 + (rf & 1)) * 64);
                 if (lane < WPB) {
@@ -803,9 +853,9 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const unsigned long long tag = (gen << 8) | (unsigned long long)rf;
                 if (lane == 0)
-                    __hip_atomic_store((gu64*)(P.rq_xf + ((size_t)g * 2 + tm) * 2 + own), tag, __ATOMIC_RELAXED,
+                    __hip_atomic_store((gu64*)(P.rq_xf + ((size_t)g * P.n_teams + tm) * 2 + own), tag, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                gu64* tf = (gu64*)(P.rq_xf + ((size_t)g * 2 + tm) * 2 + (own ^ 1));
+                gu64* tf = (gu64*)(P.rq_xf + ((size_t)g * P.n_teams + tm) * 2 + (own ^ 1));
                 SpinClock clk;
                 clk.restart();
                 bool ok = true;
@@ -885,9 +935,10 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                     s_mask[0] = m0;
                     s_mask[1] = m1;
                 }
-                if (team && tm == 0 && own <= 0) {
-                    // team A after pass 1: publish the walkers' state for team B (write-through
-                    // granules, drain, then the flag: 2 when the group is done and B may stop)
+                if (team && tm < nteam - 1 && own <= 0) {
+                    // a team before the last after its pass: publish the walkers' state for the next
+                    // team (write-through granules, drain, then the flag: 2 when the group is done and
+                    // the later teams may stop)
                     if (lane < WPB) {
                         auto st = [&](int row, unsigned long long v) {
                             __hip_atomic_store(tpub + row * 64 + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -906,23 +957,36 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                         }
                     }
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0)
+                    if (lane == 0) {
                         __hip_atomic_store(tflag, (gen << 8) | ((m0 | m1) == 0 ? 2ull : 1ull), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+                        if ((m0 | m1) == 0)
+                            __hip_atomic_store(tdone, (gen << 8) | 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                 }
             }
             __syncthreads();
-            if (team && tm == 0) {
-                // team A ends after pass 1; it finishes the group only when no walker is left for B
+            if (team && tm < nteam - 1) {
+                // a team before the last ends after its pass; it finishes the group only when no walker
+                // is left for the next team
                 finisher = own <= 0 && (s_mask[0] | s_mask[1]) == 0;
                 break;
             }
         }
         RPROF_T(pt_loop1);
         RPROF_RT(prt_loop1);
-        if (team && tm == 1) finisher = own <= 0 && !cancelled;
+        if (team && tm == nteam - 1) finisher = own <= 0 && !cancelled;
+        // a cancelled team before the last passes the cancel on (the next team polls only its flag)
+        if (team && cancelled && tm < nteam - 1 && own <= 0 && threadIdx.x == 0)
+            __hip_atomic_store(tflag, (gen << 8) | 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the group's walkers, as the likelihood kernel would have finished them (rvm_walker.h;
         // a split group's by its forward-direction workgroup, of team A or B)
+        // the group's depth for the next launches' team count (generation-tagged: a larger generation
+        // always wins the max)
+        if (finisher && threadIdx.x == 0 && P.depth_w != nullptr && rf_last > 0)
+            __hip_atomic_fetch_max(P.depth_w + gen % (RVM_DEPTH_WINDOW + 1), (gen << 8) | (unsigned long long)rf_last,
+                                   __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         if (finisher && wv == 0 && lane < WPB && lane < cnt && s_skip[lane]) {
             logl_out[wme] = -INFINITY;
             status_out[wme] = RVM_STATUS_SKIPPED;

@@ -1,10 +1,10 @@
-"""Study (CPU, oracle; usage: two_pass_study.py [iterations] [s2|hd155358]): the walker slots of the steady-state sampler's speculative launches
-(scripts/probe/steady_bench.py's chain: ens_it2000.npy, seed 2017, 6144 slots per iteration -- half
-0's proposals and half 1's against both outcomes of its partner) through the walker-level rule with
-the sampler's accept inputs (certain rejects), restated by the oracle.  Per iteration: how many
-slots reach each stage, and for the slots that need two or more halving passes their extension
-change d, final logL against their current lnp, and whether the accept test passes -- which walkers
-make half of the steady state's refinement launches take a second pass (GPU trace, r04n)."""
+"""Study (CPU, oracle): the walker-directions of a steady-state chain that need two or more halving
+passes (HD155358 by default: the ensemble of test_stretch_vs_ias15_steady_state_other_systems).
+For each such direction (not cut): per pass rf = 0 (the plan's step) .. 4 the estimate est_rf (the
+chi2 change when the coarsest level is dropped, / npoints / tol_dir: the kernel's settle test is
+est <= 1), the step-doubling change against the previous pass, and the pass's actual error
+|chi2 - chi2_IAS15| / npoints -- whether the passes these walkers climb are needed for T2, or the
+estimate over-reads.  usage: deep_walker_study.py [iterations] [hd155358|s2]  -> JSON lines."""
 import json
 import os
 import sys
@@ -23,26 +23,25 @@ from rvmcmc.state import State  # noqa: E402
 
 
 def main():
-    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 6
-    system = sys.argv[2] if len(sys.argv) > 2 else "s2"
-    if system == "hd155358":  # (the ensemble of test_stretch_vs_ias15_steady_state_other_systems)
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    system = sys.argv[2] if len(sys.argv) > 2 else "hd155358"
+    if system == "hd155358":
         from test_gpu_ias15_decisions import _hd
 
         planets, obs = _hd()
         X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_hd155358_it1000.npy"))
     else:
-        planets = S2_PLANETS
-        obs = s2_obs_oracle()  # (bench.py's FakeObservation, restated on the CPU)
+        planets, obs = S2_PLANETS, s2_obs_oracle()
         X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_it2000.npy"))
     s = State(planets=[dict(p) for p in planets])
     pm = s.param_map()
     dim = s.Nvars
-    W = len(X0)
-    n = W // 2
+    n = len(X0) // 2
     cfg = engine.IntegratorConfig()
     dt, mult, _ = cfg.plan_args(planets)
     tol, rmax, guard, _ = cfg.resolve(planets)
     nt = os.cpu_count() or 8
+    N = obs.Npoints
 
     def adapt(A, ctx=None):
         P = IP.to_oracle(pm, A)
@@ -56,17 +55,33 @@ def main():
             parts = list(ex.map(one, idx))
         return [np.concatenate([p[k] for p in parts]) for k in range(len(parts[0]))]
 
+    def analyse(P, d):
+        pl = [{"m": P[p, 0], "a": P[p, 1], "h": P[p, 2], "k": P[p, 3], "l": P[p, 4]} for p in range(len(P))]
+        t, o, e = (obs.tf, obs.rvf, obs.errorf) if d == 0 else (obs.tb, obs.rvb, obs.errorb)
+        s2 = e * e
+        ias = O.get_rv_ias15(pl, t, 1.0)[0]
+        c_ias = float(np.sum((ias - o) ** 2 / s2)) / N
+        row, prev = [], None
+        for rf in range(5):
+            m = tuple(int(k) << rf for k in mult)
+            r = O.whx_rv(pl, t, dt, m, 1.0)[0]
+            r3 = O.whx_rv(pl, t, dt, m[1:], 1.0)[0]
+            est = float(np.sum(np.abs((r - r3) * (r + r3 - 2 * o)) / s2)) / N / (0.5 * tol)
+            dch = None if prev is None else float(np.sum(np.abs((r - prev) * (r + prev - 2 * o)) / s2)) / N / (0.5 * tol)
+            c = float(np.sum((r - o) ** 2 / s2)) / N
+            row.append({"rf": rf, "est_over_tol": est, "change_over_tol": dch, "err": abs(c - c_ias)})
+            prev = r
+        return row
+
     pos = [X0[:n].copy(), X0[n:].copy()]
     lnp = [adapt(p)[0] for p in pos]
     for it in range(iters):
-        # half 0 against half 1 (as the speculative launch's slots [0, n))
         u1, u2, u3 = stretch_uniforms(2017, 0, n, it, 0)
         q0, z0 = IP.stretch_proposal(pos[0], pos[1], u1, u2, 2.0)
         ctx0 = dict(mode=np.ones(n, dtype=np.int32), dim=dim, z=z0, u=u3, lnp0=lnp[0])
         l0, s0, rf0, _, _, cut0 = adapt(q0, ctx0)
         with np.errstate(invalid="ignore"):
             acc0 = (dim - 1.0) * np.log(z0) + l0 - lnp[0] > np.log(u3)
-        # half 1 against both outcomes of its partner (slots [n, 3n))
         v1, v2, v3 = stretch_uniforms(2017, n, n, it, 1)
         zz = ((2.0 - 1.0) * v1 + 1) ** 2 / 2.0
         j = np.clip(np.floor(v2 * n).astype(int), 0, n - 1)
@@ -76,25 +91,14 @@ def main():
         ctx1 = dict(mode=np.ones(2 * n, dtype=np.int32), dim=dim, z=np.concatenate([zz, zz]),
                     u=np.concatenate([v3, v3]), lnp0=np.concatenate([lnp[1], lnp[1]]))
         l1, s1, rf1, _, _, cut1 = adapt(np.concatenate([qa, qb]), ctx1)
-        rf = np.concatenate([rf0, rf1]).max(axis=1)
-        cc = np.concatenate([cut0, cut1])
-        cut = (cc & 1).any(axis=1)
-        jumped = (cc & 2).any(axis=1)  # (study build with -DJUMP_T: the walker started at rf = 2)
-        # latency of the launch's refinement in units of one rf = 1 pass: the deepest walker's passes
-        units = np.where(rf >= 2, 2.0 ** (rf - 1) * 2 - np.where(jumped, 2, 1), 0)  # sum_{r=r0}^{rf-1} 2^(r-1)
-        lall = np.concatenate([l0, l1])
-        z3 = np.concatenate([z0, zz, zz])
-        u3a = np.concatenate([u3, v3, v3])
-        lp0 = np.concatenate([lnp[0], lnp[1], lnp[1]])
-        with np.errstate(invalid="ignore", divide="ignore"):
-            dacc = (dim - 1.0) * np.log(z3) + lall - lp0 - np.log(u3a)
-        deep = np.nonzero(rf >= 3)[0]
-        print(json.dumps({"it": it, "stage_hist": np.bincount(rf, minlength=6).tolist(), "cut": int(cut.sum()),
-                          "jumped": int(jumped.sum()), "refine_units": float(units.max()),
-                          "deep_slots": [{"slot": int(i), "stage": int(rf[i]), "cut": bool(cut[i]),
-                                          "accept_margin": float(dacc[i]), "logl": float(lall[i]),
-                                          "lnp0": float(lp0[i])} for i in deep]}), flush=True)
-        # the chain goes on with half 0's decisions, then half 1's variant by its partner's decision
+        Q = np.concatenate([q0, qa, qb])
+        rf = np.concatenate([rf0, rf1])
+        cut = np.concatenate([cut0, cut1])
+        for slot, d in zip(*np.nonzero((rf >= 3) & ((cut & 1) == 0))):
+            P = IP.to_oracle(pm, Q[slot:slot + 1])[0]
+            print(json.dumps({"it": it, "slot": int(slot), "dir": int(d), "stage": int(rf[slot, d]),
+                              "e": [float(np.hypot(P[p, 2], P[p, 3])) for p in range(len(P))],
+                              "passes": analyse(P, d)}), flush=True)
         pos[0] = np.where(acc0[:, None], q0, pos[0])
         lnp[0] = np.where(acc0, l0, lnp[0])
         pick = acc0[j]

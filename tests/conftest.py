@@ -31,6 +31,16 @@ def hd_obs_oracle():
     return O.obs_from_file(os.path.join(GOLDEN, "HD155358.vels"), Npoints=100)
 
 
+# HD155358 (BASELINE config 3): the solution mcmc_benchmark_*.py starts from (a, h, k, m, l per planet)
+HD_SOL = [6.57730330e-01, -9.72263877e-02, -7.82798396e-02, 8.84031737e-04, 4.42804990e+00,
+          1.04404207e+00, -2.05622789e-02, -1.08797961e-01, 8.30379710e-04, 1.49919861e+00]
+
+
+def hd_planets():
+    return [{"m": HD_SOL[3], "a": HD_SOL[0], "h": HD_SOL[1], "k": HD_SOL[2], "l": HD_SOL[4]},
+            {"m": HD_SOL[8], "a": HD_SOL[5], "h": HD_SOL[6], "k": HD_SOL[7], "l": HD_SOL[9]}]
+
+
 S2_PLANETS = [{"m": 1.2e-3, "a": 0.88, "h": 0.218, "k": 0.015, "l": 0.3},
               {"m": 2.1e-3, "a": 1.44 + 0.11, "h": 0.16, "k": 0.02, "l": 2.2}]  # mcmc_benchmark_mh.py:32
 S2_SCALES = {"m": 1.5e-3, "a": 0.3, "h": 0.1, "k": 0.1, "l": 3.141592653589793 / 2.}  # mcmc_benchmark_emcee.py:51

@@ -358,31 +358,42 @@ def test_t1_eccentricity_guard(W):
     assert (rf >= 1).sum() > (rf0 >= 1).sum()
 
 
-def test_refinement_layouts_bit_identical():
-    """The refinement kernel's layouts -- two teams (pass 1 and pass 2 at once, the default), one
-    team with each direction on its own workgroup (RVM_REFINE_TEAMS=0), both directions in one
-    workgroup (RVM_REFINE_SPLIT=0) -- take the same decisions with the same bits: four speculative
-    iterations of the sampler at the bench chain's steady state (extensions, halving passes,
-    certain rejects, two-pass walkers), positions, log-probabilities and plan counters compared."""
+@pytest.mark.parametrize("system", ["s2", "hd155358"])
+def test_refinement_layouts_bit_identical(system):
+    """The refinement kernel's layouts -- teams (passes 1, 2, 3 at once, the default; 2 and 4 teams),
+    one team with each direction on its own workgroup (RVM_REFINE_TEAMS=0), both directions in one
+    workgroup (RVM_REFINE_SPLIT=0) -- take the same decisions with the same bits: speculative
+    iterations of the sampler at a steady state (extensions, halving passes, certain rejects,
+    two-pass walkers; HD155358's launches climb to passes 3 and 4), positions, log-probabilities and
+    plan counters compared."""
     import os
 
-    from conftest import ROOT
+    from conftest import ROOT, hd_planets
     from rvmcmc.ensemble import EnsembleSampler
     from rvmcmc.state import State
 
     torch = _torch()
-    X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_it2000.npy"))
+    if system == "s2":
+        planets, obs = S2_PLANETS, s2_obs_oracle
+        X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_it2000.npy"))
+        iters = 4
+    else:
+        planets = hd_planets()
+        obs = lambda: O.obs_from_file(os.path.join(ROOT, "tests", "golden", "HD155358.vels"), Npoints=100)  # noqa: E731
+        X0 = np.load(os.path.join(ROOT, "scripts", "probe", "ens_hd155358_it1000.npy"))
+        iters = 6
     runs = []
-    for env in ({}, {"RVM_REFINE_TEAMS": "0"}, {"RVM_REFINE_SPLIT": "0"}):
+    for env in ({}, {"RVM_REFINE_TEAMS": "2"}, {"RVM_REFINE_TEAMS": "4"}, {"RVM_REFINE_TEAMS": "0"},
+                {"RVM_REFINE_SPLIT": "0"}):
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
-            s = State(planets=[dict(p) for p in S2_PLANETS])
-            ens = EnsembleSampler(len(X0), s, s2_obs_oracle(), seed=2017)  # (a fresh observation set: fresh plans)
+            s = State(planets=[dict(p) for p in planets])
+            ens = EnsembleSampler(len(X0), s, obs(), seed=2017)  # (a fresh observation set: fresh plans)
             ens.set_positions(X0)
             ens.compute_lnprob()
             ens.plan.faults(reset=True)
-            for _ in range(4):
+            for _ in range(iters):
                 ens.step()
             torch.cuda.synchronize()
             runs.append((ens.gather_positions(), np.concatenate([l.cpu().numpy() for l in ens.lnp]),
@@ -394,6 +405,7 @@ def test_refinement_layouts_bit_identical():
                 else:
                     os.environ[k] = v
     assert runs[0][2]["refined"] > 0 and runs[0][2]["truncated"] > 0
+    assert runs[0][2]["handoff_timeouts"] == 0
     for X, lp, f in runs[1:]:
         np.testing.assert_array_equal(X, runs[0][0])
         np.testing.assert_array_equal(lp, runs[0][1])
