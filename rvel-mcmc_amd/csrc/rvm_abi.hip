@@ -444,6 +444,10 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     P.eflag = nullptr;
     P.eager_max = 0;
     P.eager_passes = 0;
+    {
+        const char* es = getenv("RVM_EAGER_SPLIT");  // (A/B knob: 0 keeps both directions in one block)
+        P.eager_split = es && es[0] == '0' ? 0 : 1;
+    }
     P.e2_guard = INFINITY;
     P.lvx_emax = 0;
     P.lvx_stride = 0;

@@ -163,6 +163,7 @@ struct DevPlan {
     unsigned long long* eflag;
     int32_t eager_max;
     int32_t eager_passes;  // (1 or 2: how many halving passes eager_kernel runs)
+    int32_t eager_split;   // 1: an eager launch's refinement runs each direction of a group on its own block
     // the launch generation (device word, >= 1): the tag of the refinement kernel's exchange flags and
     // the eager blocks' claim words.  Read on the device by both kernels and advanced on the device
     // after every launch (the refinement kernel's last block, or gen_bump_kernel after an eager

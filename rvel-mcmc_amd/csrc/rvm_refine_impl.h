@@ -225,9 +225,13 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
     }
     const bool team = nteam >= 2;
     const int ntask_team = nteam * ntask_split;
-    // (eager: one task per group of the launch's walkers, as eager_kernel grouped them)
+    // (eager: one task per group of the launch's walkers, as eager_kernel grouped them -- two, one per
+    // direction, when they fit the grid: the eager split, round 6; a 4-wave block otherwise runs the
+    // directions of the passes after the eager ones one after the other.  RVM_EAGER_SPLIT=0: one)
     const int ngw = (W + WPB - 1) / WPB;
-    const int ntask = eager ? ngw : (team ? ntask_team : (split ? ntask_split : ng));
+    const bool esplit = eager && P.eager_split && P.rq_x != nullptr && ngw <= P.rq_xgroups &&
+                        ((int)gridDim.x & 1) == 0 && 2 * ngw <= (int)gridDim.x;
+    const int ntask = eager ? (esplit ? 2 * ngw : ngw) : (team ? ntask_team : (split ? ntask_split : ng));
     if ((int)blockIdx.x >= ntask) return;
 
     // LDS: both directions' schedules ([d][seg_h1 | obs_rv | obs_s2 | (seg_n, obs_idx)], E_d each),
@@ -290,6 +294,9 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 g = gq0 + u / nteam;
                 tm = u - (u / nteam) * nteam;
             }
+        } else if (esplit) {
+            g = t >> 1;
+            own = t & 1;
         } else if (split) {
             if (t < 2 * gq0) {
                 g = t >> 1;
@@ -490,6 +497,7 @@ __global__ __launch_bounds__(NW * 64) void refine_kernel(const DevPlan P, const 
                 if (threadIdx.x == 0) {
                     int em = 0;
                     for (int d3 = 0; d3 < 2; d3++) {
+                        if (own >= 0 && d3 != own) continue;  // (eager split: the partner's direction is its own)
                         if (!((amw >> d3) & 1))
                             __hip_atomic_store(ef + 6 + d3, (gen << 8) | 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         else if (rf <= P.eager_passes && !claim_item(ef + 2 + 2 * (rf - 1) + d3, gen, 3ull))
