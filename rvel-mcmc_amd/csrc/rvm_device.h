@@ -325,6 +325,9 @@ __device__ __forceinline__ void lane_finish(Lane<NP>& s) {
     s.GM2 = 2.0 * s.GM;
     s.idmin2 = 1.0 / s.dmin2;  // +inf for dmin2 = 0 (no exit distance)
     if constexpr (NP == 2) {
+        // (kick2 tests |r'| < dmin, the star -- planet-1 distance, on planet 1's lanes only: +inf on
+        // planet 2's makes the test false there without masking its ballot)
+        if (s.p != 0) s.idmin2 = __builtin_inf();
         // kick2: lane of planet 1: (A, B, C) = (0, -m2, m2); planet 2: (M2, -M2/M1, -m1 M2/M1)
         const bool p1 = s.p == 0;
         const double q = s.GM * s.iMi[1];
@@ -600,6 +603,28 @@ __device__ __forceinline__ bool lane_encountered(const Lane<NP>& s) {
     return ((s.encm >> base) & bits) != 0;
 }
 
+// The same as a wave mask (scalar work on Lane::encm): every lane of a walker whose kick_enc_bits
+// hold an encounter -- lane i is set exactly where lane_encountered is true on lane i
+template <int NP>
+__device__ __forceinline__ uint64_t encountered_lanes(uint64_t m) {
+    constexpr int L = LanesPerWalker<NP>::value;
+    if constexpr (L == 1) {
+        return m;
+    } else if constexpr (L == 2) {
+        const uint64_t t = (m | (m >> 1)) & 0x5555555555555555ull;  // (bits 3: either lane of the pair)
+        return t | (t << 1);
+    } else {
+        const uint64_t t = (NP == 3 ? (m | (m >> 1) | (m >> 2) | (m >> 3)) : m) & 0x1111111111111111ull;
+        return t | (t << 1) | (t << 2) | (t << 3);
+    }
+}
+
+// The wave's vote on the first Halley step (drift below) takes the failing lanes' mask and, only when
+// it is not empty, removes the lanes of walkers that have met an encounter (their values are
+// discarded, so their solves must not send the wave to the second step): ok1 = the lane is not in
+// the result, exactly as ok1 = !bad1 || lane_encountered(s).  Round 6: the per-lane
+// lane_encountered test took 3 VALU and 3 SALU of every gated step (~5 % of a lone wave's step).
+
 // G5: one more term of the guess's series, X = u (1 - us/2 + u^2 T3 + u^3 T4 + u^4 T5),
 //   T5 = (9 beta^2 - 19 beta g + 90 beta s^2 + 10 g^2 - 105 g s^2 + 105 s^4) / 120
 // (series reversion of u = G1 + s G2 + g G3 to fifth order; scripts/kepler_guess_series.py): ~9 VALU
@@ -723,26 +748,38 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
         // clean step (the early vote drained the lone wave's pipeline at the end of the Halley chain:
         // ~125 cycles per step).  A failing lane's update is recomputed.  ACC 3 gives exactly
         // ACC 0's bits.
-        const bool ok1 = (fabs(z) <= B && halley_ok<NT>(Q, x)) || lane_encountered(s);
+        // (a ballot per compare: each is the compare's own mask, where the ballot of their OR was
+        // materialised as a lane value and compared again -- two more instructions every step; and
+        // opaque, so ok1 below is read from the mask rather than re-derived from the compares)
+        uint64_t raw = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, x));
+        asm volatile("" : "+s"(raw));
         o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
-        if (__builtin_expect(ballot(!ok1) != 0, 0)) {
+        if (__builtin_expect(raw != 0, 0)) {
 #ifdef RVM_PROFILE_FAILS
             rare_count(0, 0);
 #endif
+            // (the lanes of encountered walkers out: vote_fails; with none left every lane is ok)
+            const uint64_t fm = raw & ~encountered_lanes<NP>(s.encm);
+            const bool ok1 = ((fm >> (threadIdx.x & 63)) & 1) == 0;
             second_chance(ok1, ACC == 4);
             if (!ok1) o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
         }
     } else {
         if constexpr (GATED) {
-            const bool ok1 = (fabs(z) <= B && halley_ok<NT>(Q, x)) || lane_encountered(s);
-            if (ballot(!ok1) != 0) {
+            uint64_t raw = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, x));  // (as in the late vote)
+            asm volatile("" : "+s"(raw));
+            if (__builtin_expect(raw != 0, 0)) {
 #ifdef RVM_PROFILE_FAILS
                 rare_count(0, 0);
 #endif
-                second_chance(ok1, ACC == 1 || ACC == 2);
+                const uint64_t fm = raw & ~encountered_lanes<NP>(s.encm);
+                second_chance(((fm >> (threadIdx.x & 63)) & 1) == 0, ACC == 1 || ACC == 2);
             }
         } else {
-            bad = bad || ((!(fabs(z) <= B) || !halley_ok<NT>(Q, x)) && !lane_encountered(s));
+            // (the wave's verdict, on every lane: the caller ballots it at the segment's end)
+            uint64_t raw = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, x));
+            if (__builtin_expect(raw != 0, 0)) raw &= ~encountered_lanes<NP>(s.encm);
+            bad = bad || raw != 0;
         }
         o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     }
@@ -894,7 +931,7 @@ __device__ __forceinline__ void kick2(Lane<2>& s, double c1875 = 1.875) {
     // own pair on every lane; star--planet-1 from |r'_1| on planet 1's lanes only (|r'_2| is a
     // Jacobi distance, not a pair)
     const double ir2 = s.ir * s.ir;
-    s.encm |= ballot(rsq < s.dmin2) | (ballot(ir2 > s.idmin2) & 0x5555555555555555ull);
+    s.encm |= ballot(rsq < s.dmin2) | ballot(ir2 > s.idmin2);  // (idmin2 +inf on planet 2's lanes)
     const double ic = rcube_nr(rsq, c1875);
     const double ico = pair_swap<L>(ic);
     const double A = s.kAh * (s.ir * ir2);
@@ -1043,7 +1080,7 @@ __device__ __forceinline__ KickPrep<NP> kick_prep(Lane<NP>& s, double c1875) {
             rsq = fma(oz, oz, rsq);
         }
         const double ir2 = s.ir * s.ir;
-        s.encm |= ballot(rsq < s.dmin2) | (ballot(ir2 > s.idmin2) & 0x5555555555555555ull);
+        s.encm |= ballot(rsq < s.dmin2) | ballot(ir2 > s.idmin2);  // (idmin2 +inf on planet 2's lanes)
         k.ic = rcube_nr(rsq, c1875);
         k.ico = pair_swap<L>(k.ic);
         k.ir3 = s.ir * ir2;
