@@ -766,20 +766,18 @@ __device__ __forceinline__ void drift(Lane<NP>& s, double dt, bool& bad, const V
         }
     } else {
         if constexpr (GATED) {
-            uint64_t raw = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, x));  // (as in the late vote)
-            asm volatile("" : "+s"(raw));
-            if (__builtin_expect(raw != 0, 0)) {
+            // (the early vote keeps the per-lane encounter test: the likelihood kernel's gated levels
+            // run it two waves to a SIMD, where the late vote's scalar form measured slower)
+            const bool ok1 = (fabs(z) <= B && halley_ok<NT>(Q, x)) || lane_encountered(s);
+            if (ballot(!ok1) != 0) {
 #ifdef RVM_PROFILE_FAILS
                 rare_count(0, 0);
 #endif
-                const uint64_t fm = raw & ~encountered_lanes<NP>(s.encm);
-                second_chance(((fm >> (threadIdx.x & 63)) & 1) == 0, ACC == 1 || ACC == 2);
+                second_chance(ok1, ACC == 1 || ACC == 2);
             }
         } else {
             // (the wave's verdict, on every lane: the caller ballots it at the segment's end)
-            uint64_t raw = ballot(!(fabs(z) <= B)) | ballot(!halley_ok<NT>(Q, x));
-            if (__builtin_expect(raw != 0, 0)) raw &= ~encountered_lanes<NP>(s.encm);
-            bad = bad || raw != 0;
+            bad = bad || ((!(fabs(z) <= B) || !halley_ok<NT>(Q, x)) && !lane_encountered(s));
         }
         o = drift_apply<D3>(s, dt, beta, eta, zeta, G0, G1, G2, G3, fp, fpp, Q);
     }
