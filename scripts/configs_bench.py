@@ -141,6 +141,10 @@ def config4(chains=256, steps=100, fused=True, burn_in=None, steady_steps=400):
         # (an event on the launch stream after each step: the steps' own durations, for their spread --
         # a step whose centres need a second halving pass takes about twice as long)
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+        # (the burn-in's steps are enqueued without a wait: the clock starts once they have run --
+        # rounds 6's first steady-state figures timed their tail too, 2.6 / 1.2 ms per step against
+        # the steps' own 0.8, scripts/probe/smala_host_probe.py)
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         evs[0].record()
         for i in range(n):
