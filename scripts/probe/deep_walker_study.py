@@ -4,7 +4,9 @@ For each such direction (not cut): per pass rf = 0 (the plan's step) .. 4 the es
 chi2 change when the coarsest level is dropped, / npoints / tol_dir: the kernel's settle test is
 est <= 1), the step-doubling change against the previous pass, and the pass's actual error
 |chi2 - chi2_IAS15| / npoints -- whether the passes these walkers climb are needed for T2, or the
-estimate over-reads.  usage: deep_walker_study.py [iterations] [hd155358|s2]  -> JSON lines."""
+estimate over-reads; and the same for a three-level pass (the coarsest three levels of the pass,
+6 x 2^rf steps per base step at most: est3, err3).
+usage: deep_walker_study.py [iterations] [hd155358|s2]  -> JSON lines."""
 import json
 import os
 import sys
@@ -69,7 +71,13 @@ def main():
             est = float(np.sum(np.abs((r - r3) * (r + r3 - 2 * o)) / s2)) / N / (0.5 * tol)
             dch = None if prev is None else float(np.sum(np.abs((r - prev) * (r + prev - 2 * o)) / s2)) / N / (0.5 * tol)
             c = float(np.sum((r - o) ** 2 / s2)) / N
-            row.append({"rf": rf, "est_over_tol": est, "change_over_tol": dch, "err": abs(c - c_ias)})
+            e = {"rf": rf, "est_over_tol": est, "change_over_tol": dch, "err": abs(c - c_ias)}
+            if rf >= 1:  # (a three-level pass: the coarsest three of the four, max 6 x 2^rf per base step)
+                r3l = O.whx_rv(pl, t, dt, m[:3], 1.0)[0]
+                r3d = O.whx_rv(pl, t, dt, m[1:3], 1.0)[0]
+                e["est3_over_tol"] = float(np.sum(np.abs((r3l - r3d) * (r3l + r3d - 2 * o)) / s2)) / N / (0.5 * tol)
+                e["err3"] = abs(float(np.sum((r3l - o) ** 2 / s2)) / N - c_ias)
+            row.append(e)
             prev = r
         return row
 
