@@ -1036,6 +1036,12 @@ enum { RVO_UNRESOLVED = 4 };
 #ifndef FLOOR_BOUND
 #define FLOOR_BOUND 4.0
 #endif
+/* (round 6) a walker whose pericentre passage is quicker still than the eccentricity guard's --    */
+/* (1 - e) below CUT_ECC_FACTOR x (1 - ecc_guard) -- keeps the main pass's bound after the extension: */
+/* the extension's change does not bound its error there (rvm_internal.h RVM_CUT_ECC_FACTOR)         */
+#ifndef CUT_ECC_FACTOR
+#define CUT_ECC_FACTOR 0.6712
+#endif
 
 
 static double margin_of(double x, double bound) {
@@ -1058,7 +1064,7 @@ static int decide_accepts(const rvo_decide* dc, double lp) {
 typedef struct {
     int np;
     const double* pl;
-    double hill_factor, dt, tol_dir, npoints, ecc_guard;
+    double hill_factor, dt, tol_dir, npoints, ecc_guard, e2_cut;
     int nl, ext_mult, rf_max, adaptive, ext;
     const int* mult;
     double w[8], w3[8], w5[9];
@@ -1173,6 +1179,15 @@ static void dir_extend(const rvo_plan_ctx* X, rvo_dir* D) {
         D->est = dd / X->npoints;
         D->open = 0;
         D->lb = c5;
+    } else if (X->e2_cut < INFINITY) {
+        /* (past the cut guard the bound stays the main pass's) */
+        double e2 = 0.0;
+        for (int p = 0; p < X->np; p++) {
+            const double h = X->pl[p * RVO_PSTRIDE + 2], k = X->pl[p * RVO_PSTRIDE + 3];
+            if (h * h + k * k > e2) e2 = h * h + k * k;
+        }
+        if (margin_of(e2, X->e2_cut) < D->margin) D->margin = margin_of(e2, X->e2_cut);
+        if (e2 <= X->e2_cut) D->lb = lb_of(c5, dd, D->est_raw);
     } else {
         D->lb = lb_of(c5, dd, D->est_raw);
     }
@@ -1293,6 +1308,10 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
     X.tol_dir = tol_dir;
     X.npoints = npoints;
     X.ecc_guard = ecc_guard;
+    {
+        const double ec = 1.0 - (1.0 - ecc_guard) * CUT_ECC_FACTOR;
+        X.e2_cut = ecc_guard > 0.0 ? ec * ec : INFINITY;
+    }
     X.nl = nl;
     X.mult = mult;
     X.rf_max = rf_max;

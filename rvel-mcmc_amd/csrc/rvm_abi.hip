@@ -449,6 +449,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
         P.eager_split = es && es[0] == '0' ? 0 : 1;
     }
     P.e2_guard = INFINITY;
+    P.e2_cut = INFINITY;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
     P.ext_spec = 0;
@@ -648,6 +649,10 @@ int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e) {
     if (!plan) return fail(-1, "rvm_plan_set_verify_eccentricity: null plan");
     if (std::isnan(e) || e >= 1.0) return fail(-1, "rvm_plan_set_verify_eccentricity: e must be < 1 (<= 0: off)");
     plan->dev.e2_guard = e > 0.0 ? e * e : INFINITY;
+    {
+        const double ec = 1.0 - (1.0 - e) * rvm::RVM_CUT_ECC_FACTOR;
+        plan->dev.e2_cut = e > 0.0 ? ec * ec : INFINITY;
+    }
     return 0;
 }
 

@@ -36,6 +36,13 @@ constexpr double RVM_CUT_EST_FACTOR = 100.0;
 // logL from the 5th halving on -- the finer steps' accumulated rounding -- and ended UNRESOLVED on
 // the GPU where the oracle's rounding happened to settle it)
 constexpr double RVM_FLOOR_BOUND = 4.0;
+// the certain-reject cut after the extension (round 6): for a walker whose pericentre passage is
+// quicker still than the eccentricity guard's -- (1 - e) below this factor x (1 - e_guard), 1.82x
+// quicker -- the extension's change does not bound its error (HD155358's steady state, planets of
+// e = 0.79-0.84: the extension's chi2 50-500x the true one, its change a third of the error; three
+// proposals in 24576 cut that IAS15 accepts, scripts/probe/decision_mismatch_probe.py), so its bound
+// stays the main pass's (chi2 - 100 est); oracle/rvoracle.c CUT_ECC_FACTOR
+constexpr double RVM_CUT_ECC_FACTOR = 0.6712;
 // launches of fewer walkers than this run the extension after the main pass (only when a walker is
 // flagged) instead of as a concurrent fifth wave of the one-group-per-block layout (launch_logl_t)
 constexpr int RVM_CX_MIN_WALKERS = 32;
@@ -114,6 +121,9 @@ struct DevPlan {
     // eccentricity guard (rvm_plan_set_verify_eccentricity; +inf: off): a walker with a planet of
     // e^2 above it counts as above the bound after the main pass (it gets the extension)
     double e2_guard;
+    // ... and above this e^2 (from the guard: RVM_CUT_ECC_FACTOR) the extension's change gives no
+    // lower bound for the certain-reject cut (+inf: always)
+    double e2_cut;
     int32_t lvx_emax, lvx_stride;
     // walkers handed from the likelihood kernel to the refinement kernel (rvm_refine.hip): a walker
     // with a direction still open after the main pass and the extension (and no certain reject) is

@@ -971,7 +971,8 @@ void logl_kernel(const DevPlan P, const int W,
                     if ((s_need[0] | (G > 1 ? s_need[1] : 0ull)) != 0)
                         extend_stage(lvl, grp, d, need, chi2w, enc, c5x, ddx);
                 }
-                lbw = cenc ? 0.0 : direction_lb(need, chi2, est, need0 && P.ext_mult > 0, c5x, ddx);
+                // (the extension's bound only below the cut guard, DevPlan::e2_cut)
+                lbw = cenc ? 0.0 : direction_lb(need, chi2, est, need0 && P.ext_mult > 0 && e2c <= P.e2_cut, c5x, ddx);
             }
         }
         if (cmb && wo < W) {
@@ -1262,7 +1263,7 @@ void logl_kernel(const DevPlan P, const int W,
                 // (lane = slot, extend_pass's convention) through LDS
                 if (valid && pl_idx == 0) {
                     s_fchi[ul][slot] = chi2w;
-                    s_fenc[ul][slot] = enc | (need ? 16 : 0) | (cenc ? 32 : 0);
+                    s_fenc[ul][slot] = enc | (need ? 16 : 0) | (cenc ? 32 : 0) | (e2w > P.e2_cut ? 64 : 0);
                     s_fx[0][ul][slot] = est;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1281,7 +1282,7 @@ void logl_kernel(const DevPlan P, const int W,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 double xc5 = 0.0, xdd = 0.0;
                 extend_pass(ul, d, nm, nd, c2, en, xc5, xdd);
-                const double lb = cn ? 0.0 : direction_lb(nd, cm, es, (f & 16) != 0, xc5, xdd);
+                const double lb = cn ? 0.0 : direction_lb(nd, cm, es, (f & 16) != 0 && (f & 64) == 0, xc5, xdd);
                 if (cl) finish_recompute(w0 + lane, c2, en, nd, lb);
             } else if (valid && pl_idx == 0) {
                 if (lsx && need) {  // the main pass's RV of an open direction (the ring, consume above)
@@ -1290,7 +1291,7 @@ void logl_kernel(const DevPlan P, const int W,
                         P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = cenc ? __builtin_nan("") : rg[(size_t)e * WPB];
                 }
                 finish_recompute(w, chi2w, enc, need,
-                                 cenc ? 0.0 : direction_lb(need, chi2m, est, lsx && need0, c5x, ddx));
+                                 cenc ? 0.0 : direction_lb(need, chi2m, est, lsx && need0 && e2w <= P.e2_cut, c5x, ddx));
             }
 #ifdef RVM_PROFILE
             prof_dec(rt_arr, nl - 1);
