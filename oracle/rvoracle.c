@@ -1076,11 +1076,25 @@ typedef struct {
     int cnt;
     double sign;
     double *lv0, *lv, *prev; /* main pass's levels (+ the extension), a halving pass's, the last RV */
-    int st, open, bad, stage, cut, floor;
+    int st, open, bad, stage, cut, floor, pend;
     double chi2, lb, est, est_raw, margin;
     double pest, best, bchi; /* the previous halving pass's est, the smallest est and its chi2 */
     double dext;             /* the extension's change dd / npoints (0: none) */
 } rvo_dir;
+
+/* (study, scripts/probe/encounter_confirm_study.py; 0 = the product rule): 1 = an encounter the main
+ * pass's finest level sees does not end the walker either, 2 = besides, a halving pass's encounter
+ * ends it only when the stage before it saw one too (a finer pass confirms), 3 = rule 1 and the
+ * extension's encounter refines on too (halving passes end it), 4 = rule 3 and a halving pass's
+ * encounter ends it only when the halving pass before it saw one too */
+static int enc_confirm = 0;
+void rvo_study_set_enc_confirm(int r) { enc_confirm = r; }
+/* (study, scripts/probe/cut_guard_study.py: the cut guard's factor; < 0 = CUT_ECC_FACTOR, 0 = no guard) */
+static double study_cut_factor = -1.0;
+void rvo_study_set_cut_factor(double f) { study_cut_factor = f; }
+/* (study: past the guard, the bound after the extension chi2 - min(k d, 100 est) instead of chi2 - 100 est; 0 = off) */
+static double study_guard_k = 0.0;
+void rvo_study_set_guard_k(double k) { study_guard_k = k; }
 
 static double lb_of(double chi2, double d, double est_raw) {
     const double b = chi2 - fmin(d, CUT_EST_FACTOR * est_raw);
@@ -1099,8 +1113,9 @@ static void dir_main(const rvo_plan_ctx* X, rvo_dir* D) {
         /* (round 5) adaptive: an encounter only a coarser level sees does not end the walker -- the
          * coarse levels' positions near a close approach are the least accurate -- the direction is
          * refined instead, its main pass treated like a non-finite one (rvm_logl.hip `cenc`) */
-        if (s == RVO_ENCOUNTER && X->adaptive && k != kf) {
+        if (s == RVO_ENCOUNTER && X->adaptive && (k != kf || enc_confirm)) {
             coarse = 1;
+            D->pend = 1;
             continue;
         }
         if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
@@ -1154,6 +1169,10 @@ static void dir_extend(const rvo_plan_ctx* X, rvo_dir* D) {
     D->stage = 1;
     double* lx = D->lv0 + (size_t)X->nl * D->cnt;
     const int sx = wh_direction(X->np, X->pl, X->hill_factor, D->at, D->cnt, D->sign, X->dt, X->ext_mult, lx);
+    if (sx == RVO_ENCOUNTER && enc_confirm >= 3) {
+        D->pend = 1; /* (study) */
+        return;
+    }
     if (sx == RVO_ENCOUNTER) {
         D->st = sx;
         D->open = 0;
@@ -1188,6 +1207,7 @@ static void dir_extend(const rvo_plan_ctx* X, rvo_dir* D) {
         }
         if (margin_of(e2, X->e2_cut) < D->margin) D->margin = margin_of(e2, X->e2_cut);
         if (e2 <= X->e2_cut) D->lb = lb_of(c5, dd, D->est_raw);
+        else if (study_guard_k > 0.0) D->lb = lb_of(c5, study_guard_k * dd, D->est_raw);
     } else {
         D->lb = lb_of(c5, dd, D->est_raw);
     }
@@ -1202,11 +1222,21 @@ static void dir_halve(const rvo_plan_ctx* X, rvo_dir* D, int rf) {
                                    D->lv + (size_t)k * D->cnt);
         if (s != RVO_OK && (st == RVO_OK || s == RVO_ENCOUNTER)) st = s;
     }
+    if (st == RVO_ENCOUNTER && rf < X->rf_max &&
+        ((enc_confirm == 2 && !D->pend) || (enc_confirm == 4 && D->pend != 2))) {
+        D->pend = 2; /* (study: a finer pass must confirm it) */
+        D->chi2 = D->est = D->est_raw = NAN;
+        D->lb = 0.0;
+        D->pest = INFINITY;
+        for (int i = 0; i < D->cnt; i++) D->prev[i] = NAN;
+        return;
+    }
     if (st == RVO_ENCOUNTER) {
         D->st = st;
         D->open = 0;
         return;
     }
+    D->pend = 0;
     if (st != RVO_OK) { /* a non-finite halving pass ends the walker (round 5, ADVICE r4: refining on */
         D->st = RVO_NONFINITE; /* would run the last pass at 2^rf_max x the base steps) */
         D->open = 0;
@@ -1309,7 +1339,7 @@ int rvo_logl_whx_adapt(int np, const double* pl, int has_hk, int has_inc, double
     X.npoints = npoints;
     X.ecc_guard = ecc_guard;
     {
-        const double ec = 1.0 - (1.0 - ecc_guard) * CUT_ECC_FACTOR;
+        const double ec = 1.0 - (1.0 - ecc_guard) * (study_cut_factor >= 0.0 ? study_cut_factor : CUT_ECC_FACTOR);
         X.e2_cut = ecc_guard > 0.0 ? ec * ec : INFINITY;
     }
     X.nl = nl;

@@ -650,8 +650,10 @@ int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e) {
     if (std::isnan(e) || e >= 1.0) return fail(-1, "rvm_plan_set_verify_eccentricity: e must be < 1 (<= 0: off)");
     plan->dev.e2_guard = e > 0.0 ? e * e : INFINITY;
     {
-        const double ec = 1.0 - (1.0 - e) * rvm::RVM_CUT_ECC_FACTOR;
-        plan->dev.e2_cut = e > 0.0 ? ec * ec : INFINITY;
+        const char* cf = getenv("RVM_CUT_FACTOR");  // (A/B knob: the guard's factor)
+        const double ec = 1.0 - (1.0 - e) * (cf ? atof(cf) : rvm::RVM_CUT_ECC_FACTOR);
+        const char* cg = getenv("RVM_CUT_GUARD");  // (A/B knob: 0 turns the cut guard off)
+        plan->dev.e2_cut = e > 0.0 && !(cg && atoi(cg) == 0) ? ec * ec : INFINITY;
     }
     return 0;
 }
