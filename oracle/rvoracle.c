@@ -1095,6 +1095,9 @@ void rvo_study_set_cut_factor(double f) { study_cut_factor = f; }
 /* (study: past the guard, the bound after the extension chi2 - min(k d, 100 est) instead of chi2 - 100 est; 0 = off) */
 static double study_guard_k = 0.0;
 void rvo_study_set_guard_k(double k) { study_guard_k = k; }
+/* (study: past the guard, pass 1's change d2 measured against the extension's RV, not the main pass's) */
+static int study_prev_ext = 0;
+void rvo_study_set_prev_ext(int on) { study_prev_ext = on; }
 
 static double lb_of(double chi2, double d, double est_raw) {
     const double b = chi2 - fmin(d, CUT_EST_FACTOR * est_raw);
@@ -1208,6 +1211,12 @@ static void dir_extend(const rvo_plan_ctx* X, rvo_dir* D) {
         if (margin_of(e2, X->e2_cut) < D->margin) D->margin = margin_of(e2, X->e2_cut);
         if (e2 <= X->e2_cut) D->lb = lb_of(c5, dd, D->est_raw);
         else if (study_guard_k > 0.0) D->lb = lb_of(c5, study_guard_k * dd, D->est_raw);
+        if (e2 > X->e2_cut && study_prev_ext) /* (study: pass 1's change measured against the extension) */
+            for (int i = 0; i < D->cnt; i++) {
+                double r5 = X->w5[X->nl] * lx[i];
+                for (int k = 0; k < X->nl; k++) r5 += X->w5[k] * D->lv0[(size_t)k * D->cnt + i];
+                D->prev[i] = r5;
+            }
     } else {
         D->lb = lb_of(c5, dd, D->est_raw);
     }

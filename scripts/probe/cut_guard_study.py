@@ -7,7 +7,8 @@ runs the adaptive restatement with the sampler's accept inputs (the cut on) for 
 reference's (beyond MARGIN of it, same status), walker-directions cut, the stages reached (the
 refinement work), and the three walkers of tests/golden/cut_guard_walkers.json.
 usage: cut_guard_study.py [iterations] [factors, comma-separated] [k: past the guard the bound after
-the extension is chi2 - min(k d, 100 est); 0 = chi2 - 100 est] [systems] -> JSON lines."""
+the extension is chi2 - min(k d, 100 est); 0 = chi2 - 100 est] [systems] [1: past the guard, pass 1's
+change is measured against the extension's RV instead of the main pass's] -> JSON lines."""
 import ctypes as C
 import json
 import os
@@ -31,10 +32,12 @@ def main():
     factors = [float(f) for f in (sys.argv[2] if len(sys.argv) > 2 else "0,0.6712,0.5,0.4,0.3").split(",")]
     gk = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0  # past the guard: chi2 - min(gk d, 100 est)
     systems = sys.argv[4].split(",") if len(sys.argv) > 4 else ["hd155358", "3planet", "s2"]
+    prev_ext = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # past the guard, pass 1's change against the extension
     L = O.lib()
     L.rvo_study_set_cut_factor.argtypes = [C.c_double]
     L.rvo_study_set_guard_k.argtypes = [C.c_double]
     L.rvo_study_set_guard_k(gk)
+    L.rvo_study_set_prev_ext(prev_ext)
     nt = IP.n_threads()
     with open(os.path.join(GOLDEN, "cut_guard_walkers.json")) as f:
         fixture = json.load(f)["walkers"]
@@ -81,7 +84,7 @@ def main():
                 acc = ~cut.any(axis=1) & ((dim - 1.0) * np.log(Z) + lo - L0 > np.log(U))
             bad = np.nonzero((acc != acc_ref) & ~near & (st == sq))[0]
             ec = 1.0 - (1.0 - guard) * f
-            row = {"system": name, "factor": f, "guard_k": gk, "e_cut": ec if f > 0 else None, "proposals": int(len(P)),
+            row = {"system": name, "factor": f, "guard_k": gk, "prev_ext": prev_ext, "e_cut": ec if f > 0 else None, "proposals": int(len(P)),
                    "decisions_differing": int(len(bad)), "differing_e": [round(float(e[i]), 3) for i in bad],
                    "walkers_cut": int(cut.any(axis=1).sum()), "guarded_walkers": int((e > ec).sum()) if f > 0 else 0,
                    "direction_stages_sum": int(stage.sum()),
@@ -100,6 +103,7 @@ def main():
             print(json.dumps(row), flush=True)
     L.rvo_study_set_cut_factor(-1.0)
     L.rvo_study_set_guard_k(0.0)
+    L.rvo_study_set_prev_ext(0)
 
 
 if __name__ == "__main__":
