@@ -1092,8 +1092,13 @@ void rvo_study_set_enc_confirm(int r) { enc_confirm = r; }
 /* (study, scripts/probe/cut_guard_study.py: the cut guard's factor; < 0 = CUT_ECC_FACTOR, 0 = no guard) */
 static double study_cut_factor = -1.0;
 void rvo_study_set_cut_factor(double f) { study_cut_factor = f; }
-/* (study: past the guard, the bound after the extension chi2 - min(k d, 100 est) instead of chi2 - 100 est; 0 = off) */
-static double study_guard_k = 0.0;
+/* past the cut guard the bound after the extension is chi2 - min(CUT_GUARD_K d, 100 est) (rvm_internal.h
+ * RVM_CUT_GUARD_K): the three wrong cuts of tests/test_cut_guard.py had d a third of the error; the study
+ * setter overrides it (0 = chi2 - 100 est, the first form of the guard) */
+#ifndef CUT_GUARD_K
+#define CUT_GUARD_K 10.0
+#endif
+static double study_guard_k = CUT_GUARD_K;
 void rvo_study_set_guard_k(double k) { study_guard_k = k; }
 /* (study: past the guard, pass 1's change d2 measured against the extension's RV, not the main pass's) */
 static int study_prev_ext = 0;
@@ -1210,7 +1215,7 @@ static void dir_extend(const rvo_plan_ctx* X, rvo_dir* D) {
         }
         if (margin_of(e2, X->e2_cut) < D->margin) D->margin = margin_of(e2, X->e2_cut);
         if (e2 <= X->e2_cut) D->lb = lb_of(c5, dd, D->est_raw);
-        else if (study_guard_k > 0.0) D->lb = lb_of(c5, study_guard_k * dd, D->est_raw);
+        else if (study_guard_k > 0.0) D->lb = lb_of(c5, study_guard_k * dd, D->est_raw); /* (CUT_GUARD_K) */
         if (e2 > X->e2_cut && study_prev_ext) /* (study: pass 1's change measured against the extension) */
             for (int i = 0; i < D->cnt; i++) {
                 double r5 = X->w5[X->nl] * lx[i];

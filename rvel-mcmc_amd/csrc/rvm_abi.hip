@@ -450,6 +450,7 @@ int rvm_plan_create(const rvm_config* cfg, const double* t, const double* rv, co
     }
     P.e2_guard = INFINITY;
     P.e2_cut = INFINITY;
+    P.cut_guard_k = 0.0;
     P.lvx_emax = 0;
     P.lvx_stride = 0;
     P.ext_spec = 0;
@@ -654,6 +655,8 @@ int rvm_plan_set_verify_eccentricity(rvm_plan* plan, double e) {
         const double ec = 1.0 - (1.0 - e) * (cf ? atof(cf) : rvm::RVM_CUT_ECC_FACTOR);
         const char* cg = getenv("RVM_CUT_GUARD");  // (A/B knob: 0 turns the cut guard off)
         plan->dev.e2_cut = e > 0.0 && !(cg && atoi(cg) == 0) ? ec * ec : INFINITY;
+        const char* ck = getenv("RVM_CUT_GUARD_K");  // (A/B knob: past the guard, chi2 - min(k d, 100 est))
+        plan->dev.cut_guard_k = ck ? atof(ck) : rvm::RVM_CUT_GUARD_K;
     }
     return 0;
 }

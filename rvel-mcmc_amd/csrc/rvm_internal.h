@@ -43,6 +43,9 @@ constexpr double RVM_FLOOR_BOUND = 4.0;
 // proposals in 24576 cut that IAS15 accepts, scripts/probe/decision_mismatch_probe.py), so its bound
 // stays the main pass's (chi2 - 100 est); oracle/rvoracle.c CUT_ECC_FACTOR
 constexpr double RVM_CUT_ECC_FACTOR = 0.6712;
+// past the cut guard the bound after the extension is chi2 - min(K d, 100 est), K = RVM_CUT_GUARD_K
+// (the three wrong cuts had the extension's change d a third of the error); oracle CUT_GUARD_K
+constexpr double RVM_CUT_GUARD_K = 10.0;
 // launches of fewer walkers than this run the extension after the main pass (only when a walker is
 // flagged) instead of as a concurrent fifth wave of the one-group-per-block layout (launch_logl_t)
 constexpr int RVM_CX_MIN_WALKERS = 32;
@@ -124,6 +127,7 @@ struct DevPlan {
     // ... and above this e^2 (from the guard: RVM_CUT_ECC_FACTOR) the extension's change gives no
     // lower bound for the certain-reject cut (+inf: always)
     double e2_cut;
+    double cut_guard_k;  // past the cut guard: chi2 - min(k d, 100 est) (RVM_CUT_GUARD_K; 0: chi2 - 100 est)
     int32_t lvx_emax, lvx_stride;
     // walkers handed from the likelihood kernel to the refinement kernel (rvm_refine.hip): a walker
     // with a direction still open after the main pass and the extension (and no certain reject) is

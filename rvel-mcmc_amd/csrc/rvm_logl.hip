@@ -972,7 +972,8 @@ void logl_kernel(const DevPlan P, const int W,
                         extend_stage(lvl, grp, d, need, chi2w, enc, c5x, ddx);
                 }
                 // (the extension's bound only below the cut guard, DevPlan::e2_cut)
-                lbw = cenc ? 0.0 : direction_lb(need, chi2, est, need0 && P.ext_mult > 0 && e2c <= P.e2_cut, c5x, ddx);
+                lbw = cenc ? 0.0 : direction_lb(need, chi2, est, need0 && P.ext_mult > 0 && (e2c <= P.e2_cut || P.cut_guard_k > 0.0), c5x,
+                                                   e2c <= P.e2_cut ? ddx : P.cut_guard_k * ddx);
             }
         }
         if (cmb && wo < W) {
@@ -1282,7 +1283,8 @@ void logl_kernel(const DevPlan P, const int W,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 double xc5 = 0.0, xdd = 0.0;
                 extend_pass(ul, d, nm, nd, c2, en, xc5, xdd);
-                const double lb = cn ? 0.0 : direction_lb(nd, cm, es, (f & 16) != 0 && (f & 64) == 0, xc5, xdd);
+                const double lb = cn ? 0.0 : direction_lb(nd, cm, es, (f & 16) != 0 && ((f & 64) == 0 || P.cut_guard_k > 0.0), xc5,
+                                                                 (f & 64) != 0 ? P.cut_guard_k * xdd : xdd);
                 if (cl) finish_recompute(w0 + lane, c2, en, nd, lb);
             } else if (valid && pl_idx == 0) {
                 if (lsx && need) {  // the main pass's RV of an open direction (the ring, consume above)
@@ -1291,7 +1293,8 @@ void logl_kernel(const DevPlan P, const int W,
                         P.rvp[(size_t)(d * P.lvx_emax + e) * P.lvx_stride + w] = cenc ? __builtin_nan("") : rg[(size_t)e * WPB];
                 }
                 finish_recompute(w, chi2w, enc, need,
-                                 cenc ? 0.0 : direction_lb(need, chi2m, est, lsx && need0 && e2w <= P.e2_cut, c5x, ddx));
+                                 cenc ? 0.0 : direction_lb(need, chi2m, est, lsx && need0 && (e2w <= P.e2_cut || P.cut_guard_k > 0.0), c5x,
+                                                          e2w <= P.e2_cut ? ddx : P.cut_guard_k * ddx));
             }
 #ifdef RVM_PROFILE
             prof_dec(rt_arr, nl - 1);

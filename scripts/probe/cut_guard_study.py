@@ -30,7 +30,7 @@ from rvmcmc.state import State  # noqa: E402
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     factors = [float(f) for f in (sys.argv[2] if len(sys.argv) > 2 else "0,0.6712,0.5,0.4,0.3").split(",")]
-    gk = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0  # past the guard: chi2 - min(gk d, 100 est)
+    gk = float(sys.argv[3]) if len(sys.argv) > 3 else 10.0  # past the guard: chi2 - min(gk d, 100 est)
     systems = sys.argv[4].split(",") if len(sys.argv) > 4 else ["hd155358", "3planet", "s2"]
     prev_ext = int(sys.argv[5]) if len(sys.argv) > 5 else 0  # past the guard, pass 1's change against the extension
     L = O.lib()
@@ -102,7 +102,7 @@ def main():
                 row["fixture_walkers_accepted"] = ok
             print(json.dumps(row), flush=True)
     L.rvo_study_set_cut_factor(-1.0)
-    L.rvo_study_set_guard_k(0.0)
+    L.rvo_study_set_guard_k(10.0)
     L.rvo_study_set_prev_ext(0)
 
 

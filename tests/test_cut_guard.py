@@ -5,8 +5,8 @@ At HD155358's steady state with 2048 walkers three stretch proposals in 24576 we
 cut right after the extension although IAS15 accepts them (scripts/probe/decision_mismatch_probe.py):
 their outer planets have e = 0.79-0.84, the plan's levels and the extension are far from resolving
 their pericentre passages, and the extension's change (a third of the error) was taken as the bound.
-Past the cut guard the bound stays the main pass's (chi2 - 100 est), so those walkers refine to the
-tolerance and take the reference's decision."""
+Past the cut guard the bound after the extension is chi2 - min(10 d, 100 est) (CUT_GUARD_K), not
+chi2 - min(d, 100 est), so those walkers refine to the tolerance and take the reference's decision."""
 import json
 import os
 
